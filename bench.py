@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Benchmark: Kepler power attribution on MI355X (BASELINE.json metric).
+
+One *step* = one collection interval (PowerMonitor.calculatePower,
+internal/monitor/monitor.go:399-431) over the whole fleet shard of a GPU:
+node split + segmented CPU-time sums + process/container/VM/pod attribution
+(one kacc_run_interval launch) followed by the cluster namespace totals
+(kacc_namespace_totals, then an RCCL all-reduce across GPUs when N > 1).
+
+Workload: BASELINE config 3 per GPU — 10k nodes x 2k processes, Z = 4 RAPL
+zones (package/core/uncore/dram), ~1.6k container processes / 200 containers /
+71 pods / 20 VMs per node, synthetic inputs (kepler_amd/fleet.py) resident in
+HBM before timing.  Scaling is weak: every rank owns its own 10k-node shard
+(node snapshots are independent), so N GPUs process N x 20M process rows per
+interval; only the namespace totals cross GPUs.
+
+Prints ONE JSON line on rank 0.  Launch with N > 1 as
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+METRIC = "process attributions/sec + achieved HBM GB/s, 10k-node fleet, 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--nodes", type=int, default=None, help="override nodes per GPU")
+    ap.add_argument("--distinct", type=int, default=4, help="distinct process-input sets cycled")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-nodes", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--node-order", action="store_true", help="launch heaviest nodes first")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds):
+    """Go-faithful oracle (C++ restatement with Go's data structures), 1 thread."""
+    from kepler_amd import fleet
+    from oracle.oracle import GoFaithful, Oracle
+
+    nodes = np.arange(min(n_nodes, layout.n_nodes))
+    subs = [fleet.subset_interval(a, nodes, layout.zones) for a in intervals]
+    _, sizes, _ = subs[0]
+    caps = dict(nodes=sizes["n_nodes"], proc_slots=sizes["n_procs"], ctr_slots=sizes["n_ctrs"],
+                vm_slots=sizes["n_vms"], pod_slots=sizes["n_pods"])
+    out = {}
+    for name, cls in (("gofaithful", GoFaithful), ("soa", Oracle)):
+        o = cls(layout.zones, **caps)
+        o.interval(subs[0][0], sizes)  # first read (untimed, as on the GPU)
+        done, t_run, k = 0, 0.0, 0
+        budget = seconds if name == "gofaithful" else min(seconds, 5.0)
+        while t_run < budget:
+            a = dict(subs[1 + k % (len(subs) - 1)][0])
+            na = node_steps[k % len(node_steps)]
+            for key in ("node_ts_ns", "node_usage_ratio", "node_status"):
+                a[key] = np.ascontiguousarray(na[key][nodes])
+            zidx = (nodes[:, None] * layout.zones + np.arange(layout.zones)).reshape(-1)
+            a["zone_energy"] = np.ascontiguousarray(na["zone_energy"][zidx])
+            t0 = time.perf_counter()
+            o.interval(a, sizes)
+            t_run += time.perf_counter() - t0
+            done += sizes["n_procs"]
+            k += 1
+        out[name] = dict(value=done / t_run, intervals=k, seconds=t_run)
+    return out, sizes
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from kepler_amd import accel, fleet
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+    t_setup = time.time()
+    nodes = args.nodes or {2: 1000, 3: 10000, 5: 1000}[args.config]
+    layout = fleet.config_layout(args.config, seed=fleet.SEED + 7919 * rank, nodes=nodes)
+    sim = fleet.FleetSim(layout, seed=fleet.SEED + 7919 * rank)
+    Z = layout.zones
+    sizes = layout.sizes()
+    log(rank, f"[bench] layout {sizes} Z={Z} built in {time.time() - t_setup:.1f}s")
+
+    n_steps = args.warmup + args.steps
+    n_distinct = max(1, min(args.distinct, n_steps))
+    prime = sim.next_interval()  # first read (monitor.go:326-330), untimed
+    full = [sim.next_interval() for _ in range(n_distinct)]
+    node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_steps)]
+    log(rank, f"[bench] inputs generated in {time.time() - t_setup:.1f}s")
+
+    acc = accel.Accel(Z, **layout.capacities(), device=local)
+    stream = current_stream_handle()
+    statics = to_device(layout.static_arrays())
+    dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
+                for a in full]
+    node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")
+    dev_nodes = [to_device({k: a[k] for k in node_keys}) for a in node_steps]
+    order = to_device({"o": layout.node_order_heaviest_first()})["o"] if args.node_order else None
+
+    def make(k):
+        t = dict(statics)
+        t.update(dev_full[k % n_distinct])
+        t.update(dev_nodes[k])
+        if order is not None:
+            t["node_order"] = order
+        return t
+
+    step_tensors = [make(k) for k in range(n_steps)]
+    step_ivs = [interval_from_tensors(t, sizes) for t in step_tensors]
+    prime_t = to_device(prime)
+    acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
+    acc.sync(stream)
+    del prime_t
+
+    ns_off, ns_slot = layout.namespace_csr()
+    ns_t = to_device({"off": ns_off, "slot": ns_slot})
+    n_ns = len(ns_off) - 1
+    ns_e = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
+    ns_p = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
+
+    def step(k, ev=None):
+        if ev is not None:
+            ev[0].record()
+        acc.run_interval(step_ivs[k], stream)
+        if ev is not None:
+            ev[1].record()
+        acc.namespace_totals(n_ns, ns_t["off"].data_ptr(), ns_t["slot"].data_ptr(), ns_e.data_ptr(),
+                             ns_p.data_ptr(), stream)
+        if world > 1:  # cluster-wide namespace totals over xGMI (RCCL): u64 sum is exact
+            dist.all_reduce(ns_e)
+            dist.all_reduce(ns_p)
+
+    for k in range(args.warmup):
+        step(k)
+    acc.sync(stream)
+    torch.cuda.synchronize()
+    log(rank, f"[bench] warmup done, setup {time.time() - t_setup:.1f}s")
+
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    acc.sync(stream)  # surfaces any device-detected range error
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+
+    wall_t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+    procs_t = torch.tensor([sizes["n_procs"], sizes["n_nodes"]], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(procs_t)
+    wall_max = float(wall_t.item())
+    total_procs, total_nodes = (float(x) for x in procs_t.tolist())
+
+    bytes_per_launch = accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
+                                            sizes["n_vms"], sizes["n_pods"])
+    k_avg_ms = float(np.mean(kernel_ms))
+    achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
+
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pmc = json.load(f)
+        ent = pmc.get(f"config{args.config}")
+        if ent and ent.get("n_procs") == sizes["n_procs"]:
+            traffic = ent.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": METRIC,
+        "value": total_procs * args.steps / wall_max,
+        "unit": "proc-attr/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall_max * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64+u64",
+        "data": "synthetic (kepler_amd/fleet.py, seed 0x4B45504C; inputs resident in HBM)",
+        "config": {
+            "workload": f"config{args.config}: {sizes['n_nodes']} nodes x "
+                        f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs, Z={Z} per GPU",
+            "nodes_per_gpu": sizes["n_nodes"],
+            "procs_per_gpu": sizes["n_procs"],
+            "containers_per_gpu": sizes["n_ctrs"],
+            "vms_per_gpu": sizes["n_vms"],
+            "pods_per_gpu": sizes["n_pods"],
+            "zones": Z,
+            "namespaces": n_ns,
+            "parallelism": f"node-sharded x{world} (namespace totals all-reduced over RCCL)",
+        },
+        "node_snapshots_per_s": total_nodes * args.steps / wall_max,
+        "kernel_ms": k_avg_ms,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch,
+            "kernel": "kacc::interval_kernel<4>",
+        },
+        "cpu_baseline": None,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res, cs = cpu_baseline(layout, [prime] + full, node_steps, args.cpu_nodes, args.cpu_seconds)
+        gf = res["gofaithful"]
+        result["cpu_baseline"] = {
+            "value": gf["value"],
+            "unit": "proc-attr/s",
+            "cores": 1,
+            "kind": "port",
+            "sample": f"go-faithful C++ restatement of the Go path (oracle/kor_gf_interval: string-keyed "
+                      f"maps, per-object zone maps), first {cs['n_nodes']} nodes of the same fleet "
+                      f"({cs['n_procs']} procs, Z={Z}), {gf['intervals']} intervals in {gf['seconds']:.1f}s",
+            "soa_port_1thread": res["soa"]["value"],
+        }
+        result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
+
+    if rank == 0:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    acc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

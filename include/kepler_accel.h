@@ -1,0 +1,236 @@
+/*
+ * kepler_accel.h — C ABI of the MI355X power-attribution engine.
+ *
+ * This is the drop-in boundary for Kepler's attribution hot path.  In the
+ * reference the computation is private to PowerMonitor:
+ *
+ *   internal/monitor/monitor.go:399-431  PowerMonitor.calculatePower
+ *     -> node.go:10-84      calculateNodePower   (+ node.go:87-98 calculateEnergyDelta,
+ *                                                   node.go:101-131 firstNodeRead)
+ *     -> resource/informer.go:349-410 Refresh    (segmented CPU-time sums:
+ *                                                   informer.go:223-249/469-489 containers,
+ *                                                   informer.go:275-326/491-510 pods,
+ *                                                   informer.go:251-273/433-449 VMs,
+ *                                                   informer.go:328-345 node total)
+ *     -> process.go:79-161  calculateProcessPower
+ *     -> container.go:71-153 calculateContainerPower
+ *     -> vm.go:46-121       calculateVMPower
+ *     -> pod.go:46-131      calculatePodPower
+ *
+ * The Go side (device zone readers, procfs informer, PowerMonitor snapshot
+ * orchestration, exporters) is kept.  A cgo package internal/accel (see
+ * INTEGRATION.md) packs one interval for a whole fleet of nodes into the
+ * structure-of-arrays batch below and calls kacc_run_interval(); the results
+ * land in device-resident state tables indexed by node and by workload slot,
+ * which the shim reads back into monitor.Snapshot.
+ *
+ * Units follow internal/device/energy.go: energy is uint64 micro-joules
+ * (energy.go:14), power is float64 micro-watts (energy.go:41).  Arithmetic
+ * follows Go on amd64 exactly: uint64 modular add/sub, float64 IEEE with no
+ * FMA contraction, float64->uint64 conversion with Go's amd64 semantics,
+ * time.Duration.Seconds() for the interval length.
+ *
+ * All functions return 0 on success and a negative KACC_E* code on failure;
+ * kacc_last_error() gives the message.  Every entry point calls
+ * hipSetDevice(ctx device) first, so calls may come from any OS thread (cgo);
+ * calls on one context must be serialised by the caller (the reference
+ * serialises calculatePower with singleflight, monitor.go:265-302).
+ */
+#ifndef KEPLER_ACCEL_H
+#define KEPLER_ACCEL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KACC_ABI_VERSION 1u
+#define KACC_MAX_ZONES 8u
+
+/* Status codes. */
+#define KACC_OK 0
+#define KACC_EINVAL (-1)  /* bad argument / shape */
+#define KACC_EHIP (-2)    /* HIP runtime error */
+#define KACC_ENOMEM (-3)  /* device or pinned allocation failed */
+#define KACC_ERANGE (-4)  /* device detected an out-of-range index in a batch */
+#define KACC_ESTATE (-5)  /* call not valid in the current state */
+
+/* Slot words: bits 0..30 index a workload slot table, bit 31 marks a workload
+ * that has no previous snapshot entry (first time its ID is seen; the Go code
+ * then uses the interval energy alone, process.go:133-138).                   */
+#define KACC_SLOT_NEW 0x80000000u
+#define KACC_SLOT_MASK 0x7fffffffu
+
+/* node_status bits (input). */
+#define KACC_NODE_READ_ERROR 0x1u /* a zone read failed: node.go:39-44 -> the whole
+                                      interval fails and the previous snapshot is
+                                      kept (monitor.go:328-335)                   */
+/* node_status_out values (state table). */
+#define KACC_NODE_OK 0u
+#define KACC_NODE_FIRST_READ 1u /* firstReading path, monitor.go:366-397 */
+#define KACC_NODE_SKIPPED 2u    /* read error: state left untouched      */
+
+/* kacc_interval.flags */
+#define KACC_F_NODE_CPU_DELTA_GIVEN 0x1u /* use node_cpu_delta[] instead of the
+                                             on-device sum (mock informers)     */
+
+typedef struct kacc_ctx kacc_ctx;
+
+typedef struct kacc_config {
+  uint32_t zones;       /* Z: RAPL zones per node, 1..KACC_MAX_ZONES         */
+  uint32_t reserved0;
+  uint64_t nodes;       /* node state capacity; node i of a batch is node i  */
+  uint64_t proc_slots;  /* workload slot-table capacities                    */
+  uint64_t ctr_slots;
+  uint64_t vm_slots;
+  uint64_t pod_slots;
+} kacc_config;
+
+/* One collection interval for the whole fleet.  Layout rules (checked by
+ * kacc_validate_host; the kernel additionally clamps every index so a bad
+ * batch cannot fault the GPU, it raises KACC_ERANGE instead):
+ *
+ *  - node n owns process rows [proc_off[n], proc_off[n+1]), containers
+ *    [ctr_off[n], ctr_off[n+1]), VMs [vm_off[n], vm_off[n+1]) and pods
+ *    [pod_off[n], pod_off[n+1]);
+ *  - inside a node the rows are ordered: container processes grouped by
+ *    container (in /proc listing order inside each container), then VM
+ *    processes grouped by VM, then every other process;
+ *  - container c owns rows [begin, ctr_proc_end[c]) where begin is
+ *    proc_off[n] for the node's first container, else ctr_proc_end[c-1];
+ *  - VM v owns rows [begin, vm_proc_end[v]) where begin is the end of the
+ *    node's container rows for its first VM, else vm_proc_end[v-1];
+ *  - containers are grouped by pod; pod q owns containers
+ *    [begin, pod_ctr_end[q]) with begin = ctr_off[n] for the node's first pod,
+ *    else pod_ctr_end[q-1]; containers without a pod follow the pods.
+ *
+ * In kacc_run_interval every pointer is a DEVICE pointer; in the host batch
+ * path (kacc_batch_*) they are pinned host pointers owned by the library.  */
+typedef struct kacc_interval {
+  uint32_t n_nodes, n_procs, n_ctrs, n_vms, n_pods;
+  uint32_t flags;
+  /* nodes [n_nodes] */
+  const int64_t *node_ts_ns;      /* clock.Now() of this read, monotonic ns (node.go:15) */
+  const double *node_usage_ratio; /* resources.Node().CPUUsageRatio as read before
+                                     Refresh (node.go:25): the lagged ratio          */
+  const uint32_t *node_status;    /* KACC_NODE_* bits, may be NULL                    */
+  const double *node_cpu_delta;   /* ProcessTotalCPUTimeDelta override (flags)        */
+  const uint32_t *node_order;     /* optional launch order (heaviest first), NULL=id  */
+  /* zones [n_nodes * Z], node-major */
+  const uint64_t *zone_energy;    /* EnergyZone.Energy()   (cpu_power_meter.go:22) */
+  const uint64_t *zone_max;       /* EnergyZone.MaxEnergy() (cpu_power_meter.go:26) */
+  /* per-node CSR offsets [n_nodes + 1] */
+  const uint32_t *proc_off;
+  const uint32_t *ctr_off;
+  const uint32_t *vm_off;
+  const uint32_t *pod_off;
+  /* processes [n_procs] */
+  const double *proc_cpu_delta;   /* resource.Process.CPUTimeDelta (informer.go:518) */
+  const uint32_t *proc_slot;      /* slot word                                        */
+  /* containers [n_ctrs] */
+  const uint32_t *ctr_proc_end;
+  const uint32_t *ctr_slot;
+  /* virtual machines [n_vms] */
+  const uint32_t *vm_proc_end;
+  const uint32_t *vm_slot;
+  /* pods [n_pods] */
+  const uint32_t *pod_ctr_end;
+  const uint32_t *pod_slot;
+} kacc_interval;
+
+/* Device-resident state / result tables.  [n*Z+z] tables are node-major or
+ * slot-major with the zone innermost.  After kacc_run_interval they hold the
+ * new snapshot: node zones = monitor.NodeUsage (types.go:27-40), workload
+ * zones = monitor.Usage (types.go:44-47).                                     */
+typedef enum kacc_table {
+  KACC_T_NODE_ENERGY_TOTAL = 0, /* u64 [N*Z] NodeUsage.EnergyTotal          */
+  KACC_T_NODE_ACTIVE_ENERGY,    /* u64 [N*Z] NodeUsage.activeEnergy (interval) */
+  KACC_T_NODE_ACTIVE_TOTAL,     /* u64 [N*Z] NodeUsage.ActiveEnergyTotal    */
+  KACC_T_NODE_IDLE_TOTAL,       /* u64 [N*Z] NodeUsage.IdleEnergyTotal      */
+  KACC_T_NODE_POWER,            /* f64 [N*Z] NodeUsage.Power                */
+  KACC_T_NODE_ACTIVE_POWER,     /* f64 [N*Z] NodeUsage.ActivePower          */
+  KACC_T_NODE_IDLE_POWER,       /* f64 [N*Z] NodeUsage.IdlePower            */
+  KACC_T_NODE_TS,               /* i64 [N]   Node.Timestamp (last good read) */
+  KACC_T_NODE_HAS_PREV,         /* u32 [N]   1 once a snapshot exists        */
+  KACC_T_NODE_USAGE_RATIO,      /* f64 [N]   Node.UsageRatio                 */
+  KACC_T_NODE_CPU_DELTA,        /* f64 [N]   ProcessTotalCPUTimeDelta used   */
+  KACC_T_NODE_STATUS,           /* u32 [N]   KACC_NODE_OK/FIRST_READ/SKIPPED */
+  KACC_T_PROC_ENERGY,           /* u64 [Sp*Z] Process Usage.EnergyTotal      */
+  KACC_T_PROC_POWER,            /* f64 [Sp*Z] Process Usage.Power            */
+  KACC_T_CTR_ENERGY,            /* u64 [Sc*Z]                                */
+  KACC_T_CTR_POWER,             /* f64 [Sc*Z]                                */
+  KACC_T_CTR_CPU_DELTA,         /* f64 [Sc]  resource.Container.CPUTimeDelta */
+  KACC_T_CTR_CPU_TOTAL,         /* f64 [Sc]  resource.Container.CPUTotalTime */
+  KACC_T_VM_ENERGY,             /* u64 [Sv*Z]                                */
+  KACC_T_VM_POWER,              /* f64 [Sv*Z]                                */
+  KACC_T_VM_CPU_DELTA,          /* f64 [Sv]  resource.VirtualMachine.CPUTimeDelta */
+  KACC_T_POD_ENERGY,            /* u64 [Sq*Z]                                */
+  KACC_T_POD_POWER,             /* f64 [Sq*Z]                                */
+  KACC_T_POD_CPU_DELTA,         /* f64 [Sq]  resource.Pod.CPUTimeDelta       */
+  KACC_T_POD_CPU_TOTAL,         /* f64 [Sq]  resource.Pod.CPUTotalTime       */
+  KACC_T_COUNT
+} kacc_table;
+
+/* ---- context ------------------------------------------------------------ */
+uint32_t kacc_abi_version(void);
+int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out);
+void kacc_destroy(kacc_ctx *ctx);
+const char *kacc_last_error(const kacc_ctx *ctx);
+int kacc_get_config(const kacc_ctx *ctx, kacc_config *out);
+
+/* Zero every state table (fresh PowerMonitor, snapshot == nil). */
+int kacc_reset(kacc_ctx *ctx);
+
+/* ---- the hot path ------------------------------------------------------- */
+/* Run one interval (device pointers) on `stream` (a hipStream_t; NULL = the
+ * context's own stream).  Asynchronous: call kacc_sync() to wait and to
+ * collect device-detected range errors.                                      */
+int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream);
+int kacc_sync(kacc_ctx *ctx, void *stream);
+
+/* Host-side layout check of a batch held in host memory (O(N+C+V+Q+P)). */
+int kacc_validate_host(const kacc_ctx *ctx, const kacc_interval *host_batch);
+
+/* ---- pinned host batch path (what the cgo shim uses) -------------------- */
+typedef struct kacc_batch kacc_batch;
+/* Allocates pinned host arrays for a batch of the given sizes.  *view points
+ * at the batch's own descriptor: its arrays are writable pinned host memory
+ * (cast away const) that the caller fills; the caller may also set `flags`
+ * and set the optional node_status / node_cpu_delta / node_order to NULL.   */
+int kacc_batch_alloc(kacc_ctx *ctx, uint32_t n_nodes, uint32_t n_procs, uint32_t n_ctrs,
+                     uint32_t n_vms, uint32_t n_pods, kacc_batch **out, kacc_interval **view);
+/* Validate, copy H2D and launch on the context stream (asynchronous). */
+int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *batch);
+/* Wait for the batch; afterwards the batch may be refilled and resubmitted. */
+int kacc_batch_wait(kacc_ctx *ctx, kacc_batch *batch);
+void kacc_batch_free(kacc_ctx *ctx, kacc_batch *batch);
+
+/* ---- state access -------------------------------------------------------- */
+/* Element size in bytes and element count of a table. */
+int kacc_table_info(const kacc_ctx *ctx, kacc_table t, uint64_t *elem_bytes, uint64_t *count);
+/* Device pointer of a table (for zero-copy readers on the same device). */
+int kacc_table_device_ptr(kacc_ctx *ctx, kacc_table t, void **dev_ptr);
+/* Synchronous copies of `count` elements starting at element `first`. */
+int kacc_table_download(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host_dst);
+int kacc_table_upload(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const void *host_src);
+
+/* ---- cluster namespace totals (north star: only these cross GPUs) -------- */
+/* Per-namespace sums over pods of this context: ns k owns pod slots
+ * ns_pod_slot[ns_pod_off[k] .. ns_pod_off[k+1]) summed in that order.
+ * out_energy: u64 [n_ns*Z] (modular, exact), out_power: f64 [n_ns*Z].
+ * All pointers are device pointers; asynchronous on `stream`.  The caller
+ * all-reduces the two vectors across GPUs (RCCL sum).                        */
+int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *ns_pod_off,
+                          const uint32_t *ns_pod_slot, uint64_t *out_energy, double *out_power,
+                          void *stream);
+
+/* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
+ * sizes (the roofline numerator).                  */
+uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,
+                             uint64_t n_vms, uint64_t n_pods);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KEPLER_ACCEL_H */

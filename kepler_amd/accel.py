@@ -1,0 +1,381 @@
+"""ctypes binding of the C ABI in include/kepler_accel.h (libkepler_accel.so).
+
+This is the Python twin of the cgo shim described in INTEGRATION.md: the same
+entry points a Go `internal/accel` package binds, used here by the tests and
+the benchmark.  There is no CPU fallback: if the HIP library is missing the
+import of :func:`load` raises, so a GPU run can never pass on a silent
+substitute.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_uint32, c_uint64, c_void_p
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libkepler_accel.so")
+
+KACC_ABI_VERSION = 1
+KACC_MAX_ZONES = 8
+KACC_OK = 0
+KACC_EINVAL = -1
+KACC_EHIP = -2
+KACC_ENOMEM = -3
+KACC_ERANGE = -4
+KACC_ESTATE = -5
+KACC_SLOT_NEW = 0x80000000
+KACC_SLOT_MASK = 0x7FFFFFFF
+KACC_NODE_READ_ERROR = 0x1
+KACC_NODE_OK = 0
+KACC_NODE_FIRST_READ = 1
+KACC_NODE_SKIPPED = 2
+KACC_F_NODE_CPU_DELTA_GIVEN = 0x1
+
+# kacc_table enum, in header order: (name, numpy dtype)
+TABLES = [
+    ("node_energy_total", np.uint64),
+    ("node_active_energy", np.uint64),
+    ("node_active_total", np.uint64),
+    ("node_idle_total", np.uint64),
+    ("node_power", np.float64),
+    ("node_active_power", np.float64),
+    ("node_idle_power", np.float64),
+    ("node_ts", np.int64),
+    ("node_has_prev", np.uint32),
+    ("node_usage_ratio", np.float64),
+    ("node_cpu_delta", np.float64),
+    ("node_status", np.uint32),
+    ("proc_energy", np.uint64),
+    ("proc_power", np.float64),
+    ("ctr_energy", np.uint64),
+    ("ctr_power", np.float64),
+    ("ctr_cpu_delta", np.float64),
+    ("ctr_cpu_total", np.float64),
+    ("vm_energy", np.uint64),
+    ("vm_power", np.float64),
+    ("vm_cpu_delta", np.float64),
+    ("pod_energy", np.uint64),
+    ("pod_power", np.float64),
+    ("pod_cpu_delta", np.float64),
+    ("pod_cpu_total", np.float64),
+]
+TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
+
+# exported symbols, in header order (checked by tests/test_abi.py)
+EXPORTS = [
+    "kacc_abi_version",
+    "kacc_create",
+    "kacc_destroy",
+    "kacc_last_error",
+    "kacc_get_config",
+    "kacc_reset",
+    "kacc_run_interval",
+    "kacc_sync",
+    "kacc_validate_host",
+    "kacc_batch_alloc",
+    "kacc_batch_submit",
+    "kacc_batch_wait",
+    "kacc_batch_free",
+    "kacc_table_info",
+    "kacc_table_device_ptr",
+    "kacc_table_download",
+    "kacc_table_upload",
+    "kacc_namespace_totals",
+    "kacc_interval_bytes",
+]
+
+
+class KaccConfig(ctypes.Structure):
+    _fields_ = [
+        ("zones", c_uint32),
+        ("reserved0", c_uint32),
+        ("nodes", c_uint64),
+        ("proc_slots", c_uint64),
+        ("ctr_slots", c_uint64),
+        ("vm_slots", c_uint64),
+        ("pod_slots", c_uint64),
+    ]
+
+
+# pointer fields of kacc_interval, in header order
+INTERVAL_ARRAYS = [
+    "node_ts_ns",
+    "node_usage_ratio",
+    "node_status",
+    "node_cpu_delta",
+    "node_order",
+    "zone_energy",
+    "zone_max",
+    "proc_off",
+    "ctr_off",
+    "vm_off",
+    "pod_off",
+    "proc_cpu_delta",
+    "proc_slot",
+    "ctr_proc_end",
+    "ctr_slot",
+    "vm_proc_end",
+    "vm_slot",
+    "pod_ctr_end",
+    "pod_slot",
+]
+# the optional ones may be NULL
+OPTIONAL_ARRAYS = {"node_status", "node_cpu_delta", "node_order"}
+ARRAY_DTYPES = {
+    "node_ts_ns": np.int64,
+    "node_usage_ratio": np.float64,
+    "node_status": np.uint32,
+    "node_cpu_delta": np.float64,
+    "node_order": np.uint32,
+    "zone_energy": np.uint64,
+    "zone_max": np.uint64,
+    "proc_off": np.uint32,
+    "ctr_off": np.uint32,
+    "vm_off": np.uint32,
+    "pod_off": np.uint32,
+    "proc_cpu_delta": np.float64,
+    "proc_slot": np.uint32,
+    "ctr_proc_end": np.uint32,
+    "ctr_slot": np.uint32,
+    "vm_proc_end": np.uint32,
+    "vm_slot": np.uint32,
+    "pod_ctr_end": np.uint32,
+    "pod_slot": np.uint32,
+}
+
+
+class KaccInterval(ctypes.Structure):
+    _fields_ = [
+        ("n_nodes", c_uint32),
+        ("n_procs", c_uint32),
+        ("n_ctrs", c_uint32),
+        ("n_vms", c_uint32),
+        ("n_pods", c_uint32),
+        ("flags", c_uint32),
+    ] + [(name, c_void_p) for name in INTERVAL_ARRAYS]
+
+
+class AccelError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"kacc error {code}: {msg}")
+        self.code = code
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libkepler_accel.so (raises if it was not built — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build it with `make -C kepler_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback"
+        )
+    lib = ctypes.CDLL(path)
+    lib.kacc_abi_version.restype = c_uint32
+    lib.kacc_create.argtypes = [c_int, POINTER(KaccConfig), POINTER(c_void_p)]
+    lib.kacc_destroy.argtypes = [c_void_p]
+    lib.kacc_destroy.restype = None
+    lib.kacc_last_error.argtypes = [c_void_p]
+    lib.kacc_last_error.restype = c_char_p
+    lib.kacc_get_config.argtypes = [c_void_p, POINTER(KaccConfig)]
+    lib.kacc_reset.argtypes = [c_void_p]
+    lib.kacc_run_interval.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p]
+    lib.kacc_sync.argtypes = [c_void_p, c_void_p]
+    lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
+    lib.kacc_batch_alloc.argtypes = [
+        c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
+        POINTER(c_void_p), POINTER(POINTER(KaccInterval)),
+    ]
+    lib.kacc_batch_submit.argtypes = [c_void_p, c_void_p]
+    lib.kacc_batch_wait.argtypes = [c_void_p, c_void_p]
+    lib.kacc_batch_free.argtypes = [c_void_p, c_void_p]
+    lib.kacc_batch_free.restype = None
+    lib.kacc_table_info.argtypes = [c_void_p, c_int, POINTER(c_uint64), POINTER(c_uint64)]
+    lib.kacc_table_device_ptr.argtypes = [c_void_p, c_int, POINTER(c_void_p)]
+    lib.kacc_table_download.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
+    lib.kacc_table_upload.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
+    lib.kacc_namespace_totals.argtypes = [
+        c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+    ]
+    lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
+    lib.kacc_interval_bytes.restype = c_uint64
+    if lib.kacc_abi_version() != KACC_ABI_VERSION:
+        raise ImportError("libkepler_accel ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int) -> int:
+    return int(load().kacc_interval_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods))
+
+
+def make_interval(arrays: dict, sizes: dict, flags: int = 0, ptr=None) -> KaccInterval:
+    """Build a kacc_interval from a dict of arrays.
+
+    `ptr(array) -> int` returns the address (numpy: ctypes.data, torch:
+    data_ptr()).  Missing optional arrays become NULL.  The caller keeps the
+    arrays alive while the descriptor is in use.
+    """
+    if ptr is None:
+        ptr = lambda a: a.ctypes.data  # noqa: E731
+    it = KaccInterval()
+    it.n_nodes = sizes["n_nodes"]
+    it.n_procs = sizes["n_procs"]
+    it.n_ctrs = sizes["n_ctrs"]
+    it.n_vms = sizes["n_vms"]
+    it.n_pods = sizes["n_pods"]
+    it.flags = flags
+    for name in INTERVAL_ARRAYS:
+        a = arrays.get(name)
+        if a is None:
+            if name not in OPTIONAL_ARRAYS:
+                raise ValueError(f"missing array {name}")
+            setattr(it, name, None)
+        else:
+            setattr(it, name, ptr(a) or None)  # empty torch tensors give 0 -> NULL
+    return it
+
+
+class Accel:
+    """One engine context on one GPU (kacc_ctx)."""
+
+    def __init__(self, zones: int, nodes: int, proc_slots: int, ctr_slots: int, vm_slots: int,
+                 pod_slots: int, device: int = 0):
+        self.lib = load()
+        self.cfg = KaccConfig(zones, 0, nodes, proc_slots, ctr_slots, vm_slots, pod_slots)
+        h = c_void_p()
+        rc = self.lib.kacc_create(device, ctypes.byref(self.cfg), ctypes.byref(h))
+        if rc != KACC_OK:
+            raise AccelError(rc, self.lib.kacc_last_error(None).decode())
+        self.ctx = h
+        self.zones = zones
+        self.device = device
+
+    # -- plumbing ---------------------------------------------------------
+    def _check(self, rc: int) -> None:
+        if rc != KACC_OK:
+            raise AccelError(rc, self.lib.kacc_last_error(self.ctx).decode())
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.kacc_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- hot path ----------------------------------------------------------
+    def reset(self) -> None:
+        self._check(self.lib.kacc_reset(self.ctx))
+
+    def run_interval(self, dev_interval: KaccInterval, stream: int = 0) -> None:
+        self._check(self.lib.kacc_run_interval(self.ctx, ctypes.byref(dev_interval), c_void_p(stream or None)))
+
+    def sync(self, stream: int = 0) -> None:
+        self._check(self.lib.kacc_sync(self.ctx, c_void_p(stream or None)))
+
+    def validate_host(self, host_interval: KaccInterval) -> int:
+        return self.lib.kacc_validate_host(self.ctx, ctypes.byref(host_interval))
+
+    def last_error(self) -> str:
+        return self.lib.kacc_last_error(self.ctx).decode()
+
+    # -- tables --------------------------------------------------------------
+    def table_info(self, name: str):
+        eb, cnt = c_uint64(), c_uint64()
+        self._check(self.lib.kacc_table_info(self.ctx, TABLE_INDEX[name], ctypes.byref(eb), ctypes.byref(cnt)))
+        return eb.value, cnt.value
+
+    def download(self, name: str, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        _, total = self.table_info(name)
+        if count is None:
+            count = total - first
+        out = np.empty(count, dtype=TABLES[TABLE_INDEX[name]][1])
+        self._check(self.lib.kacc_table_download(self.ctx, TABLE_INDEX[name], first, count, out.ctypes.data))
+        return out
+
+    def upload(self, name: str, values: np.ndarray, first: int = 0) -> None:
+        v = np.ascontiguousarray(values, dtype=TABLES[TABLE_INDEX[name]][1])
+        self._check(self.lib.kacc_table_upload(self.ctx, TABLE_INDEX[name], first, v.size, v.ctypes.data))
+
+    def device_ptr(self, name: str) -> int:
+        p = c_void_p()
+        self._check(self.lib.kacc_table_device_ptr(self.ctx, TABLE_INDEX[name], ctypes.byref(p)))
+        return p.value
+
+    def state(self) -> dict:
+        return {name: self.download(name) for name, _ in TABLES}
+
+    def namespace_totals(self, n_ns: int, ns_pod_off_ptr: int, ns_pod_slot_ptr: int,
+                         out_energy_ptr: int, out_power_ptr: int, stream: int = 0) -> None:
+        self._check(self.lib.kacc_namespace_totals(
+            self.ctx, n_ns, c_void_p(ns_pod_off_ptr), c_void_p(ns_pod_slot_ptr),
+            c_void_p(out_energy_ptr), c_void_p(out_power_ptr), c_void_p(stream or None)))
+
+
+@dataclass
+class HostBatch:
+    """A pinned-host batch (kacc_batch_*): the path a cgo caller takes."""
+
+    accel: Accel
+    handle: c_void_p
+    view: "ctypes._Pointer"
+
+    orig: dict = None
+
+    @classmethod
+    def alloc(cls, accel: Accel, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int):
+        h = c_void_p()
+        v = POINTER(KaccInterval)()
+        accel._check(accel.lib.kacc_batch_alloc(accel.ctx, n_nodes, n_procs, n_ctrs, n_vms, n_pods,
+                                                ctypes.byref(h), ctypes.byref(v)))
+        orig = {name: getattr(v.contents, name) for name in INTERVAL_ARRAYS}
+        return cls(accel, h, v, orig)
+
+    def array(self, name: str, count: int) -> np.ndarray:
+        addr = getattr(self.view.contents, name)
+        dt = np.dtype(ARRAY_DTYPES[name])
+        buf = (ctypes.c_char * (count * dt.itemsize)).from_address(addr)
+        return np.frombuffer(buf, dtype=dt, count=count)
+
+    def fill(self, arrays: dict, flags: int = 0) -> None:
+        v = self.view.contents
+        v.flags = flags
+        for name in INTERVAL_ARRAYS:
+            setattr(v, name, self.orig[name])
+            a = arrays.get(name)
+            if a is None:
+                if name in OPTIONAL_ARRAYS:
+                    setattr(v, name, None)
+                    continue
+                raise ValueError(name)
+            self.array(name, a.size)[:] = a
+
+    def submit(self) -> None:
+        self.accel._check(self.accel.lib.kacc_batch_submit(self.accel.ctx, self.handle))
+
+    def wait(self) -> None:
+        self.accel._check(self.accel.lib.kacc_batch_wait(self.accel.ctx, self.handle))
+
+    def free(self) -> None:
+        if self.handle:
+            self.accel.lib.kacc_batch_free(self.accel.ctx, self.handle)
+            self.handle = None

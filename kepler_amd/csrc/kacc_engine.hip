@@ -1,0 +1,919 @@
+// MI355X (gfx950) power-attribution engine: kernels + C ABI (kepler_accel.h).
+//
+// One kacc_run_interval() = one collection interval of Kepler's
+// PowerMonitor.calculatePower (internal/monitor/monitor.go:399-431) for every
+// node of a fleet, as ONE kernel launch: one workgroup per node snapshot
+// (node snapshots are independent, node.go / process.go only read the node's
+// own zones and totals).  Inside a workgroup:
+//
+//   A  node zones       node.go:10-84 / node.go:101-131 (threads z < Z)
+//   B  node CPU total   informer.go:328-345, canonical 256-lane tree order
+//   C  container / VM   informer.go:223-249 + 469-489, 251-273 + 433-449
+//                        (segmented sums, one lane per segment, listing order)
+//   D  pods             informer.go:275-326 + 491-510 (one lane per pod)
+//   E  attribution      process.go:118-148, container.go:106-140,
+//                        vm.go:78-109, pod.go:87-118 (coalesced row pass)
+//
+// Everything is HBM-bandwidth bound (≈0.1 flop/B); no MFMA.  Workload
+// energy/power live in device-resident slot tables that are updated in place,
+// so the per-row traffic is Δcpu 8 B + slot 4 B + prev total 8Z B in and
+// total 8Z B + power 8Z B out.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kepler_accel.h"
+#include "kacc_device.hpp"
+
+namespace kacc {
+
+constexpr int kBlock = 256;  // lanes of the canonical node-total tree
+constexpr int kUnroll = 4;   // process rows in flight per lane
+
+// device error bits (KACC_ERANGE)
+constexpr uint32_t kErrNode = 1u << 0;
+constexpr uint32_t kErrOffsets = 1u << 1;
+constexpr uint32_t kErrSlot = 1u << 2;
+constexpr uint32_t kErrNs = 1u << 3;
+
+struct DevState {
+  uint64_t *node_energy_total, *node_active_energy, *node_active_total, *node_idle_total;
+  double *node_power, *node_active_power, *node_idle_power;
+  int64_t *node_ts;
+  uint32_t *node_has_prev;
+  double *node_usage_ratio, *node_cpu_delta;
+  uint32_t *node_status;
+  uint64_t *proc_energy;
+  double *proc_power;
+  uint64_t *ctr_energy;
+  double *ctr_power, *ctr_cpu_delta, *ctr_cpu_total;
+  uint64_t *vm_energy;
+  double *vm_power, *vm_cpu_delta;
+  uint64_t *pod_energy;
+  double *pod_power, *pod_cpu_delta, *pod_cpu_total;
+  uint64_t proc_slots, ctr_slots, vm_slots, pod_slots;
+  uint32_t *err;
+};
+
+struct NodeShared {
+  uint64_t active_energy[KACC_MAX_ZONES];
+  double power[KACC_MAX_ZONES];
+  double active_power[KACC_MAX_ZONES];
+  double node_delta;
+};
+
+__device__ __forceinline__ void raise_err(uint32_t *err, uint32_t bit) { atomicOr(err, bit); }
+
+template <int Z>
+struct ZoneRow {  // one workload's zones, loaded/stored as 16-B vectors when Z is even
+  uint64_t v[Z];
+};
+
+template <int Z>
+__device__ __forceinline__ void load_row(const uint64_t *__restrict__ base, uint64_t s,
+                                         uint64_t (&out)[Z]) {
+  if constexpr (Z % 2 == 0) {
+    using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
+    const u64x2 *p = reinterpret_cast<const u64x2 *>(base + s * Z);
+#pragma unroll
+    for (int k = 0; k < Z / 2; ++k) {
+      const u64x2 x = p[k];
+      out[2 * k] = x.x;
+      out[2 * k + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) out[z] = base[s * Z + z];
+  }
+}
+
+template <int Z, typename T>
+__device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, const T (&in)[Z]) {
+  if constexpr (Z % 2 == 0) {
+    using v2 = __attribute__((ext_vector_type(2))) T;
+    v2 *p = reinterpret_cast<v2 *>(base + s * Z);
+#pragma unroll
+    for (int k = 0; k < Z / 2; ++k) {
+      v2 x;
+      x.x = in[2 * k];
+      x.y = in[2 * k + 1];
+      p[k] = x;
+    }
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) base[s * Z + z] = in[z];
+  }
+}
+
+// Node-uniform attribution parameters, held in registers for the row passes.
+template <int Z>
+struct Attr {
+  uint64_t aE[Z];   // NodeUsage.activeEnergy
+  double aP[Z];     // NodeUsage.ActivePower
+  uint32_t live;    // bit z: zone passes the guard (ActivePower/Power, activeEnergy, ΔcpuNode)
+  uint32_t live_pod;
+  double nd;        // ProcessTotalCPUTimeDelta
+  bool first;       // first*Read variant: EnergyTotal = interval energy, Power 0
+};
+
+// process.go:118-148 (and its container/VM/pod twins) for one row.
+template <int Z>
+__device__ __forceinline__ void attribute_row(const Attr<Z> &a, uint32_t live, double delta,
+                                              bool is_new, const uint64_t (&prev)[Z],
+                                              uint64_t (&E)[Z], double (&P)[Z]) {
+  const double ratio = delta / a.nd;  // one IEEE division per row, never a reciprocal
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    if (live & (1u << z)) {
+      const uint64_t e = go_f64_to_u64(ratio * u2f(a.aE[z]));
+      E[z] = a.first ? e : e + (is_new ? 0ull : prev[z]);
+      P[z] = a.first ? 0.0 : ratio * a.aP[z];
+    } else {  // skipped zone keeps the zero Usage of newProcess (process.go:58-63)
+      E[z] = 0;
+      P[z] = 0.0;
+    }
+  }
+}
+
+template <int Z>
+__global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b, const DevState st) {
+  __shared__ NodeShared sh;
+  __shared__ double red[kBlock];
+  __shared__ uint32_t sh_first;
+
+  const int tid = threadIdx.x;
+  uint32_t n = blockIdx.x;
+  if (b.node_order) n = b.node_order[blockIdx.x];
+  if (n >= b.n_nodes) {
+    if (tid == 0) raise_err(st.err, kErrNode);
+    return;
+  }
+  const uint32_t status = b.node_status ? b.node_status[n] : 0u;
+  if (status & KACC_NODE_READ_ERROR) {
+    // node.go:39-44 -> calculatePower fails, previous snapshot kept.
+    if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+    return;
+  }
+
+  // ---- A: node zones --------------------------------------------------------
+  if (tid == 0) sh_first = st.node_has_prev[n] == 0u ? 1u : 0u;
+  __syncthreads();
+  const bool first = sh_first != 0u;
+  if (tid < Z) {
+    const uint64_t i = static_cast<uint64_t>(n) * Z + tid;
+    const double ratio = b.node_usage_ratio[n];
+    const uint64_t abs_e = b.zone_energy[i];
+    uint64_t active;
+    double p = 0.0, ap = 0.0, ip = 0.0;
+    if (first) {  // firstNodeRead, node.go:111-128
+      active = go_f64_to_u64(u2f(abs_e) * ratio);
+      st.node_active_total[i] = active;
+      st.node_idle_total[i] = abs_e - active;
+    } else {  // calculateNodePower, node.go:50-68
+      const double dt = go_duration_seconds(go_sub_mono(b.node_ts_ns[n], st.node_ts[n]));
+      const uint64_t delta = energy_delta(abs_e, st.node_energy_total[i], b.zone_max[i]);
+      active = go_f64_to_u64(u2f(delta) * ratio);
+      st.node_active_total[i] = st.node_active_total[i] + active;
+      st.node_idle_total[i] = st.node_idle_total[i] + (delta - active);
+      p = u2f(delta) / dt;
+      ap = p * ratio;
+      ip = p - ap;
+    }
+    st.node_energy_total[i] = abs_e;
+    st.node_active_energy[i] = active;
+    st.node_power[i] = p;
+    st.node_active_power[i] = ap;
+    st.node_idle_power[i] = ip;
+    sh.active_energy[tid] = active;
+    sh.power[tid] = p;
+    sh.active_power[tid] = ap;
+  }
+
+  // ---- row ranges (clamped so a malformed batch cannot fault) ---------------
+  uint32_t p0 = b.proc_off[n], p1 = b.proc_off[n + 1];
+  uint32_t c0 = b.ctr_off[n], c1 = b.ctr_off[n + 1];
+  uint32_t v0 = b.vm_off[n], v1 = b.vm_off[n + 1];
+  uint32_t q0 = b.pod_off[n], q1 = b.pod_off[n + 1];
+  if (p1 > b.n_procs || p0 > p1 || c1 > b.n_ctrs || c0 > c1 || v1 > b.n_vms || v0 > v1 ||
+      q1 > b.n_pods || q0 > q1) {
+    if (tid == 0) raise_err(st.err, kErrOffsets);
+    p1 = min(p1, b.n_procs);
+    p0 = min(p0, p1);
+    c1 = min(c1, b.n_ctrs);
+    c0 = min(c0, c1);
+    v1 = min(v1, b.n_vms);
+    v0 = min(v0, v1);
+    q1 = min(q1, b.n_pods);
+    q0 = min(q0, q1);
+  }
+  const double *__restrict__ dcpu = b.proc_cpu_delta;
+
+  // ---- B: ProcessTotalCPUTimeDelta (informer.go:330-333) -------------------
+  if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
+    if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
+  } else {
+    double s = 0.0;
+    for (uint32_t r = p0 + tid; r < p1; r += kBlock) s += dcpu[r];
+    red[tid] = s;
+    __syncthreads();
+    if (tid < 128) red[tid] = red[tid] + red[tid + 128];
+    __syncthreads();
+    if (tid < 64) {
+      double v = red[tid] + red[tid + 64];
+#pragma unroll
+      for (int k = 32; k >= 1; k >>= 1) v = v + __shfl_down(v, k, 64);
+      if (tid == 0) sh.node_delta = v;
+    }
+  }
+
+  // ---- C: containers and VMs (segmented, one lane per segment) --------------
+  const uint32_t ctr_rows_end = c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0;
+  for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+    uint32_t beg = c == c0 ? p0 : b.ctr_proc_end[c - 1];
+    uint32_t end = b.ctr_proc_end[c];
+    const uint32_t w = b.ctr_slot[c];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    if (beg < p0 || end < beg || end > p1 || s >= st.ctr_slots) {
+      raise_err(st.err, s >= st.ctr_slots ? kErrSlot : kErrOffsets);
+      if (s >= st.ctr_slots) continue;
+      beg = max(min(beg, p1), p0);
+      end = max(min(end, p1), beg);
+    }
+    double delta = 0.0;  // resetCPUTime on first process (informer.go:229-233, 481-483)
+    double total = (w & KACC_SLOT_NEW) ? 0.0 : st.ctr_cpu_total[s];
+    for (uint32_t i = beg; i < end; ++i) {
+      const double di = dcpu[i];
+      delta = delta + di;  // informer.go:485
+      total = total + di;  // informer.go:486
+    }
+    st.ctr_cpu_delta[s] = delta;
+    st.ctr_cpu_total[s] = total;
+  }
+  for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
+    uint32_t beg = v == v0 ? max(ctr_rows_end, p0) : b.vm_proc_end[v - 1];
+    uint32_t end = b.vm_proc_end[v];
+    const uint64_t s = b.vm_slot[v] & KACC_SLOT_MASK;
+    if (beg < p0 || end < beg || end > p1 || s >= st.vm_slots) {
+      raise_err(st.err, s >= st.vm_slots ? kErrSlot : kErrOffsets);
+      if (s >= st.vm_slots) continue;
+      beg = max(min(beg, p1), p0);
+      end = max(min(end, p1), beg);
+    }
+    // updateVMCache (informer.go:445): last process in listing order wins
+    st.vm_cpu_delta[s] = end > beg ? dcpu[end - 1] : 0.0;
+  }
+  __syncthreads();
+
+  // ---- D: pods (informer.go:305-309, 502-507) -------------------------------
+  for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+    uint32_t beg = q == q0 ? c0 : b.pod_ctr_end[q - 1];
+    uint32_t end = b.pod_ctr_end[q];
+    const uint32_t w = b.pod_slot[q];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    if (beg < c0 || end < beg || end > c1 || s >= st.pod_slots) {
+      raise_err(st.err, s >= st.pod_slots ? kErrSlot : kErrOffsets);
+      if (s >= st.pod_slots) continue;
+      beg = max(min(beg, c1), c0);
+      end = max(min(end, c1), beg);
+    }
+    double delta = 0.0;
+    double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[s];
+    for (uint32_t c = beg; c < end; ++c) {
+      const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
+      if (cs >= st.ctr_slots) continue;  // already flagged in C
+      delta = delta + st.ctr_cpu_delta[cs];
+      total = total + st.ctr_cpu_total[cs];  // quirk: running container total
+    }
+    st.pod_cpu_delta[s] = delta;
+    st.pod_cpu_total[s] = total;
+  }
+  __syncthreads();
+
+  // node scalars of the new snapshot
+  if (tid == 0) {
+    st.node_ts[n] = b.node_ts_ns[n];
+    st.node_has_prev[n] = 1u;
+    st.node_usage_ratio[n] = first ? 0.0 : b.node_usage_ratio[n];  // firstNodeRead leaves 0
+    st.node_cpu_delta[n] = sh.node_delta;
+    st.node_status[n] = first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+  }
+
+  // ---- E: attribution --------------------------------------------------------
+  Attr<Z> a;
+  a.nd = sh.node_delta;
+  a.first = first;
+  a.live = 0;
+  a.live_pod = 0;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    a.aE[z] = sh.active_energy[z];
+    a.aP[z] = sh.active_power[z];
+    const bool ok = a.aE[z] != 0 && a.nd != 0;
+    if (ok && a.aP[z] != 0) a.live |= 1u << z;                    // process.go:124
+    if (ok && (first ? a.aP[z] : sh.power[z]) != 0) a.live_pod |= 1u << z;  // pod.go:96 / :23
+  }
+
+  // processes: coalesced row pass, kUnroll rows in flight per lane
+  for (uint32_t base = p0 + tid; base < p1; base += kBlock * kUnroll) {
+    double d[kUnroll];
+    uint32_t w[kUnroll];
+    uint64_t prev[kUnroll][Z];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint32_t r = base + u * kBlock;
+      const bool in = r < p1;
+      d[u] = in ? dcpu[r] : 0.0;
+      w[u] = in ? b.proc_slot[r] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint64_t s = w[u] & KACC_SLOT_MASK;
+      if (s < st.proc_slots) {
+        load_row<Z>(st.proc_energy, s, prev[u]);
+      } else {
+#pragma unroll
+        for (int z = 0; z < Z; ++z) prev[u][z] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const uint32_t r = base + u * kBlock;
+      if (r >= p1) continue;
+      const uint64_t s = w[u] & KACC_SLOT_MASK;
+      if (s >= st.proc_slots) {
+        raise_err(st.err, kErrSlot);
+        continue;
+      }
+      uint64_t E[Z];
+      double P[Z];
+      attribute_row<Z>(a, a.live, d[u], (w[u] & KACC_SLOT_NEW) != 0, prev[u], E, P);
+      store_row<Z, uint64_t>(st.proc_energy, s, E);
+      store_row<Z, double>(st.proc_power, s, P);
+    }
+  }
+
+  // containers (container.go:106-140): Δ from pass C
+  for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+    const uint32_t w = b.ctr_slot[c];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    if (s >= st.ctr_slots) continue;
+    uint64_t prev[Z], E[Z];
+    double P[Z];
+    load_row<Z>(st.ctr_energy, s, prev);
+    attribute_row<Z>(a, a.live, st.ctr_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
+    store_row<Z, uint64_t>(st.ctr_energy, s, E);
+    store_row<Z, double>(st.ctr_power, s, P);
+  }
+  // virtual machines (vm.go:78-109)
+  for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
+    const uint32_t w = b.vm_slot[v];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    if (s >= st.vm_slots) continue;
+    uint64_t prev[Z], E[Z];
+    double P[Z];
+    load_row<Z>(st.vm_energy, s, prev);
+    attribute_row<Z>(a, a.live, st.vm_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
+    store_row<Z, uint64_t>(st.vm_energy, s, E);
+    store_row<Z, double>(st.vm_power, s, P);
+  }
+  // pods (pod.go:87-118; nothing to do when none run, pod.go:70-73)
+  for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+    const uint32_t w = b.pod_slot[q];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    if (s >= st.pod_slots) continue;
+    uint64_t prev[Z], E[Z];
+    double P[Z];
+    load_row<Z>(st.pod_energy, s, prev);
+    attribute_row<Z>(a, a.live_pod, st.pod_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
+    store_row<Z, uint64_t>(st.pod_energy, s, E);
+    store_row<Z, double>(st.pod_power, s, P);
+  }
+}
+
+// Namespace totals: one lane per namespace, pods summed in the given order.
+__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t Z, uint32_t n_ns,
+                                                           const uint32_t *__restrict__ off,
+                                                           const uint32_t *__restrict__ slots,
+                                                           const uint64_t *__restrict__ pe,
+                                                           const double *__restrict__ pp,
+                                                           uint64_t pod_slots, uint64_t *out_e,
+                                                           double *out_p, uint32_t *err) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_ns) return;
+  uint64_t e[KACC_MAX_ZONES];
+  double p[KACC_MAX_ZONES];
+  for (uint32_t z = 0; z < Z; ++z) {
+    e[z] = 0;
+    p[z] = 0.0;
+  }
+  const uint32_t beg = off[k], end = off[k + 1];
+  for (uint32_t j = beg; j < end; ++j) {
+    const uint64_t s = slots[j] & KACC_SLOT_MASK;
+    if (s >= pod_slots) {
+      raise_err(err, kErrNs);
+      continue;
+    }
+    for (uint32_t z = 0; z < Z; ++z) {
+      e[z] += pe[s * Z + z];
+      p[z] = p[z] + pp[s * Z + z];
+    }
+  }
+  for (uint32_t z = 0; z < Z; ++z) {
+    out_e[static_cast<uint64_t>(k) * Z + z] = e[z];
+    out_p[static_cast<uint64_t>(k) * Z + z] = p[z];
+  }
+}
+
+}  // namespace kacc
+
+// =============================================================================
+// C ABI
+// =============================================================================
+namespace {
+
+thread_local std::string g_create_error;
+
+struct TableDesc {
+  uint32_t elem;   // bytes
+  int per;         // 0 = per node, 1 = per proc slot, 2 ctr, 3 vm, 4 pod
+  bool zoned;      // × Z
+};
+
+const TableDesc kTables[KACC_T_COUNT] = {
+    {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},
+    {8, 0, true},  {8, 0, false}, {4, 0, false}, {8, 0, false}, {8, 0, false}, {4, 0, false},
+    {8, 1, true},  {8, 1, true},  {8, 2, true},  {8, 2, true},  {8, 2, false}, {8, 2, false},
+    {8, 3, true},  {8, 3, true},  {8, 3, false}, {8, 4, true},  {8, 4, true},  {8, 4, false},
+    {8, 4, false},
+};
+
+}  // namespace
+
+struct kacc_ctx {
+  int device = 0;
+  kacc_config cfg{};
+  hipStream_t stream = nullptr;
+  void *tables[KACC_T_COUNT] = {};
+  uint64_t counts[KACC_T_COUNT] = {};
+  uint32_t *d_err = nullptr;
+  std::string err;
+};
+
+struct kacc_batch {
+  kacc_interval host{};
+  kacc_interval dev{};
+  std::vector<std::pair<void *, void *>> bufs;  // {pinned host, device}
+  std::vector<size_t> sizes;
+};
+
+namespace {
+
+int fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx)
+    ctx->err = buf;
+  else
+    g_create_error = buf;
+  return code;
+}
+
+#define KACC_HIP(ctx, call)                                                              \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail((ctx), e_ == hipErrorOutOfMemory ? KACC_ENOMEM : KACC_EHIP, "%s: %s", \
+                  #call, hipGetErrorString(e_));                                         \
+  } while (0)
+
+uint64_t table_count(const kacc_config &c, int t) {
+  const TableDesc &d = kTables[t];
+  uint64_t base = 0;
+  switch (d.per) {
+    case 0: base = c.nodes; break;
+    case 1: base = c.proc_slots; break;
+    case 2: base = c.ctr_slots; break;
+    case 3: base = c.vm_slots; break;
+    default: base = c.pod_slots; break;
+  }
+  return d.zoned ? base * c.zones : base;
+}
+
+kacc::DevState dev_state(const kacc_ctx *ctx) {
+  kacc::DevState s;
+  auto T = [ctx](int t) { return ctx->tables[t]; };
+  s.node_energy_total = (uint64_t *)T(KACC_T_NODE_ENERGY_TOTAL);
+  s.node_active_energy = (uint64_t *)T(KACC_T_NODE_ACTIVE_ENERGY);
+  s.node_active_total = (uint64_t *)T(KACC_T_NODE_ACTIVE_TOTAL);
+  s.node_idle_total = (uint64_t *)T(KACC_T_NODE_IDLE_TOTAL);
+  s.node_power = (double *)T(KACC_T_NODE_POWER);
+  s.node_active_power = (double *)T(KACC_T_NODE_ACTIVE_POWER);
+  s.node_idle_power = (double *)T(KACC_T_NODE_IDLE_POWER);
+  s.node_ts = (int64_t *)T(KACC_T_NODE_TS);
+  s.node_has_prev = (uint32_t *)T(KACC_T_NODE_HAS_PREV);
+  s.node_usage_ratio = (double *)T(KACC_T_NODE_USAGE_RATIO);
+  s.node_cpu_delta = (double *)T(KACC_T_NODE_CPU_DELTA);
+  s.node_status = (uint32_t *)T(KACC_T_NODE_STATUS);
+  s.proc_energy = (uint64_t *)T(KACC_T_PROC_ENERGY);
+  s.proc_power = (double *)T(KACC_T_PROC_POWER);
+  s.ctr_energy = (uint64_t *)T(KACC_T_CTR_ENERGY);
+  s.ctr_power = (double *)T(KACC_T_CTR_POWER);
+  s.ctr_cpu_delta = (double *)T(KACC_T_CTR_CPU_DELTA);
+  s.ctr_cpu_total = (double *)T(KACC_T_CTR_CPU_TOTAL);
+  s.vm_energy = (uint64_t *)T(KACC_T_VM_ENERGY);
+  s.vm_power = (double *)T(KACC_T_VM_POWER);
+  s.vm_cpu_delta = (double *)T(KACC_T_VM_CPU_DELTA);
+  s.pod_energy = (uint64_t *)T(KACC_T_POD_ENERGY);
+  s.pod_power = (double *)T(KACC_T_POD_POWER);
+  s.pod_cpu_delta = (double *)T(KACC_T_POD_CPU_DELTA);
+  s.pod_cpu_total = (double *)T(KACC_T_POD_CPU_TOTAL);
+  s.proc_slots = ctx->cfg.proc_slots;
+  s.ctr_slots = ctx->cfg.ctr_slots;
+  s.vm_slots = ctx->cfg.vm_slots;
+  s.pod_slots = ctx->cfg.pod_slots;
+  s.err = ctx->d_err;
+  return s;
+}
+
+template <int Z>
+void launch_z(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
+  hipLaunchKernelGGL(kacc::interval_kernel<Z>, dim3(b.n_nodes), dim3(kacc::kBlock), 0, st, b, s);
+}
+
+void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
+  switch (Z) {
+    case 1: launch_z<1>(b, s, st); break;
+    case 2: launch_z<2>(b, s, st); break;
+    case 3: launch_z<3>(b, s, st); break;
+    case 4: launch_z<4>(b, s, st); break;
+    case 5: launch_z<5>(b, s, st); break;
+    case 6: launch_z<6>(b, s, st); break;
+    case 7: launch_z<7>(b, s, st); break;
+    default: launch_z<8>(b, s, st); break;
+  }
+}
+
+int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
+  if (!b) return fail(ctx, KACC_EINVAL, "batch is NULL");
+  if (b->n_nodes > ctx->cfg.nodes)
+    return fail(ctx, KACC_EINVAL, "n_nodes %u exceeds node capacity %llu", b->n_nodes,
+                (unsigned long long)ctx->cfg.nodes);
+  if (b->n_nodes == 0) return KACC_OK;
+  if (!b->node_ts_ns || !b->node_usage_ratio || !b->zone_energy || !b->zone_max ||
+      !b->proc_off || !b->ctr_off || !b->vm_off || !b->pod_off)
+    return fail(ctx, KACC_EINVAL, "required node array is NULL");
+  if ((b->n_procs && (!b->proc_cpu_delta || !b->proc_slot)) ||
+      (b->n_ctrs && (!b->ctr_proc_end || !b->ctr_slot)) ||
+      (b->n_vms && (!b->vm_proc_end || !b->vm_slot)) ||
+      (b->n_pods && (!b->pod_ctr_end || !b->pod_slot)))
+    return fail(ctx, KACC_EINVAL, "required row array is NULL");
+  if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
+    return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
+  if (b->flags & ~KACC_F_NODE_CPU_DELTA_GIVEN)
+    return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
+  return KACC_OK;
+}
+
+int check_offsets(kacc_ctx *ctx, const char *name, const uint32_t *off, uint32_t n, uint32_t count) {
+  if (off[0] != 0) return fail(ctx, KACC_EINVAL, "%s[0] must be 0", name);
+  for (uint32_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i]) return fail(ctx, KACC_EINVAL, "%s not monotonic at %u", name, i);
+  if (off[n] != count) return fail(ctx, KACC_EINVAL, "%s[n] != row count", name);
+  return KACC_OK;
+}
+
+int check_slots(kacc_ctx *ctx, const char *name, const uint32_t *w, uint32_t n, uint64_t cap) {
+  std::vector<uint8_t> seen(cap, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t s = w[i] & KACC_SLOT_MASK;
+    if (s >= cap) return fail(ctx, KACC_EINVAL, "%s[%u]=%llu >= capacity", name, i, (unsigned long long)s);
+    if (seen[s]) return fail(ctx, KACC_EINVAL, "%s: slot %llu used twice", name, (unsigned long long)s);
+    seen[s] = 1;
+  }
+  return KACC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t kacc_abi_version(void) { return KACC_ABI_VERSION; }
+
+const char *kacc_last_error(const kacc_ctx *ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
+  if (!cfg || !out) return fail(nullptr, KACC_EINVAL, "NULL argument");
+  *out = nullptr;
+  if (cfg->zones == 0 || cfg->zones > KACC_MAX_ZONES)
+    return fail(nullptr, KACC_EINVAL, "zones must be 1..%u", KACC_MAX_ZONES);
+  if (cfg->proc_slots > KACC_SLOT_MASK || cfg->ctr_slots > KACC_SLOT_MASK ||
+      cfg->vm_slots > KACC_SLOT_MASK || cfg->pod_slots > KACC_SLOT_MASK || cfg->nodes > 0xffffffffu)
+    return fail(nullptr, KACC_EINVAL, "capacity exceeds the 31-bit slot range");
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return fail(nullptr, KACC_EHIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+  auto *ctx = new kacc_ctx;
+  ctx->device = device;
+  ctx->cfg = *cfg;
+  int rc = KACC_OK;
+  auto bail = [&](int code) {
+    g_create_error = ctx->err;
+    kacc_destroy(ctx);
+    return code;
+  };
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
+    fail(ctx, KACC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    return bail(KACC_EHIP);
+  }
+  for (int t = 0; t < KACC_T_COUNT; ++t) {
+    ctx->counts[t] = table_count(ctx->cfg, t);
+    const size_t bytes = std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem;
+    if ((e = hipMalloc(&ctx->tables[t], bytes)) != hipSuccess) {
+      fail(ctx, KACC_ENOMEM, "hipMalloc table %d (%zu B): %s", t, bytes, hipGetErrorString(e));
+      return bail(KACC_ENOMEM);
+    }
+  }
+  if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess) {
+    fail(ctx, KACC_ENOMEM, "hipMalloc err word: %s", hipGetErrorString(e));
+    return bail(KACC_ENOMEM);
+  }
+  if ((rc = kacc_reset(ctx)) != KACC_OK) return bail(rc);
+  *out = ctx;
+  return KACC_OK;
+}
+
+void kacc_destroy(kacc_ctx *ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (int t = 0; t < KACC_T_COUNT; ++t)
+    if (ctx->tables[t]) (void)hipFree(ctx->tables[t]);
+  if (ctx->d_err) (void)hipFree(ctx->d_err);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int kacc_get_config(const kacc_ctx *ctx, kacc_config *out) {
+  if (!ctx || !out) return KACC_EINVAL;
+  *out = ctx->cfg;
+  return KACC_OK;
+}
+
+int kacc_reset(kacc_ctx *ctx) {
+  if (!ctx) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  for (int t = 0; t < KACC_T_COUNT; ++t)
+    KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0,
+                                 std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
+                                 ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
+  KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return KACC_OK;
+}
+
+int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = check_shape(ctx, b);
+  if (rc != KACC_OK || b->n_nodes == 0) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  launch(ctx->cfg.zones, *b, dev_state(ctx), st);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_sync(kacc_ctx *ctx, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  KACC_HIP(ctx, hipStreamSynchronize(st));
+  uint32_t err = 0;
+  KACC_HIP(ctx, hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost));
+  if (err) {
+    KACC_HIP(ctx, hipMemset(ctx->d_err, 0, sizeof(uint32_t)));
+    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace)", err);
+  }
+  return KACC_OK;
+}
+
+int kacc_validate_host(const kacc_ctx *cctx, const kacc_interval *b) {
+  kacc_ctx *ctx = const_cast<kacc_ctx *>(cctx);
+  if (!ctx) return KACC_EINVAL;
+  int rc = check_shape(ctx, b);
+  if (rc != KACC_OK || b->n_nodes == 0) return rc;
+  const uint32_t N = b->n_nodes;
+  if ((rc = check_offsets(ctx, "proc_off", b->proc_off, N, b->n_procs))) return rc;
+  if ((rc = check_offsets(ctx, "ctr_off", b->ctr_off, N, b->n_ctrs))) return rc;
+  if ((rc = check_offsets(ctx, "vm_off", b->vm_off, N, b->n_vms))) return rc;
+  if ((rc = check_offsets(ctx, "pod_off", b->pod_off, N, b->n_pods))) return rc;
+  for (uint32_t n = 0; n < N; ++n) {
+    const uint32_t p0 = b->proc_off[n], p1 = b->proc_off[n + 1];
+    uint32_t prev = p0;
+    for (uint32_t c = b->ctr_off[n]; c < b->ctr_off[n + 1]; ++c) {
+      if (b->ctr_proc_end[c] < prev || b->ctr_proc_end[c] > p1)
+        return fail(ctx, KACC_EINVAL, "ctr_proc_end[%u] outside node %u rows", c, n);
+      prev = b->ctr_proc_end[c];
+    }
+    for (uint32_t v = b->vm_off[n]; v < b->vm_off[n + 1]; ++v) {
+      if (b->vm_proc_end[v] < prev || b->vm_proc_end[v] > p1)
+        return fail(ctx, KACC_EINVAL, "vm_proc_end[%u] outside node %u rows", v, n);
+      prev = b->vm_proc_end[v];
+    }
+    uint32_t cprev = b->ctr_off[n];
+    for (uint32_t q = b->pod_off[n]; q < b->pod_off[n + 1]; ++q) {
+      if (b->pod_ctr_end[q] < cprev || b->pod_ctr_end[q] > b->ctr_off[n + 1])
+        return fail(ctx, KACC_EINVAL, "pod_ctr_end[%u] outside node %u containers", q, n);
+      cprev = b->pod_ctr_end[q];
+    }
+  }
+  if ((rc = check_slots(ctx, "proc_slot", b->proc_slot, b->n_procs, ctx->cfg.proc_slots))) return rc;
+  if ((rc = check_slots(ctx, "ctr_slot", b->ctr_slot, b->n_ctrs, ctx->cfg.ctr_slots))) return rc;
+  if ((rc = check_slots(ctx, "vm_slot", b->vm_slot, b->n_vms, ctx->cfg.vm_slots))) return rc;
+  if ((rc = check_slots(ctx, "pod_slot", b->pod_slot, b->n_pods, ctx->cfg.pod_slots))) return rc;
+  if (b->node_order) {
+    std::vector<uint8_t> seen(N, 0);
+    for (uint32_t i = 0; i < N; ++i) {
+      if (b->node_order[i] >= N || seen[b->node_order[i]])
+        return fail(ctx, KACC_EINVAL, "node_order is not a permutation");
+      seen[b->node_order[i]] = 1;
+    }
+  }
+  return KACC_OK;
+}
+
+int kacc_batch_alloc(kacc_ctx *ctx, uint32_t N, uint32_t P, uint32_t C, uint32_t V, uint32_t Q,
+                     kacc_batch **out, kacc_interval **view) {
+  if (!ctx || !out || !view) return KACC_EINVAL;
+  if (N > ctx->cfg.nodes) return fail(ctx, KACC_EINVAL, "n_nodes exceeds capacity");
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  auto *bt = new kacc_batch;
+  const uint64_t Z = ctx->cfg.zones;
+  struct F {
+    const void **h;
+    const void **d;
+    size_t bytes;
+  };
+  kacc_interval &h = bt->host;
+  kacc_interval &d = bt->dev;
+  h.n_nodes = d.n_nodes = N;
+  h.n_procs = d.n_procs = P;
+  h.n_ctrs = d.n_ctrs = C;
+  h.n_vms = d.n_vms = V;
+  h.n_pods = d.n_pods = Q;
+  const F fields[] = {
+      {(const void **)&h.node_ts_ns, (const void **)&d.node_ts_ns, 8ull * N},
+      {(const void **)&h.node_usage_ratio, (const void **)&d.node_usage_ratio, 8ull * N},
+      {(const void **)&h.node_status, (const void **)&d.node_status, 4ull * N},
+      {(const void **)&h.node_cpu_delta, (const void **)&d.node_cpu_delta, 8ull * N},
+      {(const void **)&h.node_order, (const void **)&d.node_order, 4ull * N},
+      {(const void **)&h.zone_energy, (const void **)&d.zone_energy, 8ull * N * Z},
+      {(const void **)&h.zone_max, (const void **)&d.zone_max, 8ull * N * Z},
+      {(const void **)&h.proc_off, (const void **)&d.proc_off, 4ull * (N + 1)},
+      {(const void **)&h.ctr_off, (const void **)&d.ctr_off, 4ull * (N + 1)},
+      {(const void **)&h.vm_off, (const void **)&d.vm_off, 4ull * (N + 1)},
+      {(const void **)&h.pod_off, (const void **)&d.pod_off, 4ull * (N + 1)},
+      {(const void **)&h.proc_cpu_delta, (const void **)&d.proc_cpu_delta, 8ull * P},
+      {(const void **)&h.proc_slot, (const void **)&d.proc_slot, 4ull * P},
+      {(const void **)&h.ctr_proc_end, (const void **)&d.ctr_proc_end, 4ull * C},
+      {(const void **)&h.ctr_slot, (const void **)&d.ctr_slot, 4ull * C},
+      {(const void **)&h.vm_proc_end, (const void **)&d.vm_proc_end, 4ull * V},
+      {(const void **)&h.vm_slot, (const void **)&d.vm_slot, 4ull * V},
+      {(const void **)&h.pod_ctr_end, (const void **)&d.pod_ctr_end, 4ull * Q},
+      {(const void **)&h.pod_slot, (const void **)&d.pod_slot, 4ull * Q},
+  };
+  for (const F &f : fields) {
+    const size_t bytes = std::max<size_t>(f.bytes, 8);
+    void *hp = nullptr, *dp = nullptr;
+    hipError_t e = hipHostMalloc(&hp, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc(&dp, bytes);
+    if (e != hipSuccess) {
+      if (hp) (void)hipHostFree(hp);
+      kacc_batch_free(ctx, bt);
+      return fail(ctx, KACC_ENOMEM, "batch allocation (%zu B): %s", bytes, hipGetErrorString(e));
+    }
+    std::memset(hp, 0, bytes);
+    *f.h = hp;
+    *f.d = dp;
+    bt->bufs.emplace_back(hp, dp);
+    bt->sizes.push_back(f.bytes);
+  }
+  *out = bt;
+  *view = &bt->host;
+  return KACC_OK;
+}
+
+int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
+  if (!ctx || !bt) return KACC_EINVAL;
+  int rc = kacc_validate_host(ctx, &bt->host);
+  if (rc != KACC_OK) return rc;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  kacc_interval dv = bt->dev;
+  dv.flags = bt->host.flags;
+  // honour optional arrays the caller switched off
+  if (!bt->host.node_status) dv.node_status = nullptr;
+  if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;
+  if (!bt->host.node_order) dv.node_order = nullptr;
+  for (size_t i = 0; i < bt->bufs.size(); ++i) {
+    if (!bt->sizes[i]) continue;
+    KACC_HIP(ctx, hipMemcpyAsync(bt->bufs[i].second, bt->bufs[i].first, bt->sizes[i],
+                                 hipMemcpyHostToDevice, ctx->stream));
+  }
+  launch(ctx->cfg.zones, dv, dev_state(ctx), ctx->stream);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_batch_wait(kacc_ctx *ctx, kacc_batch *bt) {
+  if (!ctx || !bt) return KACC_EINVAL;
+  return kacc_sync(ctx, nullptr);
+}
+
+void kacc_batch_free(kacc_ctx *ctx, kacc_batch *bt) {
+  if (!bt) return;
+  if (ctx) (void)hipSetDevice(ctx->device);
+  for (auto &b : bt->bufs) {
+    if (b.first) (void)hipHostFree(b.first);
+    if (b.second) (void)hipFree(b.second);
+  }
+  delete bt;
+}
+
+int kacc_table_info(const kacc_ctx *ctx, kacc_table t, uint64_t *elem_bytes, uint64_t *count) {
+  if (!ctx || t < 0 || t >= KACC_T_COUNT) return KACC_EINVAL;
+  if (elem_bytes) *elem_bytes = kTables[t].elem;
+  if (count) *count = ctx->counts[t];
+  return KACC_OK;
+}
+
+int kacc_table_device_ptr(kacc_ctx *ctx, kacc_table t, void **dev_ptr) {
+  if (!ctx || t < 0 || t >= KACC_T_COUNT || !dev_ptr) return KACC_EINVAL;
+  *dev_ptr = ctx->tables[t];
+  return KACC_OK;
+}
+
+static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host,
+                      bool down) {
+  if (!ctx || t < 0 || t >= KACC_T_COUNT || (!host && count)) return KACC_EINVAL;
+  if (first > ctx->counts[t] || count > ctx->counts[t] - first)
+    return fail(ctx, KACC_EINVAL, "table %d range [%llu,+%llu) outside %llu", (int)t,
+                (unsigned long long)first, (unsigned long long)count,
+                (unsigned long long)ctx->counts[t]);
+  if (!count) return KACC_OK;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  char *dev = static_cast<char *>(ctx->tables[t]) + first * kTables[t].elem;
+  const size_t bytes = count * kTables[t].elem;
+  if (down)
+    KACC_HIP(ctx, hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+  else
+    KACC_HIP(ctx, hipMemcpy(dev, host, bytes, hipMemcpyHostToDevice));
+  return KACC_OK;
+}
+
+int kacc_table_download(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host_dst) {
+  return table_copy(ctx, t, first, count, host_dst, true);
+}
+
+int kacc_table_upload(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count,
+                      const void *host_src) {
+  return table_copy(ctx, t, first, count, const_cast<void *>(host_src), false);
+}
+
+int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
+                          uint64_t *out_energy, double *out_power, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (!n_ns) return KACC_OK;
+  if (!off || !slots || !out_energy || !out_power) return fail(ctx, KACC_EINVAL, "NULL argument");
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const uint32_t grid = (n_ns + kacc::kBlock - 1) / kacc::kBlock;
+  hipLaunchKernelGGL(kacc::namespace_kernel, dim3(grid), dim3(kacc::kBlock), 0, st,
+                     ctx->cfg.zones, n_ns, off, slots,
+                     (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
+                     (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots,
+                     out_energy, out_power, ctx->d_err);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V,
+                             uint64_t Q) {
+  // minimal HBM bytes of one interval_kernel launch.
+  const uint64_t node = 76 + 96ull * Z;
+  const uint64_t proc = 12 + 24ull * Z;
+  const uint64_t ctr = 32 + 24ull * Z;
+  const uint64_t vm = 16 + 24ull * Z;
+  const uint64_t pod = 32 + 24ull * Z;
+  return N * node + P * proc + C * ctr + V * vm + Q * pod;
+}
+
+}  // extern "C"

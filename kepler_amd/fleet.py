@@ -1,0 +1,330 @@
+"""Synthetic fleet generator and SoA batch layout.
+
+A *fleet* is N node snapshots.  Each node has Z RAPL zones and a process
+table laid out as the engine expects (include/kepler_accel.h): container
+processes grouped by container, then VM processes grouped by VM, then the
+other processes; containers grouped by pod.  Workloads keep stable slots in
+the device-resident tables; a process that is new this interval carries
+KACC_SLOT_NEW (process.go:133-138: no previous snapshot entry).
+
+Inputs are generated the way the Go side would produce them:
+  * zone counters advance by P(W)·dt µJ and wrap at MaxEnergy
+    (fake_cpu_power_meter.go:57 / node.go:87-98);
+  * timestamps are monotonic ns, dt = 5 s ± jitter (config.go:206 interval);
+  * per-process CPUTimeDelta = f64(ticks)/100 − previous total, exactly the
+    informer formula (procfs_reader.go:75-82, informer.go:518);
+  * the usage ratio is U[0.05, 0.95] with 1 % exact zeros (exercises the
+    zero-ActivePower skip, process.go:124).
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import numpy as np
+
+from .accel import KACC_NODE_READ_ERROR, KACC_SLOT_NEW
+
+SEED = 0x4B45504C
+# internal/device/testdata/sys/.../max_energy_range_uj
+MAX_ENERGY_RAPL = 262143328850
+# fake_cpu_power_meter.go:135 (the wrap configs)
+MAX_ENERGY_FAKE = 1_000_000
+ZONE_NAMES = {
+    1: ["package"],
+    2: ["package", "dram"],
+    3: ["package", "core", "dram"],
+    4: ["package", "core", "uncore", "dram"],
+}
+
+
+@dataclass
+class FleetLayout:
+    zones: int
+    n_nodes: int
+    proc_off: np.ndarray
+    ctr_off: np.ndarray
+    vm_off: np.ndarray
+    pod_off: np.ndarray
+    ctr_proc_end: np.ndarray
+    vm_proc_end: np.ndarray
+    pod_ctr_end: np.ndarray
+    proc_slot: np.ndarray
+    ctr_slot: np.ndarray
+    vm_slot: np.ndarray
+    pod_slot: np.ndarray
+    pod_ns: np.ndarray
+    n_namespaces: int
+
+    @property
+    def n_procs(self) -> int:
+        return int(self.proc_off[-1])
+
+    @property
+    def n_ctrs(self) -> int:
+        return int(self.ctr_off[-1])
+
+    @property
+    def n_vms(self) -> int:
+        return int(self.vm_off[-1])
+
+    @property
+    def n_pods(self) -> int:
+        return int(self.pod_off[-1])
+
+    def sizes(self) -> Dict[str, int]:
+        return dict(n_nodes=self.n_nodes, n_procs=self.n_procs, n_ctrs=self.n_ctrs,
+                    n_vms=self.n_vms, n_pods=self.n_pods)
+
+    def capacities(self) -> Dict[str, int]:
+        return dict(
+            nodes=self.n_nodes,
+            proc_slots=max(int(self.proc_slot.max(initial=0)) + 1, 1),
+            ctr_slots=max(int(self.ctr_slot.max(initial=0)) + 1, 1),
+            vm_slots=max(int(self.vm_slot.max(initial=0)) + 1, 1),
+            pod_slots=max(int(self.pod_slot.max(initial=0)) + 1, 1),
+        )
+
+    def static_arrays(self) -> Dict[str, np.ndarray]:
+        return dict(proc_off=self.proc_off, ctr_off=self.ctr_off, vm_off=self.vm_off,
+                    pod_off=self.pod_off, ctr_proc_end=self.ctr_proc_end,
+                    vm_proc_end=self.vm_proc_end, pod_ctr_end=self.pod_ctr_end)
+
+    def namespace_csr(self):
+        """ns_pod_off [n_ns+1], ns_pod_slot [Q]: pods grouped by namespace (stable)."""
+        order = np.argsort(self.pod_ns, kind="stable")
+        counts = np.bincount(self.pod_ns, minlength=self.n_namespaces)
+        off = np.zeros(self.n_namespaces + 1, dtype=np.uint32)
+        np.cumsum(counts, out=off[1:])
+        return off, self.pod_slot[order].astype(np.uint32)
+
+    def node_order_heaviest_first(self) -> np.ndarray:
+        rows = np.diff(self.proc_off.astype(np.int64))
+        return np.argsort(-rows, kind="stable").astype(np.uint32)
+
+
+def _split(rng, totals: np.ndarray, parts: np.ndarray) -> np.ndarray:
+    """Split totals[n] into parts[n] segments of size >= 1 (random), flattened."""
+    totals = totals.astype(np.int64)
+    parts = parts.astype(np.int64)
+    assert np.all(parts <= np.maximum(totals, 0)) and np.all((parts > 0) | (totals == 0))
+    n_seg = int(parts.sum())
+    sizes = np.ones(n_seg, dtype=np.int64)
+    extra = totals - parts
+    seg_base = np.zeros(len(parts), dtype=np.int64)
+    np.cumsum(parts[:-1], out=seg_base[1:])
+    n_extra = int(extra.sum())
+    if n_extra > 0:
+        owner = np.repeat(np.arange(len(parts)), extra)
+        pick = seg_base[owner] + (rng.random(n_extra) * parts[owner]).astype(np.int64)
+        sizes += np.bincount(pick, minlength=n_seg)
+    return sizes
+
+
+def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
+                ctr_frac: float = 0.79, procs_per_ctr: int = 8, vm_frac: float = 0.01,
+                procs_per_vm: int = 1, ctrs_per_pod: float = 2.5, pod_frac: float = 0.9,
+                n_namespaces: Optional[int] = None, shuffle_slots: bool = False) -> FleetLayout:
+    rng = np.random.default_rng(seed)
+    P = np.broadcast_to(np.asarray(procs_per_node, dtype=np.int64), (n_nodes,)).copy()
+    Vp = np.floor(P * vm_frac).astype(np.int64)  # VM processes
+    W = np.where(Vp > 0, np.maximum(Vp // max(procs_per_vm, 1), 1), 0)  # VMs
+    T = np.minimum(np.floor(P * ctr_frac).astype(np.int64), P - Vp)  # container processes
+    C = np.where(T > 0, np.maximum(T // procs_per_ctr, 1), 0)
+    ctr_sizes = _split(rng, T, C)
+    vm_sizes = _split(rng, Vp, W)
+    podded = np.floor(C * pod_frac).astype(np.int64)
+    Q = np.where(podded > 0, np.maximum(np.floor(podded / ctrs_per_pod).astype(np.int64), 1), 0)
+    pod_sizes = _split(rng, podded, Q)
+
+    def offsets(counts):
+        off = np.zeros(n_nodes + 1, dtype=np.int64)
+        np.cumsum(counts, out=off[1:])
+        return off
+
+    proc_off, ctr_off, vm_off, pod_off = offsets(P), offsets(C), offsets(W), offsets(Q)
+    # container c ends at node base + cumulative size within node
+    node_of_ctr = np.repeat(np.arange(n_nodes), C)
+    csum = np.cumsum(ctr_sizes)
+    ctr_base = np.repeat(np.concatenate([[0], csum])[ctr_off[:-1]], C)
+    ctr_proc_end = proc_off[node_of_ctr] + (csum - ctr_base)
+    node_of_vm = np.repeat(np.arange(n_nodes), W)
+    vsum = np.cumsum(vm_sizes)
+    vm_base = np.repeat(np.concatenate([[0], vsum])[vm_off[:-1]], W)
+    vm_proc_end = proc_off[node_of_vm] + T[node_of_vm] + (vsum - vm_base)
+    node_of_pod = np.repeat(np.arange(n_nodes), Q)
+    qsum = np.cumsum(pod_sizes)
+    pod_base = np.repeat(np.concatenate([[0], qsum])[pod_off[:-1]], Q)
+    pod_ctr_end = ctr_off[node_of_pod] + (qsum - pod_base)
+
+    n_procs, n_ctrs, n_vms, n_pods = int(proc_off[-1]), int(ctr_off[-1]), int(vm_off[-1]), int(pod_off[-1])
+    if shuffle_slots:
+        proc_slot = rng.permutation(n_procs)
+        ctr_slot = rng.permutation(n_ctrs)
+        vm_slot = rng.permutation(n_vms)
+        pod_slot = rng.permutation(n_pods)
+    else:
+        proc_slot, ctr_slot = np.arange(n_procs), np.arange(n_ctrs)
+        vm_slot, pod_slot = np.arange(n_vms), np.arange(n_pods)
+    if n_namespaces is None:
+        n_namespaces = max(n_nodes, 1)
+    pod_ns = rng.integers(0, n_namespaces, size=n_pods)
+    u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
+    return FleetLayout(
+        zones=zones, n_nodes=n_nodes,
+        proc_off=u32(proc_off), ctr_off=u32(ctr_off), vm_off=u32(vm_off), pod_off=u32(pod_off),
+        ctr_proc_end=u32(ctr_proc_end), vm_proc_end=u32(vm_proc_end), pod_ctr_end=u32(pod_ctr_end),
+        proc_slot=u32(proc_slot), ctr_slot=u32(ctr_slot), vm_slot=u32(vm_slot), pod_slot=u32(pod_slot),
+        pod_ns=u32(pod_ns), n_namespaces=n_namespaces,
+    )
+
+
+def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None) -> FleetLayout:
+    """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed)."""
+    if config == 1:  # single node, 500 procs -> 50 containers -> 20 pods, package+dram
+        return make_layout(1, 500, 2, seed, ctr_frac=0.8, procs_per_ctr=8, ctrs_per_pod=2.5,
+                           pod_frac=1.0, n_namespaces=4)
+    if config == 2:
+        return make_layout(nodes or 1000, 1000, 2, seed)
+    if config in (3, 4):
+        return make_layout(nodes or 10000, 2000, 4, seed)
+    if config == 5:
+        rng = np.random.default_rng(seed ^ 5)
+        n = nodes or 1000
+        # truncated Pareto(alpha=1.5) on [10k, 50k] procs per node
+        u = rng.random(n)
+        a, lo, hi = 1.5, 10_000.0, 50_000.0
+        p = lo / (1 - u * (1 - (lo / hi) ** a)) ** (1 / a)
+        return make_layout(n, p.astype(np.int64), 4, seed, procs_per_vm=2, vm_frac=0.02)
+    raise ValueError(config)
+
+
+@dataclass
+class FleetSim:
+    """Per-interval dynamic inputs for a layout (host numpy arrays)."""
+
+    layout: FleetLayout
+    seed: int = SEED
+    max_energy: int = MAX_ENERGY_RAPL
+    dt_ns: int = 5_000_000_000
+    jitter_ns: int = 50_000_000
+    zero_ratio_frac: float = 0.01
+    churn: float = 0.02
+    read_error_frac: float = 0.0
+    interval: int = 0
+    _rng: np.random.Generator = field(init=False, repr=False)
+
+    def __post_init__(self):
+        L = self.layout
+        self._rng = np.random.default_rng(self.seed ^ 0x51)
+        Z, N = L.zones, L.n_nodes
+        self.zone_max = np.full(N * Z, self.max_energy, dtype=np.uint64)
+        self.counters = (self._rng.random(N * Z) * self.max_energy).astype(np.uint64)
+        self.ts = (1_000_000_000_000 + self._rng.integers(0, 10**9, size=N)).astype(np.int64)
+        self.cum_ticks = self._rng.integers(0, 10_000, size=L.n_procs).astype(np.int64)
+        self.prev_total = np.zeros(L.n_procs, dtype=np.float64)  # informer cache starts empty
+        pkg = self._rng.uniform(50.0, 400.0, size=N)
+        dram = self._rng.uniform(5.0, 40.0, size=N)
+        watts = {"package": pkg, "core": 0.6 * pkg, "uncore": 0.1 * pkg, "dram": dram}
+        self.zone_watts = np.stack([watts[z] for z in ZONE_NAMES[Z]], axis=1).reshape(-1)
+
+    def next_node_inputs(self) -> Dict[str, np.ndarray]:
+        """Advance the node-level inputs (clock, counters, usage ratio) one interval."""
+        L, rng = self.layout, self._rng
+        N, Z = L.n_nodes, L.zones
+        dt = self.dt_ns + rng.integers(-self.jitter_ns, self.jitter_ns + 1, size=N)
+        self.ts = self.ts + dt
+        dts = np.repeat(dt, Z).astype(np.float64) / 1e9
+        watts = self.zone_watts * rng.uniform(0.8, 1.2, size=N * Z)
+        de = np.round(watts * dts * 1e6).astype(np.uint64)
+        self.counters = (self.counters + de) % self.zone_max
+        ratio = rng.uniform(0.05, 0.95, size=N)
+        ratio[rng.random(N) < self.zero_ratio_frac] = 0.0
+        status = np.zeros(N, dtype=np.uint32)
+        if self.read_error_frac > 0 and self.interval > 0:
+            status[rng.random(N) < self.read_error_frac] = KACC_NODE_READ_ERROR
+        return dict(node_ts_ns=self.ts.astype(np.int64), node_usage_ratio=ratio, node_status=status,
+                    zone_energy=self.counters.copy(), zone_max=self.zone_max)
+
+    def next_interval(self) -> Dict[str, np.ndarray]:
+        L, rng = self.layout, self._rng
+        P = L.n_procs
+        first = self.interval == 0
+        out = self.next_node_inputs()
+        # processes: cumulative ticks -> Go's CPUTimeDelta = ticks/100 - prev
+        dticks = np.where(rng.random(P) < 0.3, 0,
+                          np.minimum(rng.lognormal(3.0, 1.5, size=P), 50_000.0)).astype(np.int64)
+        proc_slot = L.proc_slot.copy()
+        if first:
+            proc_slot |= np.uint32(KACC_SLOT_NEW)
+        elif self.churn > 0:
+            born = rng.random(P) < self.churn  # PID reuse of the slot by a new process
+            self.cum_ticks[born] = 0
+            self.prev_total[born] = 0.0
+            proc_slot[born] |= np.uint32(KACC_SLOT_NEW)
+        self.cum_ticks += dticks
+        total = self.cum_ticks.astype(np.float64) / 100.0
+        cpu_delta = total - self.prev_total
+        self.prev_total = total
+        flag = np.uint32(KACC_SLOT_NEW) if first else np.uint32(0)
+        self.interval += 1
+        out.update(
+            proc_cpu_delta=cpu_delta,
+            proc_slot=proc_slot,
+            ctr_slot=L.ctr_slot | flag,
+            vm_slot=L.vm_slot | flag,
+            pod_slot=L.pod_slot | flag,
+        )
+        out.update(L.static_arrays())
+        return out
+
+
+def _ranges(off: np.ndarray, nodes: np.ndarray):
+    off = off.astype(np.int64)
+    lo, hi = off[nodes], off[nodes + 1]
+    idx = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]) if len(nodes) else np.zeros(0, np.int64)
+    new_off = np.zeros(len(nodes) + 1, dtype=np.int64)
+    np.cumsum(hi - lo, out=new_off[1:])
+    return idx.astype(np.int64), lo, new_off
+
+
+def subset_interval(a: Dict[str, np.ndarray], nodes: np.ndarray, zones: int):
+    """Extract the given nodes of a batch into a compact batch.
+
+    Node snapshots are independent, so the oracle can check a sample of a
+    full-size fleet.  Returns (arrays, sizes, maps) where maps[kind] are the
+    original slot ids in compact-slot order (compact slot i <-> original
+    maps[kind][i]) and maps["node"] the original node ids.
+    """
+    nodes = np.asarray(nodes, dtype=np.int64)
+    out: Dict[str, np.ndarray] = {}
+    pidx, p_lo, p_new = _ranges(a["proc_off"], nodes)
+    cidx, c_lo, c_new = _ranges(a["ctr_off"], nodes)
+    vidx, _, v_new = _ranges(a["vm_off"], nodes)
+    qidx, _, q_new = _ranges(a["pod_off"], nodes)
+    u32 = lambda x: np.ascontiguousarray(x, dtype=np.uint32)  # noqa: E731
+    zidx = (nodes[:, None] * zones + np.arange(zones)[None, :]).reshape(-1)
+    for name in ("node_ts_ns", "node_usage_ratio", "node_status", "node_cpu_delta"):
+        if a.get(name) is not None:
+            out[name] = np.ascontiguousarray(a[name][nodes])
+    out["zone_energy"] = np.ascontiguousarray(a["zone_energy"][zidx])
+    out["zone_max"] = np.ascontiguousarray(a["zone_max"][zidx])
+    out["proc_off"], out["ctr_off"] = u32(p_new), u32(c_new)
+    out["vm_off"], out["pod_off"] = u32(v_new), u32(q_new)
+    out["proc_cpu_delta"] = np.ascontiguousarray(a["proc_cpu_delta"][pidx])
+    # row shifts per node
+    shift_p = np.repeat(p_new[:-1] - p_lo, np.diff(c_new))
+    out["ctr_proc_end"] = u32(a["ctr_proc_end"][cidx].astype(np.int64) + shift_p)
+    shift_pv = np.repeat(p_new[:-1] - p_lo, np.diff(v_new))
+    out["vm_proc_end"] = u32(a["vm_proc_end"][vidx].astype(np.int64) + shift_pv)
+    shift_c = np.repeat(c_new[:-1] - c_lo, np.diff(q_new))
+    out["pod_ctr_end"] = u32(a["pod_ctr_end"][qidx].astype(np.int64) + shift_c)
+    maps = {"node": nodes}
+    for kind, idx in (("proc", pidx), ("ctr", cidx), ("vm", vidx), ("pod", qidx)):
+        w = a[f"{kind}_slot"][idx].astype(np.uint32)
+        orig = (w & np.uint32(0x7FFFFFFF)).astype(np.int64)
+        out[f"{kind}_slot"] = u32(np.arange(len(idx), dtype=np.int64) | (w & np.uint32(0x80000000)))
+        maps[kind] = orig
+    sizes = dict(n_nodes=len(nodes), n_procs=len(pidx), n_ctrs=len(cidx), n_vms=len(vidx), n_pods=len(qidx))
+    return out, sizes, maps

@@ -1,0 +1,165 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/build/libkepler_oracle.so, the CPU restatement of
+Kepler's attribution path.  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg import this module, as the checker or the CPU
+baseline; the product path (kepler_amd) never does.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_int, c_int64, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+from kepler_amd.accel import TABLES, KaccInterval, make_interval
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libkepler_oracle.so")
+
+KOR_SUM_TREE256 = 0
+KOR_SUM_LISTING = 1
+
+
+class KorState(ctypes.Structure):
+    _fields_ = [("zones", c_uint32), ("reserved0", c_uint32), ("nodes", c_uint64),
+                ("proc_slots", c_uint64), ("ctr_slots", c_uint64), ("vm_slots", c_uint64),
+                ("pod_slots", c_uint64)] + [(name, c_void_p) for name, _ in TABLES]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.kor_go_f64_to_u64.argtypes = [c_double]
+    lib.kor_go_f64_to_u64.restype = c_uint64
+    lib.kor_go_duration_seconds.argtypes = [c_int64]
+    lib.kor_go_duration_seconds.restype = c_double
+    lib.kor_calculate_energy_delta.argtypes = [c_uint64, c_uint64, c_uint64]
+    lib.kor_calculate_energy_delta.restype = c_uint64
+    lib.kor_interval.argtypes = [POINTER(KorState), POINTER(KaccInterval), c_int]
+    lib.kor_namespace_totals.argtypes = [POINTER(KorState), c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kor_aggregated_max.argtypes = [c_uint32, c_void_p]
+    lib.kor_aggregated_max.restype = c_uint64
+    lib.kor_aggregated_energy.argtypes = [c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]
+    lib.kor_aggregated_energy.restype = c_uint64
+    lib.kor_gf_create.argtypes = [c_uint32]
+    lib.kor_gf_create.restype = c_void_p
+    lib.kor_gf_destroy.argtypes = [c_void_p]
+    lib.kor_gf_destroy.restype = None
+    lib.kor_gf_interval.argtypes = [c_void_p, POINTER(KorState), POINTER(KaccInterval)]
+    _lib = lib
+    return lib
+
+
+def go_f64_to_u64(x: float) -> int:
+    return int(load().kor_go_f64_to_u64(x))
+
+
+def go_duration_seconds(ns: int) -> float:
+    return float(load().kor_go_duration_seconds(ns))
+
+
+def calculate_energy_delta(cur: int, prev: int, max_j: int) -> int:
+    return int(load().kor_calculate_energy_delta(cur, prev, max_j))
+
+
+class OracleState:
+    """Host state tables with the same layout as the device tables."""
+
+    def __init__(self, zones, nodes, proc_slots, ctr_slots, vm_slots, pod_slots):
+        self.zones = zones
+        per = {"node": nodes, "proc": proc_slots, "ctr": ctr_slots, "vm": vm_slots, "pod": pod_slots}
+        zoned = {"energy", "power", "energy_total", "active_energy", "active_total", "idle_total",
+                 "active_power", "idle_power"}
+        self.t = {}
+        for name, dt in TABLES:
+            kind, rest = name.split("_", 1)
+            n = per[kind] * (zones if rest in zoned else 1)
+            self.t[name] = np.zeros(max(n, 1), dtype=dt)[:n] if n else np.zeros(0, dtype=dt)
+        self.c = KorState(zones, 0, nodes, proc_slots, ctr_slots, vm_slots, pod_slots,
+                          *[self.t[name].ctypes.data for name, _ in TABLES])
+
+    def __getitem__(self, name):
+        return self.t[name]
+
+    def copy_tables(self):
+        return {k: v.copy() for k, v in self.t.items()}
+
+
+class Oracle:
+    def __init__(self, zones, nodes, proc_slots, ctr_slots, vm_slots, pod_slots, sum_mode=KOR_SUM_TREE256):
+        self.lib = load()
+        self.state = OracleState(zones, nodes, proc_slots, ctr_slots, vm_slots, pod_slots)
+        self.sum_mode = sum_mode
+
+    def interval(self, arrays: dict, sizes: dict, flags: int = 0) -> None:
+        it = make_interval(arrays, sizes, flags)
+        rc = self.lib.kor_interval(ctypes.byref(self.state.c), ctypes.byref(it), self.sum_mode)
+        if rc != 0:
+            raise RuntimeError(f"kor_interval failed: {rc}")
+
+    def namespace_totals(self, ns_off: np.ndarray, ns_slot: np.ndarray):
+        n_ns = len(ns_off) - 1
+        e = np.zeros(n_ns * self.state.zones, dtype=np.uint64)
+        p = np.zeros(n_ns * self.state.zones, dtype=np.float64)
+        ns_off = np.ascontiguousarray(ns_off, dtype=np.uint32)
+        ns_slot = np.ascontiguousarray(ns_slot, dtype=np.uint32)
+        self.lib.kor_namespace_totals(ctypes.byref(self.state.c), n_ns, ns_off.ctypes.data,
+                                      ns_slot.ctypes.data, e.ctypes.data, p.ctypes.data)
+        return e, p
+
+
+class GoFaithful:
+    """The Go-data-structure baseline (string-keyed maps, per-object zone maps)."""
+
+    def __init__(self, zones, nodes, proc_slots, ctr_slots, vm_slots, pod_slots):
+        self.lib = load()
+        self.state = OracleState(zones, nodes, proc_slots, ctr_slots, vm_slots, pod_slots)
+        self.h = self.lib.kor_gf_create(zones)
+
+    def interval(self, arrays: dict, sizes: dict, flags: int = 0) -> None:
+        it = make_interval(arrays, sizes, flags)
+        rc = self.lib.kor_gf_interval(self.h, ctypes.byref(self.state.c), ctypes.byref(it))
+        if rc != 0:
+            raise RuntimeError(f"kor_gf_interval failed: {rc}")
+
+    def close(self):
+        if self.h:
+            self.lib.kor_gf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+class AggregatedZone:
+    """device/energy_zone.go:97-148 over n sub-zones (KAT helper)."""
+
+    def __init__(self, sub_max):
+        self.lib = load()
+        self.sub_max = np.ascontiguousarray(sub_max, dtype=np.uint64)
+        self.n = len(self.sub_max)
+        self.last = np.zeros(self.n, dtype=np.uint64)
+        self.seen = np.zeros(self.n, dtype=np.uint8)
+        self.current = np.zeros(1, dtype=np.uint64)
+        self.max = int(self.lib.kor_aggregated_max(self.n, self.sub_max.ctypes.data))
+
+    def energy(self, readings) -> int:
+        r = np.ascontiguousarray(readings, dtype=np.uint64)
+        return int(self.lib.kor_aggregated_energy(self.n, r.ctypes.data, self.sub_max.ctypes.data,
+                                                  self.last.ctypes.data, self.seen.ctypes.data,
+                                                  self.current.ctypes.data, self.max))

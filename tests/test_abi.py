@@ -1,0 +1,83 @@
+"""The C-ABI library: loads, exports every declared symbol, struct layout (CPU)."""
+
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from kepler_amd import accel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kepler_accel.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kacc_[a-z_0-9]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(accel.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "kepler_amd", "csrc")], check=True)
+    return accel.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    decl = declared_functions()
+    assert sorted(accel.EXPORTS) == decl
+    for name in decl:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", accel.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (kacc_\w+)", out))
+    assert set(decl) <= exported
+
+
+def test_abi_version(lib):
+    assert lib.kacc_abi_version() == accel.KACC_ABI_VERSION
+
+
+def test_struct_layout_matches_header(tmp_path):
+    c = tmp_path / "layout.c"
+    fields = ["n_nodes", "flags"] + accel.INTERVAL_ARRAYS
+    body = "\n".join(f'printf("%zu\\n", offsetof(kacc_interval, {f}));' for f in fields)
+    c.write_text(f"""
+#include <stddef.h>
+#include <stdio.h>
+#include "kepler_accel.h"
+int main(void) {{
+  printf("%zu\\n%zu\\n", sizeof(kacc_interval), sizeof(kacc_config));
+  printf("%zu\\n", offsetof(kacc_config, nodes));
+  {body}
+  return 0;
+}}""")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(accel.KaccInterval)
+    assert vals[1] == ctypes.sizeof(accel.KaccConfig)
+    assert vals[2] == accel.KaccConfig.nodes.offset
+    for f, off in zip(fields, vals[3:]):
+        assert getattr(accel.KaccInterval, f).offset == off, f
+
+
+def test_interval_bytes_formula(lib):
+    # node 76+96Z, proc 12+24Z, ctr 32+24Z, vm 16+24Z, pod 32+24Z
+    z = 4
+    assert accel.interval_bytes(z, 1, 0, 0, 0, 0) == 76 + 96 * z
+    assert accel.interval_bytes(z, 0, 1, 0, 0, 0) == 12 + 24 * z
+    assert accel.interval_bytes(z, 0, 0, 1, 1, 1) == (32 + 16 + 32) + 3 * 24 * z
+    n, p, c, v, q = 10_000, 20_000_000, 1_975_000, 200_000, 711_000
+    assert accel.interval_bytes(z, n, p, c, v, q) == n * 460 + p * 108 + c * 128 + v * 112 + q * 128
+
+
+def test_bad_arguments_do_not_crash(lib):
+    cfg = accel.KaccConfig(0, 0, 1, 1, 1, 1, 1)  # zones = 0 is invalid
+    h = ctypes.c_void_p()
+    assert lib.kacc_create(0, ctypes.byref(cfg), ctypes.byref(h)) == accel.KACC_EINVAL
+    assert b"zones" in lib.kacc_last_error(None)
+    assert lib.kacc_reset(None) == accel.KACC_EINVAL
+    assert lib.kacc_run_interval(None, None, None) == accel.KACC_EINVAL

@@ -1,0 +1,220 @@
+"""Parity of the HIP engine (through the C ABI) with the oracle — MI355X only.
+
+Integer tables (energies, counters, statuses) must be bit-exact.  Float64
+tables are bit-exact too against the oracle in the engine's canonical
+summation order; against the listing-order sum (one of Go's map orders) the
+tolerance is the north star's: <= 1e-12 relative on totals and <= 1 µJ per
+workload.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from kat_runner import load_golden_fleet, load_kats, run_case
+from kepler_amd import accel, fleet
+from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+pytestmark = pytest.mark.gpu
+
+KATS = load_kats()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_ready():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    accel.load()  # raises if the HIP library is missing: no fallback
+
+
+class EngineBackend:
+    """Device-pointer path: kacc_run_interval on torch's current stream."""
+
+    def __init__(self, zones, caps):
+        self.acc = accel.Accel(zones, **caps)
+
+    def upload(self, table, first, values):
+        self.acc.upload(table, np.array(values), first)
+
+    def interval(self, arrays, sizes, flags):
+        t = to_device(arrays)
+        it = interval_from_tensors(t, sizes, flags)
+        s = current_stream_handle()
+        self.acc.run_interval(it, s)
+        self.acc.sync(s)
+
+    def table(self, name):
+        return self.acc.download(name)
+
+
+class HostBatchBackend(EngineBackend):
+    """Pinned host path: kacc_batch_alloc / submit / wait (the cgo path)."""
+
+    def interval(self, arrays, sizes, flags):
+        b = accel.HostBatch.alloc(self.acc, **sizes)
+        try:
+            b.fill(arrays, flags)
+            b.submit()
+            b.wait()
+        finally:
+            b.free()
+
+
+@pytest.mark.parametrize("case", KATS["cases"], ids=[c["name"] for c in KATS["cases"]])
+def test_engine_kat(case):
+    run_case(case, EngineBackend)
+
+
+@pytest.mark.parametrize("case", KATS["cases"], ids=[c["name"] for c in KATS["cases"]])
+def test_engine_kat_host_batch(case):
+    run_case(case, HostBatchBackend)
+
+
+def test_golden_fleet_bit_exact():
+    zones, caps, sizes, intervals = load_golden_fleet()
+    be = EngineBackend(zones, caps)
+    for k, (ins, outs) in enumerate(intervals):
+        be.interval(ins, sizes, 0)
+        for name, want in outs.items():
+            np.testing.assert_array_equal(be.table(name), want, err_msg=f"interval {k} {name}")
+
+
+def run_both(layout, sim_kwargs, n_intervals, node_order=False, seed=1):
+    from oracle.oracle import KOR_SUM_LISTING, Oracle
+
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=seed, **sim_kwargs)
+    eng = EngineBackend(layout.zones, caps)
+    ora = Oracle(layout.zones, **caps)
+    lst = Oracle(layout.zones, **caps, sum_mode=KOR_SUM_LISTING)
+    for _ in range(n_intervals):
+        a = sim.next_interval()
+        if node_order:
+            a["node_order"] = layout.node_order_heaviest_first()
+        eng.interval(a, layout.sizes(), 0)
+        ora.interval(a, layout.sizes())
+        lst.interval(a, layout.sizes())
+        for name, _ in accel.TABLES:
+            np.testing.assert_array_equal(eng.table(name), ora.state[name], err_msg=name)
+    return eng, ora, lst
+
+
+FLEETS = [
+    ("z1-small", dict(n_nodes=5, procs_per_node=[1, 0, 40, 300, 7], zones=1)),
+    ("z2-config2-like", dict(n_nodes=64, procs_per_node=1000, zones=2)),
+    ("z3-odd", dict(n_nodes=33, procs_per_node=257, zones=3, procs_per_vm=3, vm_frac=0.05)),
+    ("z4-config3-like", dict(n_nodes=48, procs_per_node=2000, zones=4, shuffle_slots=True)),
+    ("z8-max-zones", dict(n_nodes=9, procs_per_node=511, zones=8)),
+    ("z4-skew", dict(n_nodes=6, procs_per_node=[10000, 50000, 12000, 31000, 10, 0], zones=4,
+                     procs_per_vm=2, vm_frac=0.02)),
+]
+
+
+@pytest.mark.parametrize("name,kw", FLEETS, ids=[f[0] for f in FLEETS])
+def test_random_fleet_bit_exact(name, kw):
+    layout = fleet.make_layout(seed=11, **kw)
+    eng, ora, lst = run_both(layout, dict(churn=0.03, zero_ratio_frac=0.05, read_error_frac=0.05), 4)
+    # listing-order (Go map order) oracle: <= 1e-12 relative on the node totals,
+    # <= 1 µJ per workload energy
+    nd_e, nd_l = eng.table("node_cpu_delta"), lst.state["node_cpu_delta"]
+    np.testing.assert_allclose(nd_e, nd_l, rtol=1e-12, atol=0)
+    for kind in ("proc", "ctr", "vm", "pod"):
+        de = eng.table(f"{kind}_energy").astype(np.int64) - lst.state[f"{kind}_energy"].astype(np.int64)
+        assert np.abs(de).max(initial=0) <= 1, kind
+        np.testing.assert_allclose(eng.table(f"{kind}_power"), lst.state[f"{kind}_power"], rtol=1e-12, atol=1e-6)
+
+
+def test_wrapping_fake_meter_and_node_order():
+    layout = fleet.make_layout(40, [0, 1, 2, 3, 500, 2000, 64, 65] * 5, 2, seed=3, shuffle_slots=True)
+    run_both(layout, dict(max_energy=fleet.MAX_ENERGY_FAKE, churn=0.1), 5, node_order=True, seed=5)
+
+
+def test_node_cpu_delta_given():
+    layout = fleet.make_layout(16, 300, 2, seed=9)
+    from oracle.oracle import Oracle
+
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=9)
+    eng = EngineBackend(layout.zones, caps)
+    ora = Oracle(layout.zones, **caps)
+    for k in range(3):
+        a = sim.next_interval()
+        a["node_cpu_delta"] = np.full(layout.n_nodes, 1234.5 + k)
+        eng.interval(a, layout.sizes(), accel.KACC_F_NODE_CPU_DELTA_GIVEN)
+        ora.interval(a, layout.sizes(), accel.KACC_F_NODE_CPU_DELTA_GIVEN)
+        for name, _ in accel.TABLES:
+            np.testing.assert_array_equal(eng.table(name), ora.state[name], err_msg=name)
+
+
+def test_namespace_totals_match_oracle():
+    layout = fleet.make_layout(32, 800, 4, seed=13, n_namespaces=7)
+    eng, ora, _ = run_both(layout, dict(churn=0.0), 3)
+    off, slots = layout.namespace_csr()
+    e_o, p_o = ora.namespace_totals(off, slots)
+    d_off, d_slots = to_device({"o": off, "s": slots})["o"], to_device({"s": slots})["s"]
+    out_e = torch.zeros(len(e_o), dtype=torch.int64, device="cuda")
+    out_p = torch.zeros(len(p_o), dtype=torch.float64, device="cuda")
+    s = current_stream_handle()
+    eng.acc.namespace_totals(len(off) - 1, d_off.data_ptr(), d_slots.data_ptr(), out_e.data_ptr(),
+                             out_p.data_ptr(), s)
+    eng.acc.sync(s)
+    np.testing.assert_array_equal(out_e.cpu().numpy().view(np.uint64), e_o)
+    np.testing.assert_array_equal(out_p.cpu().numpy(), p_o)
+
+
+def test_out_of_range_slot_is_reported_not_faulted():
+    layout = fleet.make_layout(4, 100, 2, seed=17)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=17)
+    eng = EngineBackend(layout.zones, caps)
+    a = sim.next_interval()
+    a["proc_slot"] = a["proc_slot"].copy()
+    a["proc_slot"][5] = (caps["proc_slots"] + 100) | accel.KACC_SLOT_NEW
+    t = to_device(a)
+    it = interval_from_tensors(t, layout.sizes())
+    s = current_stream_handle()
+    eng.acc.run_interval(it, s)
+    with pytest.raises(accel.AccelError) as ei:
+        eng.acc.sync(s)
+    assert ei.value.code == accel.KACC_ERANGE
+    # host validation rejects the same batch before it reaches the GPU
+    assert eng.acc.validate_host(accel.make_interval(a, layout.sizes())) == accel.KACC_EINVAL
+
+
+@pytest.mark.slow
+def test_config3_full_size_properties_and_sampled_parity():
+    """10k nodes x 2k procs, Z=4 (BASELINE config 3) through 3 intervals:
+    size-independent properties on every node + oracle parity on a sample."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.config_layout(3)
+    Z = layout.zones
+    sim = fleet.FleetSim(layout, seed=21)
+    eng = EngineBackend(Z, layout.capacities())
+    rng = np.random.default_rng(0)
+    sample = np.sort(rng.choice(layout.n_nodes, 40, replace=False))
+    ora = None
+    for k in range(3):
+        a = sim.next_interval()
+        eng.interval(a, layout.sizes(), 0)
+        sub, sub_sizes, maps = fleet.subset_interval(a, sample, Z)
+        if ora is None:
+            ora = Oracle(Z, nodes=len(sample), proc_slots=sub_sizes["n_procs"], ctr_slots=sub_sizes["n_ctrs"],
+                         vm_slots=sub_sizes["n_vms"], pod_slots=sub_sizes["n_pods"])
+        ora.interval(sub, sub_sizes)
+    # sampled parity (bit exact)
+    for name, _ in accel.TABLES:
+        kind = name.split("_")[0]
+        full = eng.table(name)
+        per = len(full) // (layout.n_nodes if kind == "node" else layout.capacities()[f"{kind}_slots"])
+        idx = maps[kind]
+        got = full.reshape(-1, per)[idx].reshape(-1)
+        np.testing.assert_array_equal(got, ora.state[name], err_msg=name)
+    # conservation on every node: sum of process power == ActivePower (rel 1e-9),
+    # sum of process interval energy within [aE - rows, aE]
+    ap = eng.table("node_active_power").reshape(-1, Z)
+    pp = eng.table("proc_power").reshape(-1, Z)
+    off = layout.proc_off.astype(np.int64)
+    sums = np.add.reduceat(pp[layout.proc_slot], off[:-1], axis=0)
+    nd = eng.table("node_cpu_delta")
+    ok = (nd != 0)[:, None] & (ap != 0)
+    assert np.all(np.abs(sums - ap)[ok] <= 1e-9 * np.abs(ap)[ok])
