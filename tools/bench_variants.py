@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Interleaved timing of interval-kernel ablation variants on config 3 (one process).
+
+Variants (kacc_debug.h): 0 production, 1 skip aggregates, 2 skip processes,
+3 node phases only, 4 unstaged, 8 non-temporal stores, 9 = 1|8.
+Also times the namespace kernel.  Prints a JSON summary.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch
+
+    from kepler_amd import accel, fleet
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,1,2,3,4,8").split(",")]
+    rounds = int(os.environ.get("ROUNDS", "10"))
+    cfg = int(os.environ.get("CONFIG", "3"))
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    layout = fleet.config_layout(cfg)
+    sim = fleet.FleetSim(layout)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    stream = current_stream_handle()
+    assert stream != 0
+    prime = to_device(sim.next_interval())
+    acc.run_interval(interval_from_tensors(prime, layout.sizes()), stream)
+    a = to_device(sim.next_interval())
+    it = interval_from_tensors(a, layout.sizes())
+    Z = layout.zones
+    sizes = layout.sizes()
+    nbytes = accel.interval_bytes(Z, *[sizes[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
+    times = {v: [] for v in variants}
+    for v in variants:  # warm
+        acc.run_variant(it, stream, v)
+    acc.sync(stream)
+    for _ in range(rounds):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            acc.run_variant(it, stream, v)
+            e1.record()
+            e1.synchronize()
+            times[v].append(e0.elapsed_time(e1))
+    acc.sync(stream)
+    off, slots = layout.namespace_csr()
+    ns = to_device({"o": off, "s": slots})
+    n_ns = len(off) - 1
+    oe = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
+    op = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
+    ns_t = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        acc.namespace_totals(n_ns, ns["o"].data_ptr(), ns["s"].data_ptr(), oe.data_ptr(), op.data_ptr(), stream)
+        e1.record()
+        e1.synchronize()
+        ns_t.append(e0.elapsed_time(e1))
+    acc.sync(stream)
+    out = {"config": cfg, "sizes": sizes, "bytes_per_launch": nbytes,
+           "variants": {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for v, t in times.items()},
+           "namespace_ms": float(np.median(ns_t))}
+    if 0 in times:
+        out["achieved_GBps_v0"] = nbytes / (np.median(times[0]) * 1e-3) / 1e9
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
