@@ -99,6 +99,9 @@ def main():
     import torch.distributed as dist
 
     torch.cuda.set_device(local)
+    # an explicit stream: the engine launches on it and the HIP events below
+    # time exactly that stream (a NULL handle would mean the context's stream)
+    torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
@@ -122,6 +125,7 @@ def main():
 
     acc = accel.Accel(Z, **layout.capacities(), device=local)
     stream = current_stream_handle()
+    assert stream != 0
     statics = to_device(layout.static_arrays())
     dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
                 for a in full]

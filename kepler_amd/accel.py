@@ -208,6 +208,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     ]
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
+    lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
     if lib.kacc_abi_version() != KACC_ABI_VERSION:
         raise ImportError("libkepler_accel ABI version mismatch")
     _lib = lib
@@ -288,6 +289,11 @@ class Accel:
 
     def run_interval(self, dev_interval: KaccInterval, stream: int = 0) -> None:
         self._check(self.lib.kacc_run_interval(self.ctx, ctypes.byref(dev_interval), c_void_p(stream or None)))
+
+    def run_variant(self, dev_interval: KaccInterval, stream: int, variant: int) -> None:
+        """Timing ablation (kacc_debug.h); variant != 0 is not the reference semantics."""
+        self._check(self.lib.kacc_debug_run_variant(self.ctx, ctypes.byref(dev_interval),
+                                                    c_void_p(stream or None), variant))
 
     def sync(self, stream: int = 0) -> None:
         self._check(self.lib.kacc_sync(self.ctx, c_void_p(stream or None)))

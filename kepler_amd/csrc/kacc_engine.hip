@@ -28,12 +28,24 @@
 #include <vector>
 
 #include "../../include/kepler_accel.h"
+#include "kacc_debug.h"
 #include "kacc_device.hpp"
 
 namespace kacc {
 
-constexpr int kBlock = 256;  // lanes of the canonical node-total tree
-constexpr int kUnroll = 4;   // process rows in flight per lane
+constexpr int kBlock = 256;                  // lanes of the canonical node-total tree
+constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
+constexpr int kLoadsPerLane = kRowsLds / kBlock;
+constexpr int kCtrLds = 512;                 // container Δ / total staged in LDS
+constexpr int kUnroll = 4;                   // process rows in flight per lane (attribution)
+constexpr int kNsWave = 64;                  // lanes per namespace (namespace_kernel)
+
+// Debug variants (kacc_debug_run_variant, timing ablations only; results of a
+// variant != 0 are NOT the reference semantics).
+constexpr int kVarSkipAggregates = 1;  // skip containers / VMs / pods
+constexpr int kVarSkipProcs = 2;       // skip the process attribution pass
+constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
+constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
 
 // device error bits (KACC_ERANGE)
 constexpr uint32_t kErrNode = 1u << 0;
@@ -65,14 +77,21 @@ struct NodeShared {
   double power[KACC_MAX_ZONES];
   double active_power[KACC_MAX_ZONES];
   double node_delta;
+  uint32_t first;
 };
 
 __device__ __forceinline__ void raise_err(uint32_t *err, uint32_t bit) { atomicOr(err, bit); }
 
-template <int Z>
-struct ZoneRow {  // one workload's zones, loaded/stored as 16-B vectors when Z is even
-  uint64_t v[Z];
-};
+// Block-uniform values live in SGPRs (saves VGPRs for rows in flight).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ double uniform_f64(double x) {
+  return __longlong_as_double(static_cast<long long>(uniform_u64(static_cast<uint64_t>(__double_as_longlong(x)))));
+}
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
 template <int Z>
 __device__ __forceinline__ void load_row(const uint64_t *__restrict__ base, uint64_t s,
@@ -92,7 +111,7 @@ __device__ __forceinline__ void load_row(const uint64_t *__restrict__ base, uint
   }
 }
 
-template <int Z, typename T>
+template <int Z, bool NT, typename T>
 __device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, const T (&in)[Z]) {
   if constexpr (Z % 2 == 0) {
     using v2 = __attribute__((ext_vector_type(2))) T;
@@ -102,23 +121,31 @@ __device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, cons
       v2 x;
       x.x = in[2 * k];
       x.y = in[2 * k + 1];
-      p[k] = x;
+      if constexpr (NT)
+        __builtin_nontemporal_store(x, p + k);
+      else
+        p[k] = x;
     }
   } else {
 #pragma unroll
-    for (int z = 0; z < Z; ++z) base[s * Z + z] = in[z];
+    for (int z = 0; z < Z; ++z) {
+      if constexpr (NT)
+        __builtin_nontemporal_store(in[z], base + s * Z + z);
+      else
+        base[s * Z + z] = in[z];
+    }
   }
 }
 
-// Node-uniform attribution parameters, held in registers for the row passes.
+// Node-uniform attribution parameters (SGPRs) for the row passes.
 template <int Z>
 struct Attr {
-  uint64_t aE[Z];   // NodeUsage.activeEnergy
-  double aP[Z];     // NodeUsage.ActivePower
-  uint32_t live;    // bit z: zone passes the guard (ActivePower/Power, activeEnergy, ΔcpuNode)
-  uint32_t live_pod;
-  double nd;        // ProcessTotalCPUTimeDelta
-  bool first;       // first*Read variant: EnergyTotal = interval energy, Power 0
+  uint64_t aE[Z];  // NodeUsage.activeEnergy
+  double aP[Z];    // NodeUsage.ActivePower
+  uint32_t live;   // bit z: zone passes the guard (ActivePower, activeEnergy, ΔcpuNode)
+  uint32_t live_pod;  // pod.go:96 guards on Power instead of ActivePower
+  double nd;       // ProcessTotalCPUTimeDelta
+  uint32_t first;  // first*Read variant: EnergyTotal = interval energy, Power 0
 };
 
 // process.go:118-148 (and its container/VM/pod twins) for one row.
@@ -140,11 +167,28 @@ __device__ __forceinline__ void attribute_row(const Attr<Z> &a, uint32_t live, d
   }
 }
 
-template <int Z>
+// One aggregate row (container / VM / pod): read-modify-write of its slot.
+template <int Z, bool NT>
+__device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, double delta,
+                                               uint32_t w, uint64_t *__restrict__ energy,
+                                               double *__restrict__ power) {
+  const uint64_t s = w & KACC_SLOT_MASK;
+  uint64_t prev[Z], E[Z];
+  double P[Z];
+  load_row<Z>(energy, s, prev);
+  attribute_row<Z>(a, live, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
+  store_row<Z, NT, uint64_t>(energy, s, E);
+  store_row<Z, NT, double>(power, s, P);
+}
+
+template <int Z, int V>
 __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b, const DevState st) {
-  __shared__ NodeShared sh;
+  constexpr bool kNT = (V & kVarNtStores) != 0;
+  __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
+  __shared__ double s_cd[kCtrLds];   // container Δ of this interval
+  __shared__ double s_ct[kCtrLds];   // container running CPU total
   __shared__ double red[kBlock];
-  __shared__ uint32_t sh_first;
+  __shared__ NodeShared sh;
 
   const int tid = threadIdx.x;
   uint32_t n = blockIdx.x;
@@ -160,11 +204,31 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
     return;
   }
 
-  // ---- A: node zones --------------------------------------------------------
-  if (tid == 0) sh_first = st.node_has_prev[n] == 0u ? 1u : 0u;
-  __syncthreads();
-  const bool first = sh_first != 0u;
+  // ---- row ranges (clamped so a malformed batch cannot fault) ---------------
+  uint32_t p0 = b.proc_off[n], p1 = b.proc_off[n + 1];
+  uint32_t c0 = b.ctr_off[n], c1 = b.ctr_off[n + 1];
+  uint32_t v0 = b.vm_off[n], v1 = b.vm_off[n + 1];
+  uint32_t q0 = b.pod_off[n], q1 = b.pod_off[n + 1];
+  if (p1 > b.n_procs || p0 > p1 || c1 > b.n_ctrs || c0 > c1 || v1 > b.n_vms || v0 > v1 ||
+      q1 > b.n_pods || q0 > q1) {
+    if (tid == 0) raise_err(st.err, kErrOffsets);
+    p1 = min(p1, b.n_procs);
+    p0 = min(p0, p1);
+    c1 = min(c1, b.n_ctrs);
+    c0 = min(c0, c1);
+    v1 = min(v1, b.n_vms);
+    v0 = min(v0, v1);
+    q1 = min(q1, b.n_pods);
+    q0 = min(q0, q1);
+  }
+  const uint32_t rows = p1 - p0;
+  const bool staged = (V & kVarUnstaged) == 0 && rows <= static_cast<uint32_t>(kRowsLds);
+  const bool cstaged = (c1 - c0) <= static_cast<uint32_t>(kCtrLds);
+  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;  // node-local row index
+
+  // ---- A: node zones (threads z < Z) ----------------------------------------
   if (tid < Z) {
+    const bool first = st.node_has_prev[n] == 0u;
     const uint64_t i = static_cast<uint64_t>(n) * Z + tid;
     const double ratio = b.node_usage_ratio[n];
     const uint64_t abs_e = b.zone_energy[i];
@@ -192,240 +256,262 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
     sh.active_energy[tid] = active;
     sh.power[tid] = p;
     sh.active_power[tid] = ap;
+    if (tid == 0) sh.first = first ? 1u : 0u;
   }
 
-  // ---- row ranges (clamped so a malformed batch cannot fault) ---------------
-  uint32_t p0 = b.proc_off[n], p1 = b.proc_off[n + 1];
-  uint32_t c0 = b.ctr_off[n], c1 = b.ctr_off[n + 1];
-  uint32_t v0 = b.vm_off[n], v1 = b.vm_off[n + 1];
-  uint32_t q0 = b.pod_off[n], q1 = b.pod_off[n + 1];
-  if (p1 > b.n_procs || p0 > p1 || c1 > b.n_ctrs || c0 > c1 || v1 > b.n_vms || v0 > v1 ||
-      q1 > b.n_pods || q0 > q1) {
-    if (tid == 0) raise_err(st.err, kErrOffsets);
-    p1 = min(p1, b.n_procs);
-    p0 = min(p0, p1);
-    c1 = min(c1, b.n_ctrs);
-    c0 = min(c0, c1);
-    v1 = min(v1, b.n_vms);
-    v0 = min(v0, v1);
-    q1 = min(q1, b.n_pods);
-    q0 = min(q0, q1);
+  // ---- B: stage Δcpu, ProcessTotalCPUTimeDelta (informer.go:330-333) --------
+  // Lane l sums rows l, l+256, l+512, ... in order; loads are issued
+  // kLoadsPerLane at a time (independent), the adds stay sequential.
+  double s = 0.0;
+  for (uint32_t base = 0; base < rows; base += kRowsLds) {
+    double v[kLoadsPerLane];
+#pragma unroll
+    for (int k = 0; k < kLoadsPerLane; ++k) {
+      const uint32_t i = base + tid + k * kBlock;
+      v[k] = i < rows ? dcpu[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kLoadsPerLane; ++k) {
+      const uint32_t i = base + tid + k * kBlock;
+      if (i < rows) {
+        if (staged) s_d[i] = v[k];
+        s = s + v[k];
+      }
+    }
   }
-  const double *__restrict__ dcpu = b.proc_cpu_delta;
-
-  // ---- B: ProcessTotalCPUTimeDelta (informer.go:330-333) -------------------
+  red[tid] = s;
+  __syncthreads();
   if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
     if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
   } else {
-    double s = 0.0;
-    for (uint32_t r = p0 + tid; r < p1; r += kBlock) s += dcpu[r];
-    red[tid] = s;
-    __syncthreads();
     if (tid < 128) red[tid] = red[tid] + red[tid + 128];
     __syncthreads();
     if (tid < 64) {
-      double v = red[tid] + red[tid + 64];
+      double x = red[tid] + red[tid + 64];
 #pragma unroll
-      for (int k = 32; k >= 1; k >>= 1) v = v + __shfl_down(v, k, 64);
-      if (tid == 0) sh.node_delta = v;
+      for (int k = 32; k >= 1; k >>= 1) x = x + __shfl_down(x, k, 64);
+      if (tid == 0) sh.node_delta = x;
     }
   }
+  auto row_delta = [&](uint32_t i) -> double { return staged ? s_d[i] : dcpu[i]; };
 
-  // ---- C: containers and VMs (segmented, one lane per segment) --------------
-  const uint32_t ctr_rows_end = c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0;
-  for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
-    uint32_t beg = c == c0 ? p0 : b.ctr_proc_end[c - 1];
-    uint32_t end = b.ctr_proc_end[c];
-    const uint32_t w = b.ctr_slot[c];
-    const uint64_t s = w & KACC_SLOT_MASK;
-    if (beg < p0 || end < beg || end > p1 || s >= st.ctr_slots) {
-      raise_err(st.err, s >= st.ctr_slots ? kErrSlot : kErrOffsets);
-      if (s >= st.ctr_slots) continue;
-      beg = max(min(beg, p1), p0);
-      end = max(min(end, p1), beg);
+  if constexpr ((V & kVarSkipAggregates) == 0) {
+    // ---- C: containers and VMs (segmented, one lane per segment) ------------
+    const uint32_t ctr_rows_end = (c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0) - p0;
+    for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+      uint32_t beg = c == c0 ? p0 : b.ctr_proc_end[c - 1];
+      uint32_t end = b.ctr_proc_end[c];
+      const uint32_t w = b.ctr_slot[c];
+      const uint64_t sl = w & KACC_SLOT_MASK;
+      if (beg < p0 || end < beg || end > p1 || sl >= st.ctr_slots) {
+        raise_err(st.err, sl >= st.ctr_slots ? kErrSlot : kErrOffsets);
+        beg = max(min(beg, p1), p0);
+        end = max(min(end, p1), beg);
+      }
+      double delta = 0.0;  // resetCPUTime on the first process (informer.go:229-233, 481-483)
+      double total = (w & KACC_SLOT_NEW) || sl >= st.ctr_slots ? 0.0 : st.ctr_cpu_total[sl];
+      for (uint32_t i = beg - p0; i < end - p0; ++i) {
+        const double di = row_delta(i);
+        delta = delta + di;  // informer.go:485
+        total = total + di;  // informer.go:486
+      }
+      if (sl < st.ctr_slots) {
+        st.ctr_cpu_delta[sl] = delta;
+        st.ctr_cpu_total[sl] = total;
+      }
+      if (cstaged) {
+        s_cd[c - c0] = sl < st.ctr_slots ? delta : 0.0;
+        s_ct[c - c0] = sl < st.ctr_slots ? total : 0.0;
+      }
     }
-    double delta = 0.0;  // resetCPUTime on first process (informer.go:229-233, 481-483)
-    double total = (w & KACC_SLOT_NEW) ? 0.0 : st.ctr_cpu_total[s];
-    for (uint32_t i = beg; i < end; ++i) {
-      const double di = dcpu[i];
-      delta = delta + di;  // informer.go:485
-      total = total + di;  // informer.go:486
+    for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
+      uint32_t beg = v == v0 ? ctr_rows_end + p0 : b.vm_proc_end[v - 1];
+      uint32_t end = b.vm_proc_end[v];
+      const uint64_t sl = b.vm_slot[v] & KACC_SLOT_MASK;
+      if (beg < p0 || end < beg || end > p1 || sl >= st.vm_slots) {
+        raise_err(st.err, sl >= st.vm_slots ? kErrSlot : kErrOffsets);
+        if (sl >= st.vm_slots) continue;
+        beg = max(min(beg, p1), p0);
+        end = max(min(end, p1), beg);
+      }
+      // updateVMCache (informer.go:445): the last process in listing order wins
+      st.vm_cpu_delta[sl] = end > beg ? row_delta(end - 1 - p0) : 0.0;
     }
-    st.ctr_cpu_delta[s] = delta;
-    st.ctr_cpu_total[s] = total;
-  }
-  for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
-    uint32_t beg = v == v0 ? max(ctr_rows_end, p0) : b.vm_proc_end[v - 1];
-    uint32_t end = b.vm_proc_end[v];
-    const uint64_t s = b.vm_slot[v] & KACC_SLOT_MASK;
-    if (beg < p0 || end < beg || end > p1 || s >= st.vm_slots) {
-      raise_err(st.err, s >= st.vm_slots ? kErrSlot : kErrOffsets);
-      if (s >= st.vm_slots) continue;
-      beg = max(min(beg, p1), p0);
-      end = max(min(end, p1), beg);
-    }
-    // updateVMCache (informer.go:445): last process in listing order wins
-    st.vm_cpu_delta[s] = end > beg ? dcpu[end - 1] : 0.0;
   }
   __syncthreads();
 
-  // ---- D: pods (informer.go:305-309, 502-507) -------------------------------
-  for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
-    uint32_t beg = q == q0 ? c0 : b.pod_ctr_end[q - 1];
-    uint32_t end = b.pod_ctr_end[q];
-    const uint32_t w = b.pod_slot[q];
-    const uint64_t s = w & KACC_SLOT_MASK;
-    if (beg < c0 || end < beg || end > c1 || s >= st.pod_slots) {
-      raise_err(st.err, s >= st.pod_slots ? kErrSlot : kErrOffsets);
-      if (s >= st.pod_slots) continue;
-      beg = max(min(beg, c1), c0);
-      end = max(min(end, c1), beg);
+  if constexpr ((V & kVarSkipAggregates) == 0) {
+    // ---- D: pods (informer.go:305-309, 502-507) -----------------------------
+    for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+      uint32_t beg = q == q0 ? c0 : b.pod_ctr_end[q - 1];
+      uint32_t end = b.pod_ctr_end[q];
+      const uint32_t w = b.pod_slot[q];
+      const uint64_t sl = w & KACC_SLOT_MASK;
+      if (beg < c0 || end < beg || end > c1 || sl >= st.pod_slots) {
+        raise_err(st.err, sl >= st.pod_slots ? kErrSlot : kErrOffsets);
+        if (sl >= st.pod_slots) continue;
+        beg = max(min(beg, c1), c0);
+        end = max(min(end, c1), beg);
+      }
+      double delta = 0.0;
+      double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
+      for (uint32_t c = beg; c < end; ++c) {
+        if (cstaged) {
+          delta = delta + s_cd[c - c0];
+          total = total + s_ct[c - c0];  // quirk: the container's running total
+        } else {
+          const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
+          if (cs >= st.ctr_slots) continue;  // flagged in C
+          delta = delta + st.ctr_cpu_delta[cs];
+          total = total + st.ctr_cpu_total[cs];
+        }
+      }
+      st.pod_cpu_delta[sl] = delta;
+      st.pod_cpu_total[sl] = total;
     }
-    double delta = 0.0;
-    double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[s];
-    for (uint32_t c = beg; c < end; ++c) {
-      const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
-      if (cs >= st.ctr_slots) continue;  // already flagged in C
-      delta = delta + st.ctr_cpu_delta[cs];
-      total = total + st.ctr_cpu_total[cs];  // quirk: running container total
-    }
-    st.pod_cpu_delta[s] = delta;
-    st.pod_cpu_total[s] = total;
-  }
-  __syncthreads();
-
-  // node scalars of the new snapshot
-  if (tid == 0) {
-    st.node_ts[n] = b.node_ts_ns[n];
-    st.node_has_prev[n] = 1u;
-    st.node_usage_ratio[n] = first ? 0.0 : b.node_usage_ratio[n];  // firstNodeRead leaves 0
-    st.node_cpu_delta[n] = sh.node_delta;
-    st.node_status[n] = first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+    __syncthreads();
   }
 
-  // ---- E: attribution --------------------------------------------------------
+  // ---- E: attribution ----------------------------------------------------------
   Attr<Z> a;
-  a.nd = sh.node_delta;
-  a.first = first;
+  a.nd = uniform_f64(sh.node_delta);
+  a.first = uniform_u32(sh.first);
   a.live = 0;
   a.live_pod = 0;
 #pragma unroll
   for (int z = 0; z < Z; ++z) {
-    a.aE[z] = sh.active_energy[z];
-    a.aP[z] = sh.active_power[z];
+    a.aE[z] = uniform_u64(sh.active_energy[z]);
+    a.aP[z] = uniform_f64(sh.active_power[z]);
+    const double pw = uniform_f64(sh.power[z]);
     const bool ok = a.aE[z] != 0 && a.nd != 0;
-    if (ok && a.aP[z] != 0) a.live |= 1u << z;                    // process.go:124
-    if (ok && (first ? a.aP[z] : sh.power[z]) != 0) a.live_pod |= 1u << z;  // pod.go:96 / :23
+    if (ok && a.aP[z] != 0) a.live |= 1u << z;                           // process.go:124
+    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;      // pod.go:96 / :23
+  }
+  if (tid == 0) {  // node scalars of the new snapshot
+    st.node_ts[n] = b.node_ts_ns[n];
+    st.node_has_prev[n] = 1u;
+    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];  // firstNodeRead leaves 0
+    st.node_cpu_delta[n] = a.nd;
+    st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
 
-  // processes: coalesced row pass, kUnroll rows in flight per lane
-  for (uint32_t base = p0 + tid; base < p1; base += kBlock * kUnroll) {
-    double d[kUnroll];
-    uint32_t w[kUnroll];
-    uint64_t prev[kUnroll][Z];
+  if constexpr ((V & kVarSkipProcs) == 0) {
+    // processes: coalesced row pass, kUnroll rows in flight per lane
+    const uint32_t *__restrict__ pslot = b.proc_slot + p0;
+    for (uint32_t base = tid; base < rows; base += kBlock * kUnroll) {
+      double d[kUnroll];
+      uint32_t w[kUnroll];
+      uint64_t prev[kUnroll][Z];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const uint32_t r = base + u * kBlock;
-      const bool in = r < p1;
-      d[u] = in ? dcpu[r] : 0.0;
-      w[u] = in ? b.proc_slot[r] : 0xffffffffu;
-    }
-#pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const uint64_t s = w[u] & KACC_SLOT_MASK;
-      if (s < st.proc_slots) {
-        load_row<Z>(st.proc_energy, s, prev[u]);
-      } else {
-#pragma unroll
-        for (int z = 0; z < Z; ++z) prev[u][z] = 0;
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t r = base + u * kBlock;
+        const bool in = r < rows;
+        w[u] = in ? pslot[r] : 0xffffffffu;
+        d[u] = in ? row_delta(r) : 0.0;
       }
-    }
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const uint32_t r = base + u * kBlock;
-      if (r >= p1) continue;
-      const uint64_t s = w[u] & KACC_SLOT_MASK;
-      if (s >= st.proc_slots) {
-        raise_err(st.err, kErrSlot);
-        continue;
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint64_t sl = w[u] & KACC_SLOT_MASK;
+        if (sl < st.proc_slots) {
+          load_row<Z>(st.proc_energy, sl, prev[u]);
+        } else {
+#pragma unroll
+          for (int z = 0; z < Z; ++z) prev[u][z] = 0;
+        }
       }
-      uint64_t E[Z];
-      double P[Z];
-      attribute_row<Z>(a, a.live, d[u], (w[u] & KACC_SLOT_NEW) != 0, prev[u], E, P);
-      store_row<Z, uint64_t>(st.proc_energy, s, E);
-      store_row<Z, double>(st.proc_power, s, P);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const uint32_t r = base + u * kBlock;
+        if (r >= rows) continue;
+        const uint64_t sl = w[u] & KACC_SLOT_MASK;
+        if (sl >= st.proc_slots) {
+          raise_err(st.err, kErrSlot);
+          continue;
+        }
+        uint64_t E[Z];
+        double P[Z];
+        attribute_row<Z>(a, a.live, d[u], (w[u] & KACC_SLOT_NEW) != 0, prev[u], E, P);
+        store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
+        store_row<Z, kNT, double>(st.proc_power, sl, P);
+      }
     }
   }
 
-  // containers (container.go:106-140): Δ from pass C
-  for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
-    const uint32_t w = b.ctr_slot[c];
-    const uint64_t s = w & KACC_SLOT_MASK;
-    if (s >= st.ctr_slots) continue;
-    uint64_t prev[Z], E[Z];
-    double P[Z];
-    load_row<Z>(st.ctr_energy, s, prev);
-    attribute_row<Z>(a, a.live, st.ctr_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
-    store_row<Z, uint64_t>(st.ctr_energy, s, E);
-    store_row<Z, double>(st.ctr_power, s, P);
-  }
-  // virtual machines (vm.go:78-109)
-  for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
-    const uint32_t w = b.vm_slot[v];
-    const uint64_t s = w & KACC_SLOT_MASK;
-    if (s >= st.vm_slots) continue;
-    uint64_t prev[Z], E[Z];
-    double P[Z];
-    load_row<Z>(st.vm_energy, s, prev);
-    attribute_row<Z>(a, a.live, st.vm_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
-    store_row<Z, uint64_t>(st.vm_energy, s, E);
-    store_row<Z, double>(st.vm_power, s, P);
-  }
-  // pods (pod.go:87-118; nothing to do when none run, pod.go:70-73)
-  for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
-    const uint32_t w = b.pod_slot[q];
-    const uint64_t s = w & KACC_SLOT_MASK;
-    if (s >= st.pod_slots) continue;
-    uint64_t prev[Z], E[Z];
-    double P[Z];
-    load_row<Z>(st.pod_energy, s, prev);
-    attribute_row<Z>(a, a.live_pod, st.pod_cpu_delta[s], (w & KACC_SLOT_NEW) != 0, prev, E, P);
-    store_row<Z, uint64_t>(st.pod_energy, s, E);
-    store_row<Z, double>(st.pod_power, s, P);
+  if constexpr ((V & kVarSkipAggregates) == 0) {
+    // containers (container.go:106-140): Δ from pass C
+    for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+      const uint32_t w = b.ctr_slot[c];
+      if ((w & KACC_SLOT_MASK) >= st.ctr_slots) continue;
+      const double delta = cstaged ? s_cd[c - c0] : st.ctr_cpu_delta[w & KACC_SLOT_MASK];
+      attribute_slot<Z, kNT>(a, a.live, delta, w, st.ctr_energy, st.ctr_power);
+    }
+    // virtual machines (vm.go:78-109)
+    for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
+      const uint32_t w = b.vm_slot[v];
+      if ((w & KACC_SLOT_MASK) >= st.vm_slots) continue;
+      attribute_slot<Z, kNT>(a, a.live, st.vm_cpu_delta[w & KACC_SLOT_MASK], w, st.vm_energy,
+                             st.vm_power);
+    }
+    // pods (pod.go:87-118; nothing to do when none run, pod.go:70-73)
+    for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+      const uint32_t w = b.pod_slot[q];
+      if ((w & KACC_SLOT_MASK) >= st.pod_slots) continue;
+      attribute_slot<Z, kNT>(a, a.live_pod, st.pod_cpu_delta[w & KACC_SLOT_MASK], w,
+                             st.pod_energy, st.pod_power);
+    }
   }
 }
 
-// Namespace totals: one lane per namespace, pods summed in the given order.
-__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t Z, uint32_t n_ns,
+// Namespace totals: one wave per namespace; lane l sums pods l, l+64, ... in
+// CSR order, then the 64 lane sums are halved pairwise (l += l+s, s=32..1).
+// u64 energy sums are order independent; f64 power follows this fixed order.
+template <int Z>
+__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
                                                            const uint32_t *__restrict__ off,
                                                            const uint32_t *__restrict__ slots,
                                                            const uint64_t *__restrict__ pe,
                                                            const double *__restrict__ pp,
                                                            uint64_t pod_slots, uint64_t *out_e,
                                                            double *out_p, uint32_t *err) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) / kNsWave;
+  const uint32_t lane = threadIdx.x % kNsWave;
   if (k >= n_ns) return;
-  uint64_t e[KACC_MAX_ZONES];
-  double p[KACC_MAX_ZONES];
-  for (uint32_t z = 0; z < Z; ++z) {
+  unsigned long long e[Z];
+  double p[Z];
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
     e[z] = 0;
     p[z] = 0.0;
   }
   const uint32_t beg = off[k], end = off[k + 1];
-  for (uint32_t j = beg; j < end; ++j) {
+  for (uint32_t j = beg + lane; j < end; j += kNsWave) {
     const uint64_t s = slots[j] & KACC_SLOT_MASK;
     if (s >= pod_slots) {
       raise_err(err, kErrNs);
       continue;
     }
-    for (uint32_t z = 0; z < Z; ++z) {
-      e[z] += pe[s * Z + z];
+    uint64_t er[Z];
+    load_row<Z>(pe, s, er);
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      e[z] += er[z];
       p[z] = p[z] + pp[s * Z + z];
     }
   }
-  for (uint32_t z = 0; z < Z; ++z) {
-    out_e[static_cast<uint64_t>(k) * Z + z] = e[z];
-    out_p[static_cast<uint64_t>(k) * Z + z] = p[z];
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+#pragma unroll
+    for (int sft = kNsWave / 2; sft >= 1; sft >>= 1) {
+      e[z] += __shfl_down(e[z], sft, kNsWave);
+      p[z] = p[z] + __shfl_down(p[z], sft, kNsWave);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      out_e[static_cast<uint64_t>(k) * Z + z] = e[z];
+      out_p[static_cast<uint64_t>(k) * Z + z] = p[z];
+    }
   }
 }
 
@@ -543,22 +629,49 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   return s;
 }
 
-template <int Z>
-void launch_z(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
-  hipLaunchKernelGGL(kacc::interval_kernel<Z>, dim3(b.n_nodes), dim3(kacc::kBlock), 0, st, b, s);
+template <int Z, int V>
+void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
+  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kBlock), 0, st, b, s);
 }
 
 void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   switch (Z) {
-    case 1: launch_z<1>(b, s, st); break;
-    case 2: launch_z<2>(b, s, st); break;
-    case 3: launch_z<3>(b, s, st); break;
-    case 4: launch_z<4>(b, s, st); break;
-    case 5: launch_z<5>(b, s, st); break;
-    case 6: launch_z<6>(b, s, st); break;
-    case 7: launch_z<7>(b, s, st); break;
-    default: launch_z<8>(b, s, st); break;
+    case 1: launch_zv<1, 0>(b, s, st); break;
+    case 2: launch_zv<2, 0>(b, s, st); break;
+    case 3: launch_zv<3, 0>(b, s, st); break;
+    case 4: launch_zv<4, 0>(b, s, st); break;
+    case 5: launch_zv<5, 0>(b, s, st); break;
+    case 6: launch_zv<6, 0>(b, s, st); break;
+    case 7: launch_zv<7, 0>(b, s, st); break;
+    default: launch_zv<8, 0>(b, s, st); break;
   }
+}
+
+// timing ablations (Z = 4 only): see kacc::kVar*
+bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevState &s,
+                    hipStream_t st) {
+  if (Z != 4) return false;
+  switch (v) {
+    case 0: launch_zv<4, 0>(b, s, st); return true;
+    case 1: launch_zv<4, 1>(b, s, st); return true;
+    case 2: launch_zv<4, 2>(b, s, st); return true;
+    case 3: launch_zv<4, 3>(b, s, st); return true;
+    case 4: launch_zv<4, 4>(b, s, st); return true;
+    case 8: launch_zv<4, 8>(b, s, st); return true;
+    case 9: launch_zv<4, 9>(b, s, st); return true;
+    default: return false;
+  }
+}
+
+template <int Z>
+void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const kacc_ctx *ctx,
+               uint64_t *out_e, double *out_p, hipStream_t st) {
+  const uint32_t per_block = kacc::kBlock / kacc::kNsWave;
+  const uint32_t grid = (n_ns + per_block - 1) / per_block;
+  hipLaunchKernelGGL((kacc::namespace_kernel<Z>), dim3(grid), dim3(kacc::kBlock), 0, st, n_ns, off,
+                     slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
+                     (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p,
+                     ctx->d_err);
 }
 
 int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
@@ -895,12 +1008,16 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, con
   if (!off || !slots || !out_energy || !out_power) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  const uint32_t grid = (n_ns + kacc::kBlock - 1) / kacc::kBlock;
-  hipLaunchKernelGGL(kacc::namespace_kernel, dim3(grid), dim3(kacc::kBlock), 0, st,
-                     ctx->cfg.zones, n_ns, off, slots,
-                     (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
-                     (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots,
-                     out_energy, out_power, ctx->d_err);
+  switch (ctx->cfg.zones) {
+    case 1: launch_ns<1>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 2: launch_ns<2>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 3: launch_ns<3>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 4: launch_ns<4>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 5: launch_ns<5>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 6: launch_ns<6>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    case 7: launch_ns<7>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+    default: launch_ns<8>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
+  }
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
@@ -914,6 +1031,20 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
   const uint64_t vm = 16 + 24ull * Z;
   const uint64_t pod = 32 + 24ull * Z;
   return N * node + P * proc + C * ctr + V * vm + Q * pod;
+}
+
+// Internal (kacc_debug.h): timing ablations of the interval kernel.  A variant
+// other than 0 does NOT compute the reference semantics.
+int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, int variant) {
+  if (!ctx) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = check_shape(ctx, b);
+  if (rc != KACC_OK || b->n_nodes == 0) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (!launch_variant(ctx->cfg.zones, variant, *b, dev_state(ctx), st))
+    return fail(ctx, KACC_EINVAL, "variant %d not built for Z=%u", variant, ctx->cfg.zones);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
 }
 
 }  // extern "C"

@@ -36,6 +36,10 @@ ZONE_NAMES = {
     2: ["package", "dram"],
     3: ["package", "core", "dram"],
     4: ["package", "core", "uncore", "dram"],
+    5: ["package", "core", "uncore", "dram", "psys"],
+    6: ["package", "core", "uncore", "dram", "psys", "pp0"],
+    7: ["package", "core", "uncore", "dram", "psys", "pp0", "pp1"],
+    8: ["package", "core", "uncore", "dram", "psys", "pp0", "pp1", "package-1"],
 }
 
 
@@ -226,7 +230,8 @@ class FleetSim:
         self.prev_total = np.zeros(L.n_procs, dtype=np.float64)  # informer cache starts empty
         pkg = self._rng.uniform(50.0, 400.0, size=N)
         dram = self._rng.uniform(5.0, 40.0, size=N)
-        watts = {"package": pkg, "core": 0.6 * pkg, "uncore": 0.1 * pkg, "dram": dram}
+        watts = {"package": pkg, "core": 0.6 * pkg, "uncore": 0.1 * pkg, "dram": dram,
+                 "psys": 1.3 * pkg + dram, "pp0": 0.55 * pkg, "pp1": 0.05 * pkg, "package-1": 0.9 * pkg}
         self.zone_watts = np.stack([watts[z] for z in ZONE_NAMES[Z]], axis=1).reshape(-1)
 
     def next_node_inputs(self) -> Dict[str, np.ndarray]:

@@ -24,6 +24,7 @@ KATS = load_kats()
 def gpu_ready():
     assert torch.cuda.is_available(), "GPU tests need an MI355X"
     accel.load()  # raises if the HIP library is missing: no fallback
+    torch.cuda.set_stream(torch.cuda.Stream())  # engine + copies on one explicit stream
 
 
 class EngineBackend:
@@ -159,6 +160,11 @@ def test_namespace_totals_match_oracle():
     eng.acc.sync(s)
     np.testing.assert_array_equal(out_e.cpu().numpy().view(np.uint64), e_o)
     np.testing.assert_array_equal(out_p.cpu().numpy(), p_o)
+    # against a plain list-order sum: <= 1e-12 relative (north-star totals bar)
+    pp = ora.state["pod_power"].reshape(-1, layout.zones)
+    ref = np.array([[sum(pp[s_, z] for s_ in slots[off[k]:off[k + 1]]) for z in range(layout.zones)]
+                    for k in range(len(off) - 1)]).reshape(-1)
+    np.testing.assert_allclose(out_p.cpu().numpy(), ref, rtol=1e-12, atol=0)
 
 
 def test_out_of_range_slot_is_reported_not_faulted():
