@@ -33,11 +33,13 @@
 
 namespace kacc {
 
-constexpr int kBlock = 256;                  // lanes of the canonical node-total tree
+constexpr int kThreads = 512;                // workgroup of the interval kernel (8 waves)
+constexpr int kTree = 256;                   // lanes of the canonical node-total tree
 constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
-constexpr int kLoadsPerLane = kRowsLds / kBlock;
-constexpr int kCtrLds = 512;                 // container Δ / total staged in LDS
-constexpr int kUnroll = 4;                   // process rows in flight per lane (attribution)
+constexpr int kRowsPerThread = kRowsLds / kThreads;
+constexpr int kLoadsPerLane = kRowsLds / kTree;
+constexpr int kUnroll = 2;                   // process rows in flight per lane (generic path)
+constexpr int kBlock = 256;                  // namespace kernel workgroup
 constexpr int kNsWave = 64;                  // lanes per namespace (namespace_kernel)
 
 // Debug variants (kacc_debug_run_variant, timing ablations only; results of a
@@ -181,13 +183,20 @@ __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, 
   store_row<Z, NT, double>(power, s, P);
 }
 
+// Generic path (big nodes / many aggregates): loops, Δ re-read from global.
 template <int Z, int V>
-__global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b, const DevState st) {
+__device__ void generic_node(const kacc_interval &b, const DevState &st, const uint32_t n,
+                             const uint32_t p0, const uint32_t p1, const uint32_t c0,
+                             const uint32_t c1, const uint32_t v0, const uint32_t v1,
+                             const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh);
+
+template <int Z, int V>
+__global__ __launch_bounds__(kThreads, (Z <= 4 ? 6 : 2)) void interval_kernel(const kacc_interval b, const DevState st) {
   constexpr bool kNT = (V & kVarNtStores) != 0;
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
-  __shared__ double s_cd[kCtrLds];   // container Δ of this interval
-  __shared__ double s_ct[kCtrLds];   // container running CPU total
-  __shared__ double red[kBlock];
+  __shared__ double s_cd[kThreads];  // container Δ of this interval (fast path)
+  __shared__ double s_ct[kThreads];  // container running CPU total (fast path)
+  __shared__ double red[kTree];
   __shared__ NodeShared sh;
 
   const int tid = threadIdx.x;
@@ -221,12 +230,11 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
     q1 = min(q1, b.n_pods);
     q0 = min(q0, q1);
   }
-  const uint32_t rows = p1 - p0;
-  const bool staged = (V & kVarUnstaged) == 0 && rows <= static_cast<uint32_t>(kRowsLds);
-  const bool cstaged = (c1 - c0) <= static_cast<uint32_t>(kCtrLds);
-  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;  // node-local row index
+  const uint32_t rows = p1 - p0, nc = c1 - c0, nv = v1 - v0, nq = q1 - q0;
+  const bool fast = (V & kVarUnstaged) == 0 && rows <= static_cast<uint32_t>(kRowsLds) &&
+                    nc + nv + nq <= static_cast<uint32_t>(kThreads);
 
-  // ---- A: node zones (threads z < Z) ----------------------------------------
+  // ---- A: node zones (threads z < Z): node.go:10-84 / node.go:101-131 -----------
   if (tid < Z) {
     const bool first = st.node_has_prev[n] == 0u;
     const uint64_t i = static_cast<uint64_t>(n) * Z + tid;
@@ -259,27 +267,237 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
     if (tid == 0) sh.first = first ? 1u : 0u;
   }
 
-  // ---- B: stage Δcpu, ProcessTotalCPUTimeDelta (informer.go:330-333) --------
-  // Lane l sums rows l, l+256, l+512, ... in order; loads are issued
-  // kLoadsPerLane at a time (independent), the adds stay sequential.
-  double s = 0.0;
-  for (uint32_t base = 0; base < rows; base += kRowsLds) {
-    double v[kLoadsPerLane];
+  if (!fast) {
+    generic_node<Z, V>(b, st, n, p0, p1, c0, c1, v0, v1, q0, q1, red, sh);
+    return;
+  }
+
+  // ======================= fast path: one node fits the block ===================
+  // Every global load the node needs is issued here, before the first barrier:
+  // the rows' Δ and slot words, then (dependent) their previous totals; one
+  // aggregate per lane (containers, then VMs, then pods) with its range,
+  // slot, previous totals and running CPU total.
+  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
+  const uint32_t *__restrict__ pslot = b.proc_slot + p0;
+  double d[kRowsPerThread];
+  uint32_t w[kRowsPerThread];
 #pragma unroll
-    for (int k = 0; k < kLoadsPerLane; ++k) {
-      const uint32_t i = base + tid + k * kBlock;
-      v[k] = i < rows ? dcpu[i] : 0.0;
+  for (int k = 0; k < kRowsPerThread; ++k) {
+    const uint32_t r = tid + k * kThreads;
+    const bool in = r < rows;
+    d[k] = in ? dcpu[r] : 0.0;
+    w[k] = in ? pslot[r] : 0xffffffffu;
+  }
+  // aggregate role of this lane: 1 container, 2 VM, 3 pod
+  uint32_t role = 0, j = 0, a_beg = 0, a_end = 0, a_w = 0xffffffffu;
+  uint64_t a_cap = 0;
+  if ((V & kVarSkipAggregates) == 0) {
+    if (static_cast<uint32_t>(tid) < nc) {
+      role = 1;
+      j = tid;
+      a_beg = j == 0 ? p0 : b.ctr_proc_end[c0 + j - 1];
+      a_end = b.ctr_proc_end[c0 + j];
+      a_w = b.ctr_slot[c0 + j];
+      a_cap = st.ctr_slots;
+    } else if (static_cast<uint32_t>(tid) < nc + nv) {
+      role = 2;
+      j = tid - nc;
+      a_beg = j == 0 ? (nc ? b.ctr_proc_end[c1 - 1] : p0) : b.vm_proc_end[v0 + j - 1];
+      a_end = b.vm_proc_end[v0 + j];
+      a_w = b.vm_slot[v0 + j];
+      a_cap = st.vm_slots;
+    } else if (static_cast<uint32_t>(tid) < nc + nv + nq) {
+      role = 3;
+      j = tid - nc - nv;
+      a_beg = j == 0 ? c0 : b.pod_ctr_end[q0 + j - 1];
+      a_end = b.pod_ctr_end[q0 + j];
+      a_w = b.pod_slot[q0 + j];
+      a_cap = st.pod_slots;
     }
+  }
+  const uint64_t a_s = a_w & KACC_SLOT_MASK;
+  const bool a_ok = role != 0 && a_s < a_cap;
+  // per-role tables, re-derived at each use (keeps 8 VGPRs of pointers dead)
+  auto a_energy = [&]() { return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy; };
+  auto a_power = [&]() { return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power; };
+  auto a_cpu_total = [&]() { return role == 1 ? st.ctr_cpu_total : st.pod_cpu_total; };
+  auto a_cpu_delta = [&]() {
+    return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
+  };
+  // second-level gathers (depend on the slot words)
+  uint64_t prev[kRowsPerThread][Z];
+  if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-    for (int k = 0; k < kLoadsPerLane; ++k) {
-      const uint32_t i = base + tid + k * kBlock;
-      if (i < rows) {
-        if (staged) s_d[i] = v[k];
-        s = s + v[k];
+    for (int k = 0; k < kRowsPerThread; ++k) {
+      const uint64_t sl = w[k] & KACC_SLOT_MASK;
+      if (sl < st.proc_slots) {
+        load_row<Z>(st.proc_energy, sl, prev[k]);
+      } else {
+#pragma unroll
+        for (int z = 0; z < Z; ++z) prev[k][z] = 0;
       }
     }
   }
-  red[tid] = s;
+  uint64_t a_prev[Z];
+  double a_total = 0.0;
+  if (a_ok) {
+    load_row<Z>(a_energy(), a_s, a_prev);
+    if (role != 2 && !(a_w & KACC_SLOT_NEW)) a_total = a_cpu_total()[a_s];
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) a_prev[z] = 0;
+  }
+  if (role != 0 && !a_ok) raise_err(st.err, kErrSlot);
+
+  // ---- B: stage Δ, ProcessTotalCPUTimeDelta (informer.go:330-333) ------------
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; ++k) {
+    const uint32_t r = tid + k * kThreads;
+    if (r < rows) s_d[r] = d[k];
+  }
+  __syncthreads();
+  if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
+    if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
+  } else {
+    // lane l < 256 sums rows l, l+256, l+512, ... in order; then the halving tree
+    if (tid < kTree) {
+      double s = 0.0;
+      for (uint32_t r = tid; r < rows; r += kTree) s = s + s_d[r];
+      red[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 128) red[tid] = red[tid] + red[tid + 128];
+    __syncthreads();
+    if (tid < 64) {
+      double x = red[tid] + red[tid + 64];
+#pragma unroll
+      for (int k = 32; k >= 1; k >>= 1) x = x + __shfl_down(x, k, 64);
+      if (tid == 0) sh.node_delta = x;
+    }
+  }
+
+  // ---- C: containers and VMs (segmented sums, one lane per segment) ----------
+  double a_delta = 0.0;
+  if (role == 1 || role == 2) {
+    uint32_t beg = a_beg, end = a_end;
+    if (beg < p0 || end < beg || end > p1) {
+      raise_err(st.err, kErrOffsets);
+      beg = max(min(beg, p1), p0);
+      end = max(min(end, p1), beg);
+    }
+    if (role == 1) {
+      // resetCPUTime on the first process (informer.go:229-233, 481-486)
+      for (uint32_t i = beg - p0; i < end - p0; ++i) {
+        const double di = s_d[i];
+        a_delta = a_delta + di;
+        a_total = a_total + di;
+      }
+      s_cd[j] = a_ok ? a_delta : 0.0;
+      s_ct[j] = a_ok ? a_total : 0.0;
+    } else {
+      // updateVMCache (informer.go:445): the last process in listing order wins
+      a_delta = end > beg ? s_d[end - 1 - p0] : 0.0;
+    }
+    if (a_ok) {
+      a_cpu_delta()[a_s] = a_delta;
+      if (role == 1) a_cpu_total()[a_s] = a_total;
+    }
+  }
+  __syncthreads();
+
+  // ---- D: pods (informer.go:305-309, 502-507) ----------------------------------
+  if (role == 3) {
+    uint32_t beg = a_beg, end = a_end;
+    if (beg < c0 || end < beg || end > c1) {
+      raise_err(st.err, kErrOffsets);
+      beg = max(min(beg, c1), c0);
+      end = max(min(end, c1), beg);
+    }
+    for (uint32_t c = beg - c0; c < end - c0; ++c) {
+      a_delta = a_delta + s_cd[c];
+      a_total = a_total + s_ct[c];  // quirk: the container's running total
+    }
+    if (a_ok) {
+      a_cpu_delta()[a_s] = a_delta;
+      a_cpu_total()[a_s] = a_total;
+    }
+  }
+
+  // ---- E: attribution ------------------------------------------------------------
+  Attr<Z> a;
+  a.nd = uniform_f64(sh.node_delta);
+  a.first = uniform_u32(sh.first);
+  a.live = 0;
+  a.live_pod = 0;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    a.aE[z] = uniform_u64(sh.active_energy[z]);
+    a.aP[z] = uniform_f64(sh.active_power[z]);
+    const double pw = uniform_f64(sh.power[z]);
+    const bool ok = a.aE[z] != 0 && a.nd != 0;
+    if (ok && a.aP[z] != 0) a.live |= 1u << z;                       // process.go:124
+    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;  // pod.go:96 / :23
+  }
+  if (tid == 0) {  // node scalars of the new snapshot
+    st.node_ts[n] = b.node_ts_ns[n];
+    st.node_has_prev[n] = 1u;
+    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];  // firstNodeRead leaves 0
+    st.node_cpu_delta[n] = a.nd;
+    st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+  }
+  if (a_ok) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+    uint64_t E[Z];
+    double P[Z];
+    attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0,
+                     a_prev, E, P);
+    store_row<Z, kNT, uint64_t>(a_energy(), a_s, E);
+    store_row<Z, kNT, double>(a_power(), a_s, P);
+  }
+  if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; ++k) {
+      const uint32_t r = tid + k * kThreads;
+      if (r >= rows) continue;
+      const uint64_t sl = w[k] & KACC_SLOT_MASK;
+      if (sl >= st.proc_slots) {
+        raise_err(st.err, kErrSlot);
+        continue;
+      }
+      uint64_t E[Z];
+      double P[Z];
+      attribute_row<Z>(a, a.live, s_d[r], (w[k] & KACC_SLOT_NEW) != 0, prev[k], E, P);
+      store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
+      store_row<Z, kNT, double>(st.proc_power, sl, P);
+    }
+  }
+}
+
+template <int Z, int V>
+__device__ void generic_node(const kacc_interval &b, const DevState &st, const uint32_t n,
+                             const uint32_t p0, const uint32_t p1, const uint32_t c0,
+                             const uint32_t c1, const uint32_t v0, const uint32_t v1,
+                             const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh) {
+  constexpr bool kNT = (V & kVarNtStores) != 0;
+  const int tid = threadIdx.x;
+  const uint32_t rows = p1 - p0;
+  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
+
+  // ---- B: ProcessTotalCPUTimeDelta, lanes < 256 stream the rows from HBM ----
+  if (tid < kTree) {
+    double s = 0.0;
+    for (uint32_t base = 0; base < rows; base += kRowsLds) {
+      double v[kLoadsPerLane];
+#pragma unroll
+      for (int k = 0; k < kLoadsPerLane; ++k) {
+        const uint32_t i = base + tid + k * kTree;
+        v[k] = i < rows ? dcpu[i] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < kLoadsPerLane; ++k)
+        if (base + tid + k * kTree < rows) s = s + v[k];
+    }
+    red[tid] = s;
+  }
   __syncthreads();
   if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
     if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
@@ -293,39 +511,33 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
       if (tid == 0) sh.node_delta = x;
     }
   }
-  auto row_delta = [&](uint32_t i) -> double { return staged ? s_d[i] : dcpu[i]; };
 
   if constexpr ((V & kVarSkipAggregates) == 0) {
-    // ---- C: containers and VMs (segmented, one lane per segment) ------------
-    const uint32_t ctr_rows_end = (c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0) - p0;
-    for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+    // ---- C: containers and VMs ----------------------------------------------
+    const uint32_t ctr_rows_end = c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0;
+    for (uint32_t c = c0 + tid; c < c1; c += kThreads) {
       uint32_t beg = c == c0 ? p0 : b.ctr_proc_end[c - 1];
       uint32_t end = b.ctr_proc_end[c];
       const uint32_t w = b.ctr_slot[c];
       const uint64_t sl = w & KACC_SLOT_MASK;
       if (beg < p0 || end < beg || end > p1 || sl >= st.ctr_slots) {
         raise_err(st.err, sl >= st.ctr_slots ? kErrSlot : kErrOffsets);
+        if (sl >= st.ctr_slots) continue;
         beg = max(min(beg, p1), p0);
         end = max(min(end, p1), beg);
       }
-      double delta = 0.0;  // resetCPUTime on the first process (informer.go:229-233, 481-483)
-      double total = (w & KACC_SLOT_NEW) || sl >= st.ctr_slots ? 0.0 : st.ctr_cpu_total[sl];
+      double delta = 0.0;
+      double total = (w & KACC_SLOT_NEW) ? 0.0 : st.ctr_cpu_total[sl];
       for (uint32_t i = beg - p0; i < end - p0; ++i) {
-        const double di = row_delta(i);
-        delta = delta + di;  // informer.go:485
-        total = total + di;  // informer.go:486
+        const double di = dcpu[i];
+        delta = delta + di;
+        total = total + di;
       }
-      if (sl < st.ctr_slots) {
-        st.ctr_cpu_delta[sl] = delta;
-        st.ctr_cpu_total[sl] = total;
-      }
-      if (cstaged) {
-        s_cd[c - c0] = sl < st.ctr_slots ? delta : 0.0;
-        s_ct[c - c0] = sl < st.ctr_slots ? total : 0.0;
-      }
+      st.ctr_cpu_delta[sl] = delta;
+      st.ctr_cpu_total[sl] = total;
     }
-    for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
-      uint32_t beg = v == v0 ? ctr_rows_end + p0 : b.vm_proc_end[v - 1];
+    for (uint32_t v = v0 + tid; v < v1; v += kThreads) {
+      uint32_t beg = v == v0 ? ctr_rows_end : b.vm_proc_end[v - 1];
       uint32_t end = b.vm_proc_end[v];
       const uint64_t sl = b.vm_slot[v] & KACC_SLOT_MASK;
       if (beg < p0 || end < beg || end > p1 || sl >= st.vm_slots) {
@@ -334,15 +546,13 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
         beg = max(min(beg, p1), p0);
         end = max(min(end, p1), beg);
       }
-      // updateVMCache (informer.go:445): the last process in listing order wins
-      st.vm_cpu_delta[sl] = end > beg ? row_delta(end - 1 - p0) : 0.0;
+      st.vm_cpu_delta[sl] = end > beg ? dcpu[end - 1 - p0] : 0.0;
     }
   }
   __syncthreads();
-
   if constexpr ((V & kVarSkipAggregates) == 0) {
-    // ---- D: pods (informer.go:305-309, 502-507) -----------------------------
-    for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+    // ---- D: pods --------------------------------------------------------------
+    for (uint32_t q = q0 + tid; q < q1; q += kThreads) {
       uint32_t beg = q == q0 ? c0 : b.pod_ctr_end[q - 1];
       uint32_t end = b.pod_ctr_end[q];
       const uint32_t w = b.pod_slot[q];
@@ -356,23 +566,18 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
       double delta = 0.0;
       double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
       for (uint32_t c = beg; c < end; ++c) {
-        if (cstaged) {
-          delta = delta + s_cd[c - c0];
-          total = total + s_ct[c - c0];  // quirk: the container's running total
-        } else {
-          const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
-          if (cs >= st.ctr_slots) continue;  // flagged in C
-          delta = delta + st.ctr_cpu_delta[cs];
-          total = total + st.ctr_cpu_total[cs];
-        }
+        const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
+        if (cs >= st.ctr_slots) continue;
+        delta = delta + st.ctr_cpu_delta[cs];
+        total = total + st.ctr_cpu_total[cs];
       }
       st.pod_cpu_delta[sl] = delta;
       st.pod_cpu_total[sl] = total;
     }
-    __syncthreads();
   }
+  __syncthreads();
 
-  // ---- E: attribution ----------------------------------------------------------
+  // ---- E: attribution ------------------------------------------------------------
   Attr<Z> a;
   a.nd = uniform_f64(sh.node_delta);
   a.first = uniform_u32(sh.first);
@@ -384,30 +589,28 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
     a.aP[z] = uniform_f64(sh.active_power[z]);
     const double pw = uniform_f64(sh.power[z]);
     const bool ok = a.aE[z] != 0 && a.nd != 0;
-    if (ok && a.aP[z] != 0) a.live |= 1u << z;                           // process.go:124
-    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;      // pod.go:96 / :23
+    if (ok && a.aP[z] != 0) a.live |= 1u << z;
+    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;
   }
-  if (tid == 0) {  // node scalars of the new snapshot
+  if (tid == 0) {
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
-    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];  // firstNodeRead leaves 0
+    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];
     st.node_cpu_delta[n] = a.nd;
     st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
-
   if constexpr ((V & kVarSkipProcs) == 0) {
-    // processes: coalesced row pass, kUnroll rows in flight per lane
     const uint32_t *__restrict__ pslot = b.proc_slot + p0;
-    for (uint32_t base = tid; base < rows; base += kBlock * kUnroll) {
+    for (uint32_t base = tid; base < rows; base += kThreads * kUnroll) {
       double d[kUnroll];
       uint32_t w[kUnroll];
       uint64_t prev[kUnroll][Z];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t r = base + u * kBlock;
+        const uint32_t r = base + u * kThreads;
         const bool in = r < rows;
         w[u] = in ? pslot[r] : 0xffffffffu;
-        d[u] = in ? row_delta(r) : 0.0;
+        d[u] = in ? dcpu[r] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
@@ -421,7 +624,7 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t r = base + u * kBlock;
+        const uint32_t r = base + u * kThreads;
         if (r >= rows) continue;
         const uint64_t sl = w[u] & KACC_SLOT_MASK;
         if (sl >= st.proc_slots) {
@@ -436,24 +639,20 @@ __global__ __launch_bounds__(kBlock) void interval_kernel(const kacc_interval b,
       }
     }
   }
-
   if constexpr ((V & kVarSkipAggregates) == 0) {
-    // containers (container.go:106-140): Δ from pass C
-    for (uint32_t c = c0 + tid; c < c1; c += kBlock) {
+    for (uint32_t c = c0 + tid; c < c1; c += kThreads) {
       const uint32_t w = b.ctr_slot[c];
       if ((w & KACC_SLOT_MASK) >= st.ctr_slots) continue;
-      const double delta = cstaged ? s_cd[c - c0] : st.ctr_cpu_delta[w & KACC_SLOT_MASK];
-      attribute_slot<Z, kNT>(a, a.live, delta, w, st.ctr_energy, st.ctr_power);
+      attribute_slot<Z, kNT>(a, a.live, st.ctr_cpu_delta[w & KACC_SLOT_MASK], w, st.ctr_energy,
+                             st.ctr_power);
     }
-    // virtual machines (vm.go:78-109)
-    for (uint32_t v = v0 + tid; v < v1; v += kBlock) {
+    for (uint32_t v = v0 + tid; v < v1; v += kThreads) {
       const uint32_t w = b.vm_slot[v];
       if ((w & KACC_SLOT_MASK) >= st.vm_slots) continue;
       attribute_slot<Z, kNT>(a, a.live, st.vm_cpu_delta[w & KACC_SLOT_MASK], w, st.vm_energy,
                              st.vm_power);
     }
-    // pods (pod.go:87-118; nothing to do when none run, pod.go:70-73)
-    for (uint32_t q = q0 + tid; q < q1; q += kBlock) {
+    for (uint32_t q = q0 + tid; q < q1; q += kThreads) {
       const uint32_t w = b.pod_slot[q];
       if ((w & KACC_SLOT_MASK) >= st.pod_slots) continue;
       attribute_slot<Z, kNT>(a, a.live_pod, st.pod_cpu_delta[w & KACC_SLOT_MASK], w,
@@ -631,7 +830,7 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
 
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
-  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kBlock), 0, st, b, s);
+  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kThreads), 0, st, b, s);
 }
 
 void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {

@@ -107,6 +107,10 @@ FLEETS = [
     ("z8-max-zones", dict(n_nodes=9, procs_per_node=511, zones=8)),
     ("z4-skew", dict(n_nodes=6, procs_per_node=[10000, 50000, 12000, 31000, 10, 0], zones=4,
                      procs_per_vm=2, vm_frac=0.02)),
+    # fast/generic path boundaries: 2048 rows staged in LDS, <= 512 aggregates per node
+    ("z4-rows-boundary", dict(n_nodes=6, procs_per_node=[2047, 2048, 2049, 4096, 1, 0], zones=4)),
+    ("z2-many-aggregates", dict(n_nodes=5, procs_per_node=[600, 700, 800, 2000, 300], zones=2,
+                                procs_per_ctr=1, ctrs_per_pod=1.0, vm_frac=0.05)),
 ]
 
 
