@@ -40,6 +40,8 @@ constexpr int kRowsPerThread = kRowsLds / kThreads;
 constexpr int kLoadsPerLane = kRowsLds / kTree;
 constexpr int kUnroll = 2;                   // process rows in flight per lane (generic path)
 constexpr int kBlock = 256;                  // namespace kernel workgroup
+template <int Z>
+constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 64-row groups
 constexpr int kNsWave = 64;                  // lanes per namespace (namespace_kernel)
 
 // Debug variants (kacc_debug_run_variant, timing ablations only; results of a
@@ -48,6 +50,8 @@ constexpr int kVarSkipAggregates = 1;  // skip containers / VMs / pods
 constexpr int kVarSkipProcs = 2;       // skip the process attribution pass
 constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
 constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
+constexpr int kVarOcc2 = 16;           // 2 workgroups per CU (no register cap)
+constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
 
 // device error bits (KACC_ERANGE)
 constexpr uint32_t kErrNode = 1u << 0;
@@ -183,6 +187,79 @@ __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, 
   store_row<Z, NT, double>(power, s, P);
 }
 
+// A 64-row group whose slots are consecutive (slot(row g+l) = s0 + l) is
+// moved with 1 KiB-contiguous wave instructions: its Z/2 × 64 16-B pieces of
+// the energy (and power) table are spread over the lanes, piece p = l + 64j
+// holding zones 2(p mod Z/2) and 2(p mod Z/2)+1 of row p div (Z/2).  Same
+// arithmetic as attribute_row, only the lane <-> (row, zone) mapping differs.
+template <int Z>
+__device__ __forceinline__ void load_group(const uint64_t *__restrict__ base, uint64_t s0,
+                                           uint64_t (&out)[Z]) {
+  using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
+  const u64x2 *p = reinterpret_cast<const u64x2 *>(base + s0 * Z);
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int j = 0; j < Z / 2; ++j) {
+    const u64x2 x = p[lane + 64 * j];
+    out[2 * j] = x.x;
+    out[2 * j + 1] = x.y;
+  }
+}
+
+template <int Z, bool NT>
+__device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShared &sh,
+                                                const double *s_d_group, uint32_t w_lane,
+                                                uint64_t s0, const uint64_t (&prev)[Z],
+                                                uint64_t *__restrict__ energy,
+                                                double *__restrict__ power) {
+  using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
+  using f64x2 = __attribute__((ext_vector_type(2))) double;
+  constexpr int kHalf = Z / 2;
+  const uint32_t lane = threadIdx.x & 63u;
+  u64x2 *pe = reinterpret_cast<u64x2 *>(energy + s0 * Z);
+  f64x2 *pp = reinterpret_cast<f64x2 *>(power + s0 * Z);
+#pragma unroll
+  for (int j = 0; j < kHalf; ++j) {
+    const uint32_t piece = lane + 64u * j;
+    const uint32_t row = piece / kHalf;
+    const uint32_t zp = piece % kHalf;
+    const uint32_t wr = __shfl(w_lane, static_cast<int>(row), 64);
+    const bool is_new = (wr & KACC_SLOT_NEW) != 0;
+    const double ratio = s_d_group[row] / a.nd;  // the row's own IEEE division
+    uint64_t E[2];
+    double P[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      // zone 2*zp+h: lane-dependent, so read from LDS (a register array
+      // indexed by a lane value would be demoted to scratch)
+      const uint32_t z = 2 * zp + h;
+      const uint64_t aE = sh.active_energy[z];
+      const double aP = sh.active_power[z];
+      if (a.live & (1u << z)) {
+        const uint64_t e = go_f64_to_u64(ratio * u2f(aE));
+        E[h] = a.first ? e : e + (is_new ? 0ull : prev[2 * j + h]);
+        P[h] = a.first ? 0.0 : ratio * aP;
+      } else {
+        E[h] = 0;
+        P[h] = 0.0;
+      }
+    }
+    u64x2 ev;
+    ev.x = E[0];
+    ev.y = E[1];
+    f64x2 pv;
+    pv.x = P[0];
+    pv.y = P[1];
+    if constexpr (NT) {
+      __builtin_nontemporal_store(ev, pe + piece);
+      __builtin_nontemporal_store(pv, pp + piece);
+    } else {
+      pe[piece] = ev;
+      pp[piece] = pv;
+    }
+  }
+}
+
 // Generic path (big nodes / many aggregates): loops, Δ re-read from global.
 template <int Z, int V>
 __device__ void generic_node(const kacc_interval &b, const DevState &st, const uint32_t n,
@@ -191,7 +268,7 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
                              const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh);
 
 template <int Z, int V>
-__global__ __launch_bounds__(kThreads, (Z <= 4 ? 6 : 2)) void interval_kernel(const kacc_interval b, const DevState st) {
+__global__ __launch_bounds__(kThreads, ((V & kVarOcc2) || Z > 4) ? 2 : 6) void interval_kernel(const kacc_interval b, const DevState st) {
   constexpr bool kNT = (V & kVarNtStores) != 0;
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
   __shared__ double s_cd[kThreads];  // container Δ of this interval (fast path)
@@ -324,12 +401,24 @@ __global__ __launch_bounds__(kThreads, (Z <= 4 ? 6 : 2)) void interval_kernel(co
   auto a_cpu_delta = [&]() {
     return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
   };
-  // second-level gathers (depend on the slot words)
+  // second-level gathers (depend on the slot words).  A 64-row group with
+  // consecutive slots is loaded 1 KiB-contiguous per wave instruction.
   uint64_t prev[kRowsPerThread][Z];
+  uint32_t contig = 0;  // bit k: group k of this wave is transposed (wave-uniform)
   if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint64_t sl = w[k] & KACC_SLOT_MASK;
+      if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+        const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));  // lane 0's slot
+        const bool mine = (tid + k * kThreads) < rows && sl == s0 + (tid & 63) &&
+                          s0 + 64 <= st.proc_slots;
+        if (__all(mine)) {
+          contig |= 1u << k;
+          load_group<Z>(st.proc_energy, s0, prev[k]);
+          continue;
+        }
+      }
       if (sl < st.proc_slots) {
         load_row<Z>(st.proc_energy, sl, prev[k]);
       } else {
@@ -457,6 +546,14 @@ __global__ __launch_bounds__(kThreads, (Z <= 4 ? 6 : 2)) void interval_kernel(co
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint32_t r = tid + k * kThreads;
+      if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+        if (contig & (1u << k)) {
+          const uint64_t s0 = uniform_u32(w[k] & KACC_SLOT_MASK);
+          attribute_group<Z, kNT>(a, sh, s_d + (r - (tid & 63)), w[k], s0, prev[k],
+                                  st.proc_energy, st.proc_power);
+          continue;
+        }
+      }
       if (r >= rows) continue;
       const uint64_t sl = w[k] & KACC_SLOT_MASK;
       if (sl >= st.proc_slots) {
@@ -858,6 +955,11 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 4: launch_zv<4, 4>(b, s, st); return true;
     case 8: launch_zv<4, 8>(b, s, st); return true;
     case 9: launch_zv<4, 9>(b, s, st); return true;
+    case 16: launch_zv<4, 16>(b, s, st); return true;
+    case 32: launch_zv<4, 32>(b, s, st); return true;
+    case 48: launch_zv<4, 48>(b, s, st); return true;
+    case 17: launch_zv<4, 17>(b, s, st); return true;
+    case 18: launch_zv<4, 18>(b, s, st); return true;
     default: return false;
   }
 }

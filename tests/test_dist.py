@@ -1,0 +1,64 @@
+"""Multi-process path on CPU: node-sharded ranks + all-reduced namespace totals (gloo, world 2).
+
+The GPU run uses one process per GPU and RCCL; the sharding plan and the
+reduction are the same code paths, exercised here with the oracle standing in
+for the engine on each rank (no GPU in this container).
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kepler_amd import fleet, shard
+    from oracle.oracle import Oracle
+
+    L = fleet.make_layout(24, [300, 2000, 5, 0, 700, 64] * 4, 4, seed=31, n_namespaces=6, shuffle_slots=True)
+    sim = fleet.FleetSim(L, seed=31, churn=0.05, read_error_frac=0.05)
+    lo, hi, sl = shard.shard(L, world)[rank]
+    o = Oracle(L.zones, **sl.capacities())
+    for _ in range(3):
+        a = sim.next_interval()  # every rank replays the same fleet inputs
+        sub, sizes, _ = fleet.subset_interval(a, np.arange(lo, hi), L.zones)
+        o.interval(sub, sizes)
+    e, p = o.namespace_totals(*sl.namespace_csr())
+    te = torch.from_numpy(e.view(np.int64).copy())
+    tp = torch.from_numpy(p.copy())
+    dist.all_reduce(te)  # two's-complement int64 sum == modular u64 sum
+    dist.all_reduce(tp)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "e.npy"), te.numpy().view(np.uint64))
+        np.save(os.path.join(out_dir, "p.npy"), tp.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_namespace_totals(tmp_path, oracle_lib):
+    from kepler_amd import fleet
+    from oracle.oracle import Oracle
+
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    L = fleet.make_layout(24, [300, 2000, 5, 0, 700, 64] * 4, 4, seed=31, n_namespaces=6, shuffle_slots=True)
+    sim = fleet.FleetSim(L, seed=31, churn=0.05, read_error_frac=0.05)
+    o = Oracle(L.zones, **L.capacities())
+    for _ in range(3):
+        o.interval(sim.next_interval(), L.sizes())
+    e_full, p_full = o.namespace_totals(*L.namespace_csr())
+    np.testing.assert_array_equal(np.load(tmp_path / "e.npy"), e_full)
+    np.testing.assert_allclose(np.load(tmp_path / "p.npy"), p_full, rtol=1e-12)
