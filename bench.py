@@ -187,6 +187,20 @@ def main():
     acc.sync(stream)  # surfaces any device-detected range error
     kernel_ms = [a.elapsed_time(b) for a, b in events]
 
+    # same-box reference for the roofline: a 1.28 GB device-to-device copy
+    src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
+    dst = torch.empty_like(src)
+    cps = []
+    for _ in range(5):
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        dst.copy_(src)
+        c1.record()
+        c1.synchronize()
+        cps.append(c0.elapsed_time(c1))
+    copy_gbps = 2 * src.numel() * 8 / (float(np.median(cps[1:])) * 1e-3) / 1e9
+    del src, dst
+
     wall_t = torch.tensor([wall], dtype=torch.float64, device="cuda")
     procs_t = torch.tensor([sizes["n_procs"], sizes["n_nodes"]], dtype=torch.float64, device="cuda")
     if world > 1:
@@ -244,7 +258,9 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
-            "kernel": "kacc::interval_kernel<4>",
+            "kernel": "kacc::interval_kernel<4> (+ generic_kernel<4>, empty at config 3)",
+            "same_box_copy_GBps": copy_gbps,
+            "frac_of_copy": achieved / copy_gbps,
         },
         "cpu_baseline": None,
     }

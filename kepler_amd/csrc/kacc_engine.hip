@@ -20,6 +20,7 @@
 // total 8Z B + power 8Z B out.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
@@ -33,10 +34,8 @@
 
 namespace kacc {
 
-constexpr int kThreads = 512;                // workgroup of the interval kernel (8 waves)
 constexpr int kTree = 256;                   // lanes of the canonical node-total tree
 constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
-constexpr int kRowsPerThread = kRowsLds / kThreads;
 constexpr int kLoadsPerLane = kRowsLds / kTree;
 constexpr int kUnroll = 2;                   // process rows in flight per lane (generic path)
 constexpr int kBlock = 256;                  // namespace kernel workgroup
@@ -52,6 +51,13 @@ constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
 constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
 constexpr int kVarOcc2 = 16;           // 2 workgroups per CU (no register cap)
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
+constexpr int kVarWide = 64;           // 1024-thread workgroups, 2 rows per lane
+constexpr int kGenThreads = 512;       // generic (big-node) workgroup
+
+template <int V>
+constexpr int kTpb = (V & kVarWide) ? 1024 : 512;  // threads per workgroup
+template <int V>
+constexpr int kRpt = kRowsLds / kTpb<V>;            // fast-path rows per lane
 
 // device error bits (KACC_ERANGE)
 constexpr uint32_t kErrNode = 1u << 0;
@@ -76,6 +82,8 @@ struct DevState {
   double *pod_power, *pod_cpu_delta, *pod_cpu_total;
   uint64_t proc_slots, ctr_slots, vm_slots, pod_slots;
   uint32_t *err;
+  uint32_t *gen_list;  // [nodes] nodes routed to the generic kernel this launch
+  uint32_t *gen_ctr;   // [0] list length, [1] dequeue head, [2] exits (re-armed by the last exit)
 };
 
 struct NodeShared {
@@ -108,6 +116,24 @@ __device__ __forceinline__ void load_row(const uint64_t *__restrict__ base, uint
 #pragma unroll
     for (int k = 0; k < Z / 2; ++k) {
       const u64x2 x = p[k];
+      out[2 * k] = x.x;
+      out[2 * k + 1] = x.y;
+    }
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) out[z] = base[s * Z + z];
+  }
+}
+
+template <int Z>
+__device__ __forceinline__ void load_row_f64(const double *__restrict__ base, uint64_t s,
+                                             double (&out)[Z]) {
+  if constexpr (Z % 2 == 0) {
+    using f64x2 = __attribute__((ext_vector_type(2))) double;
+    const f64x2 *p = reinterpret_cast<const f64x2 *>(base + s * Z);
+#pragma unroll
+    for (int k = 0; k < Z / 2; ++k) {
+      const f64x2 x = p[k];
       out[2 * k] = x.x;
       out[2 * k + 1] = x.y;
     }
@@ -260,19 +286,83 @@ __device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShar
   }
 }
 
+// Phase A for one zone (thread z < Z): node.go:10-84 / node.go:101-131.
+template <int Z>
+__device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState &st, uint32_t n,
+                                          int z, NodeShared &sh) {
+  const bool first = st.node_has_prev[n] == 0u;
+  const uint64_t i = static_cast<uint64_t>(n) * Z + z;
+  const double ratio = b.node_usage_ratio[n];
+  const uint64_t abs_e = b.zone_energy[i];
+  uint64_t active;
+  double p = 0.0, ap = 0.0, ip = 0.0;
+  if (first) {  // firstNodeRead, node.go:111-128
+    active = go_f64_to_u64(u2f(abs_e) * ratio);
+    st.node_active_total[i] = active;
+    st.node_idle_total[i] = abs_e - active;
+  } else {  // calculateNodePower, node.go:50-68
+    const double dt = go_duration_seconds(go_sub_mono(b.node_ts_ns[n], st.node_ts[n]));
+    const uint64_t delta = energy_delta(abs_e, st.node_energy_total[i], b.zone_max[i]);
+    active = go_f64_to_u64(u2f(delta) * ratio);
+    st.node_active_total[i] = st.node_active_total[i] + active;
+    st.node_idle_total[i] = st.node_idle_total[i] + (delta - active);
+    p = u2f(delta) / dt;
+    ap = p * ratio;
+    ip = p - ap;
+  }
+  st.node_energy_total[i] = abs_e;
+  st.node_active_energy[i] = active;
+  st.node_power[i] = p;
+  st.node_active_power[i] = ap;
+  st.node_idle_power[i] = ip;
+  sh.active_energy[z] = active;
+  sh.power[z] = p;
+  sh.active_power[z] = ap;
+  if (z == 0) sh.first = first ? 1u : 0u;
+}
+
+struct NodeRanges {
+  uint32_t p0, p1, c0, c1, v0, v1, q0, q1;
+};
+
+// Row ranges of node n, clamped so a malformed batch cannot fault.
+__device__ __forceinline__ NodeRanges node_ranges(const kacc_interval &b, const DevState &st,
+                                                  uint32_t n, int tid) {
+  NodeRanges r{b.proc_off[n], b.proc_off[n + 1], b.ctr_off[n], b.ctr_off[n + 1],
+               b.vm_off[n],   b.vm_off[n + 1],   b.pod_off[n], b.pod_off[n + 1]};
+  if (r.p1 > b.n_procs || r.p0 > r.p1 || r.c1 > b.n_ctrs || r.c0 > r.c1 || r.v1 > b.n_vms ||
+      r.v0 > r.v1 || r.q1 > b.n_pods || r.q0 > r.q1) {
+    if (tid == 0) raise_err(st.err, kErrOffsets);
+    r.p1 = min(r.p1, b.n_procs);
+    r.p0 = min(r.p0, r.p1);
+    r.c1 = min(r.c1, b.n_ctrs);
+    r.c0 = min(r.c0, r.c1);
+    r.v1 = min(r.v1, b.n_vms);
+    r.v0 = min(r.v0, r.v1);
+    r.q1 = min(r.q1, b.n_pods);
+    r.q0 = min(r.q0, r.q1);
+  }
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ bool fits_fast(const NodeRanges &r) {
+  return (V & kVarUnstaged) == 0 && r.p1 - r.p0 <= static_cast<uint32_t>(kRowsLds) &&
+         (r.c1 - r.c0) + (r.v1 - r.v0) + (r.q1 - r.q0) <= static_cast<uint32_t>(kTpb<V>);
+}
+
 // Generic path (big nodes / many aggregates): loops, Δ re-read from global.
 template <int Z, int V>
-__device__ void generic_node(const kacc_interval &b, const DevState &st, const uint32_t n,
-                             const uint32_t p0, const uint32_t p1, const uint32_t c0,
-                             const uint32_t c1, const uint32_t v0, const uint32_t v1,
-                             const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh);
-
-template <int Z, int V>
-__global__ __launch_bounds__(kThreads, ((V & kVarOcc2) || Z > 4) ? 2 : 6) void interval_kernel(const kacc_interval b, const DevState st) {
+__global__ __launch_bounds__(kTpb<V>, (V & kVarWide) ? ((Z <= 4) ? 8 : 4)
+                                      : (((V & kVarOcc2) || Z > 4) ? 2 : 6))
+void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restrict__ gen_list,
+                     uint32_t *__restrict__ gen_ctr) {
+  constexpr int kThreads = kTpb<V>;
+  constexpr int kRowsPerThread = kRpt<V>;
   constexpr bool kNT = (V & kVarNtStores) != 0;
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
-  __shared__ double s_cd[kThreads];  // container Δ of this interval (fast path)
-  __shared__ double s_ct[kThreads];  // container running CPU total (fast path)
+  __shared__ double s_cd[kThreads];  // container Δ of this interval
+  __shared__ double s_ct[kThreads];  // container running CPU total
   __shared__ double red[kTree];
   __shared__ NodeShared sh;
 
@@ -289,65 +379,17 @@ __global__ __launch_bounds__(kThreads, ((V & kVarOcc2) || Z > 4) ? 2 : 6) void i
     if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
     return;
   }
-
-  // ---- row ranges (clamped so a malformed batch cannot fault) ---------------
-  uint32_t p0 = b.proc_off[n], p1 = b.proc_off[n + 1];
-  uint32_t c0 = b.ctr_off[n], c1 = b.ctr_off[n + 1];
-  uint32_t v0 = b.vm_off[n], v1 = b.vm_off[n + 1];
-  uint32_t q0 = b.pod_off[n], q1 = b.pod_off[n + 1];
-  if (p1 > b.n_procs || p0 > p1 || c1 > b.n_ctrs || c0 > c1 || v1 > b.n_vms || v0 > v1 ||
-      q1 > b.n_pods || q0 > q1) {
-    if (tid == 0) raise_err(st.err, kErrOffsets);
-    p1 = min(p1, b.n_procs);
-    p0 = min(p0, p1);
-    c1 = min(c1, b.n_ctrs);
-    c0 = min(c0, c1);
-    v1 = min(v1, b.n_vms);
-    v0 = min(v0, v1);
-    q1 = min(q1, b.n_pods);
-    q0 = min(q0, q1);
-  }
-  const uint32_t rows = p1 - p0, nc = c1 - c0, nv = v1 - v0, nq = q1 - q0;
-  const bool fast = (V & kVarUnstaged) == 0 && rows <= static_cast<uint32_t>(kRowsLds) &&
-                    nc + nv + nq <= static_cast<uint32_t>(kThreads);
-
-  // ---- A: node zones (threads z < Z): node.go:10-84 / node.go:101-131 -----------
-  if (tid < Z) {
-    const bool first = st.node_has_prev[n] == 0u;
-    const uint64_t i = static_cast<uint64_t>(n) * Z + tid;
-    const double ratio = b.node_usage_ratio[n];
-    const uint64_t abs_e = b.zone_energy[i];
-    uint64_t active;
-    double p = 0.0, ap = 0.0, ip = 0.0;
-    if (first) {  // firstNodeRead, node.go:111-128
-      active = go_f64_to_u64(u2f(abs_e) * ratio);
-      st.node_active_total[i] = active;
-      st.node_idle_total[i] = abs_e - active;
-    } else {  // calculateNodePower, node.go:50-68
-      const double dt = go_duration_seconds(go_sub_mono(b.node_ts_ns[n], st.node_ts[n]));
-      const uint64_t delta = energy_delta(abs_e, st.node_energy_total[i], b.zone_max[i]);
-      active = go_f64_to_u64(u2f(delta) * ratio);
-      st.node_active_total[i] = st.node_active_total[i] + active;
-      st.node_idle_total[i] = st.node_idle_total[i] + (delta - active);
-      p = u2f(delta) / dt;
-      ap = p * ratio;
-      ip = p - ap;
-    }
-    st.node_energy_total[i] = abs_e;
-    st.node_active_energy[i] = active;
-    st.node_power[i] = p;
-    st.node_active_power[i] = ap;
-    st.node_idle_power[i] = ip;
-    sh.active_energy[tid] = active;
-    sh.power[tid] = p;
-    sh.active_power[tid] = ap;
-    if (tid == 0) sh.first = first ? 1u : 0u;
-  }
-
-  if (!fast) {
-    generic_node<Z, V>(b, st, n, p0, p1, c0, c1, v0, v1, q0, q1, red, sh);
+  const NodeRanges rg = node_ranges(b, st, n, tid);
+  if (!fits_fast<V>(rg)) {  // handled by generic_kernel (work list, dequeued)
+    if (tid == 0) gen_list[atomicAdd(gen_ctr, 1u)] = n;
     return;
   }
+  const uint32_t p0 = rg.p0, p1 = rg.p1, c0 = rg.c0, c1 = rg.c1, v0 = rg.v0, v1 = rg.v1,
+                 q0 = rg.q0, q1 = rg.q1;
+  const uint32_t rows = p1 - p0, nc = c1 - c0, nv = v1 - v0, nq = q1 - q0;
+
+  // ---- A: node zones (threads z < Z) ------------------------------------------
+  if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
 
   // ======================= fast path: one node fits the block ===================
   // Every global load the node needs is issued here, before the first barrier:
@@ -575,6 +617,7 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
                              const uint32_t c1, const uint32_t v0, const uint32_t v1,
                              const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh) {
   constexpr bool kNT = (V & kVarNtStores) != 0;
+  constexpr int kThreads = kGenThreads;
   const int tid = threadIdx.x;
   const uint32_t rows = p1 - p0;
   const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
@@ -758,6 +801,42 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
   }
 }
 
+// Nodes that do not fit a fast workgroup (> 2048 rows or > kTpb aggregates,
+// e.g. BASELINE config 5's 10–50k-process nodes), dequeued one at a time
+// (one returning atomicAdd per node; load-balanced for skewed fleets).
+template <int Z, int V>
+__global__ __launch_bounds__(kGenThreads) void generic_kernel(const kacc_interval b,
+                                                              const DevState st,
+                                                              const uint32_t *__restrict__ gen_list,
+                                                              uint32_t *__restrict__ gen_ctr) {
+  __shared__ double red[kTree];
+  __shared__ NodeShared sh;
+  __shared__ uint32_t s_idx;
+  const int tid = threadIdx.x;
+  const uint32_t count = __hip_atomic_load(gen_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (tid == 0) s_idx = count ? atomicAdd(gen_ctr + 1, 1u) : count;
+    __syncthreads();
+    const uint32_t idx = s_idx;
+    __syncthreads();
+    if (idx >= count) break;
+    const uint32_t n = gen_list[idx];
+    const NodeRanges rg = node_ranges(b, st, n, tid);
+    if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
+    generic_node<Z, V>(b, st, n, rg.p0, rg.p1, rg.c0, rg.c1, rg.v0, rg.v1, rg.q0, rg.q1, red, sh);
+    __syncthreads();  // LDS (red, sh) reused by the next node
+  }
+  // The last workgroup to leave re-arms the list for the next launch (no
+  // per-launch memset): [0] length, [1] dequeue head, [2] exit count.
+  if (tid == 0) {
+    if (atomicAdd(gen_ctr + 2, 1u) == gridDim.x - 1) {
+      __hip_atomic_store(gen_ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen_ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Namespace totals: one wave per namespace; lane l sums pods l, l+64, ... in
 // CSR order, then the 64 lane sums are halved pairwise (l += l+s, s=32..1).
 // u64 energy sums are order independent; f64 power follows this fixed order.
@@ -788,10 +867,12 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
     }
     uint64_t er[Z];
     load_row<Z>(pe, s, er);
+    double pr[Z];
+    load_row_f64<Z>(pp, s, pr);
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
       e[z] += er[z];
-      p[z] = p[z] + pp[s * Z + z];
+      p[z] = p[z] + pr[z];
     }
   }
 #pragma unroll
@@ -843,6 +924,8 @@ struct kacc_ctx {
   void *tables[KACC_T_COUNT] = {};
   uint64_t counts[KACC_T_COUNT] = {};
   uint32_t *d_err = nullptr;
+  uint32_t *d_gen_list = nullptr;
+  uint32_t *d_gen_ctr = nullptr;
   std::string err;
 };
 
@@ -922,12 +1005,21 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.vm_slots = ctx->cfg.vm_slots;
   s.pod_slots = ctx->cfg.pod_slots;
   s.err = ctx->d_err;
+  s.gen_list = ctx->d_gen_list;
+  s.gen_ctr = ctx->d_gen_ctr;
   return s;
 }
 
+// One interval = reset the big-node work list, the fast kernel (one workgroup
+// per node; oversized nodes are appended to the list) and the generic kernel
+// that drains the list.
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
-  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kThreads), 0, st, b, s);
+  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
+                     s, s.gen_list, s.gen_ctr);
+  const uint32_t gen_grid = std::min<uint32_t>(b.n_nodes, 256u);
+  hipLaunchKernelGGL((kacc::generic_kernel<Z, V>), dim3(gen_grid), dim3(kacc::kGenThreads), 0, st,
+                     b, s, s.gen_list, s.gen_ctr);
 }
 
 void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
@@ -960,6 +1052,8 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 48: launch_zv<4, 48>(b, s, st); return true;
     case 17: launch_zv<4, 17>(b, s, st); return true;
     case 18: launch_zv<4, 18>(b, s, st); return true;
+    case 64: launch_zv<4, 64>(b, s, st); return true;
+    case 96: launch_zv<4, 96>(b, s, st); return true;
     default: return false;
   }
 }
@@ -1056,8 +1150,11 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
       return bail(KACC_ENOMEM);
     }
   }
-  if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess) {
-    fail(ctx, KACC_ENOMEM, "hipMalloc err word: %s", hipGetErrorString(e));
+  if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_gen_list, std::max<uint64_t>(cfg->nodes, 1) * sizeof(uint32_t))) !=
+          hipSuccess ||
+      (e = hipMalloc(&ctx->d_gen_ctr, 16)) != hipSuccess) {
+    fail(ctx, KACC_ENOMEM, "hipMalloc work words: %s", hipGetErrorString(e));
     return bail(KACC_ENOMEM);
   }
   if ((rc = kacc_reset(ctx)) != KACC_OK) return bail(rc);
@@ -1072,6 +1169,8 @@ void kacc_destroy(kacc_ctx *ctx) {
   for (int t = 0; t < KACC_T_COUNT; ++t)
     if (ctx->tables[t]) (void)hipFree(ctx->tables[t]);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
+  if (ctx->d_gen_list) (void)hipFree(ctx->d_gen_list);
+  if (ctx->d_gen_ctr) (void)hipFree(ctx->d_gen_ctr);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1090,6 +1189,7 @@ int kacc_reset(kacc_ctx *ctx) {
                                  std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
                                  ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(ctx->d_gen_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return KACC_OK;
 }

@@ -21,7 +21,7 @@ def main():
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
-    variants = [int(x) for x in os.environ.get("VARIANTS", "0,16,32,48,1,17,2,3").split(",")]
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,16,32,64,96,1,2,3").split(",")]
     rounds = int(os.environ.get("ROUNDS", "10"))
     cfg = int(os.environ.get("CONFIG", "3"))
     torch.cuda.set_device(0)
@@ -34,8 +34,11 @@ def main():
     assert stream != 0
     prime = to_device(sim.next_interval())
     acc.run_interval(interval_from_tensors(prime, layout.sizes()), stream)
-    a = to_device(sim.next_interval())
-    it = interval_from_tensors(a, layout.sizes())
+    # distinct input sets cycled like bench.py (no cache reuse between launches)
+    n_distinct = int(os.environ.get("DISTINCT", "4"))
+    dev = [to_device(sim.next_interval()) for _ in range(n_distinct)]
+    ivs = [interval_from_tensors(a, layout.sizes()) for a in dev]
+    it = ivs[0]
     Z = layout.zones
     sizes = layout.sizes()
     nbytes = accel.interval_bytes(Z, *[sizes[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
@@ -43,9 +46,12 @@ def main():
     for v in variants:  # warm
         acc.run_variant(it, stream, v)
     acc.sync(stream)
+    launch = 0
     for _ in range(rounds):
         for v in variants:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            it = ivs[launch % n_distinct]
+            launch += 1
             e0.record()
             acc.run_variant(it, stream, v)
             e1.record()
@@ -66,7 +72,19 @@ def main():
         e1.synchronize()
         ns_t.append(e0.elapsed_time(e1))
     acc.sync(stream)
-    out = {"config": cfg, "sizes": sizes, "bytes_per_launch": nbytes,
+    # same-box reference: a 1.28 GB device copy (torch copy_ kernel)
+    src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
+    dst = torch.empty_like(src)
+    cp = []
+    for _ in range(rounds + 2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        e1.synchronize()
+        cp.append(e0.elapsed_time(e1))
+    copy_gbps = 2 * src.numel() * 8 / (np.median(cp[2:]) * 1e-3) / 1e9
+    out = {"config": cfg, "copy_GBps": copy_gbps, "sizes": sizes, "bytes_per_launch": nbytes,
            "variants": {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for v, t in times.items()},
            "namespace_ms": float(np.median(ns_t))}
     if 0 in times:
