@@ -52,6 +52,7 @@ constexpr int kVarNtStores = 8;        // non-temporal stores for the row output
 constexpr int kVarOcc2 = 16;           // 2 workgroups per CU (no register cap)
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
 constexpr int kVarWide = 64;           // 1024-thread workgroups, 2 rows per lane
+constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
 constexpr int kGenThreads = 512;       // generic (big-node) workgroup
 
 template <int V>
@@ -234,7 +235,7 @@ __device__ __forceinline__ void load_group(const uint64_t *__restrict__ base, ui
 
 template <int Z, bool NT>
 __device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShared &sh,
-                                                const double *s_d_group, uint32_t w_lane,
+                                                const double *s_d_group, const uint32_t *s_w_group,
                                                 uint64_t s0, const uint64_t (&prev)[Z],
                                                 uint64_t *__restrict__ energy,
                                                 double *__restrict__ power) {
@@ -249,7 +250,7 @@ __device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShar
     const uint32_t piece = lane + 64u * j;
     const uint32_t row = piece / kHalf;
     const uint32_t zp = piece % kHalf;
-    const uint32_t wr = __shfl(w_lane, static_cast<int>(row), 64);
+    const uint32_t wr = s_w_group[row];
     const bool is_new = (wr & KACC_SLOT_NEW) != 0;
     const double ratio = s_d_group[row] / a.nd;  // the row's own IEEE division
     uint64_t E[2];
@@ -361,6 +362,7 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
   constexpr int kRowsPerThread = kRpt<V>;
   constexpr bool kNT = (V & kVarNtStores) != 0;
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
+  __shared__ uint32_t s_w[kRowsLds];  // and their slot words (frees VGPRs across barriers)
   __shared__ double s_cd[kThreads];  // container Δ of this interval
   __shared__ double s_ct[kThreads];  // container running CPU total
   __shared__ double red[kTree];
@@ -408,34 +410,42 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
     w[k] = in ? pslot[r] : 0xffffffffu;
   }
   // aggregate role of this lane: 1 container, 2 VM, 3 pod
-  uint32_t role = 0, j = 0, a_beg = 0, a_end = 0, a_w = 0xffffffffu;
-  uint64_t a_cap = 0;
-  if ((V & kVarSkipAggregates) == 0) {
-    if (static_cast<uint32_t>(tid) < nc) {
-      role = 1;
-      j = tid;
+  // role/index/validity are recomputed from tid and the node's (SGPR) counts
+  // wherever needed instead of being held in VGPRs across the barriers.
+  const uint32_t utid = static_cast<uint32_t>(tid);
+  auto role_of = [&]() -> uint32_t {
+    if ((V & kVarSkipAggregates) != 0) return 0u;
+    return utid < nc ? 1u : utid < nc + nv ? 2u : utid < nc + nv + nq ? 3u : 0u;
+  };
+  auto index_of = [&]() -> uint32_t {  // position inside the role's range
+    return utid < nc ? utid : utid < nc + nv ? utid - nc : utid - nc - nv;
+  };
+  uint32_t a_beg = 0, a_end = 0, a_w = 0xffffffffu;
+  {
+    const uint32_t role = role_of(), j = index_of();
+    if (role == 1) {
       a_beg = j == 0 ? p0 : b.ctr_proc_end[c0 + j - 1];
       a_end = b.ctr_proc_end[c0 + j];
       a_w = b.ctr_slot[c0 + j];
-      a_cap = st.ctr_slots;
-    } else if (static_cast<uint32_t>(tid) < nc + nv) {
-      role = 2;
-      j = tid - nc;
+    } else if (role == 2) {
       a_beg = j == 0 ? (nc ? b.ctr_proc_end[c1 - 1] : p0) : b.vm_proc_end[v0 + j - 1];
       a_end = b.vm_proc_end[v0 + j];
       a_w = b.vm_slot[v0 + j];
-      a_cap = st.vm_slots;
-    } else if (static_cast<uint32_t>(tid) < nc + nv + nq) {
-      role = 3;
-      j = tid - nc - nv;
+    } else if (role == 3) {
       a_beg = j == 0 ? c0 : b.pod_ctr_end[q0 + j - 1];
       a_end = b.pod_ctr_end[q0 + j];
       a_w = b.pod_slot[q0 + j];
-      a_cap = st.pod_slots;
     }
   }
-  const uint64_t a_s = a_w & KACC_SLOT_MASK;
-  const bool a_ok = role != 0 && a_s < a_cap;
+  auto a_cap = [&]() -> uint64_t {
+    const uint32_t role = role_of();
+    return role == 1 ? st.ctr_slots : role == 2 ? st.vm_slots : role == 3 ? st.pod_slots : 0;
+  };
+  const uint32_t a_s = a_w & KACC_SLOT_MASK;
+  auto a_ok_f = [&]() -> bool { return role_of() != 0 && a_s < a_cap(); };
+  const bool a_ok = a_ok_f();
+  const uint32_t role = role_of();
+  const uint32_t j = index_of();
   // per-role tables, re-derived at each use (keeps 8 VGPRs of pointers dead)
   auto a_energy = [&]() { return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy; };
   auto a_power = [&]() { return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power; };
@@ -472,7 +482,7 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
   uint64_t a_prev[Z];
   double a_total = 0.0;
   if (a_ok) {
-    load_row<Z>(a_energy(), a_s, a_prev);
+    if constexpr ((V & kVarLateAgg) == 0) load_row<Z>(a_energy(), a_s, a_prev);
     if (role != 2 && !(a_w & KACC_SLOT_NEW)) a_total = a_cpu_total()[a_s];
   } else {
 #pragma unroll
@@ -484,7 +494,10 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
 #pragma unroll
   for (int k = 0; k < kRowsPerThread; ++k) {
     const uint32_t r = tid + k * kThreads;
-    if (r < rows) s_d[r] = d[k];
+    if (r < rows) {
+      s_d[r] = d[k];
+      s_w[r] = w[k];
+    }
   }
   __syncthreads();
   if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
@@ -576,39 +589,44 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
     st.node_cpu_delta[n] = a.nd;
     st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
-  if (a_ok) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+  auto aggregate_out = [&]() {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+    if (!a_ok) return;
+    if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), a_s, a_prev);
     uint64_t E[Z];
     double P[Z];
     attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0,
                      a_prev, E, P);
     store_row<Z, kNT, uint64_t>(a_energy(), a_s, E);
     store_row<Z, kNT, double>(a_power(), a_s, P);
-  }
+  };
+  if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
   if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint32_t r = tid + k * kThreads;
       if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
         if (contig & (1u << k)) {
-          const uint64_t s0 = uniform_u32(w[k] & KACC_SLOT_MASK);
-          attribute_group<Z, kNT>(a, sh, s_d + (r - (tid & 63)), w[k], s0, prev[k],
+          const uint64_t s0 = uniform_u32(s_w[r - (tid & 63)] & KACC_SLOT_MASK);
+          attribute_group<Z, kNT>(a, sh, s_d + (r - (tid & 63)), s_w + (r - (tid & 63)), s0, prev[k],
                                   st.proc_energy, st.proc_power);
           continue;
         }
       }
       if (r >= rows) continue;
-      const uint64_t sl = w[k] & KACC_SLOT_MASK;
+      const uint32_t wk = s_w[r];
+      const uint64_t sl = wk & KACC_SLOT_MASK;
       if (sl >= st.proc_slots) {
         raise_err(st.err, kErrSlot);
         continue;
       }
       uint64_t E[Z];
       double P[Z];
-      attribute_row<Z>(a, a.live, s_d[r], (w[k] & KACC_SLOT_NEW) != 0, prev[k], E, P);
+      attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E, P);
       store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
       store_row<Z, kNT, double>(st.proc_power, sl, P);
     }
   }
+  if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
 }
 
 template <int Z, int V>
@@ -1054,6 +1072,8 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 18: launch_zv<4, 18>(b, s, st); return true;
     case 64: launch_zv<4, 64>(b, s, st); return true;
     case 96: launch_zv<4, 96>(b, s, st); return true;
+    case 128: launch_zv<4, 128>(b, s, st); return true;
+    case 192: launch_zv<4, 192>(b, s, st); return true;
     default: return false;
   }
 }

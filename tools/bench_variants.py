@@ -21,7 +21,7 @@ def main():
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
-    variants = [int(x) for x in os.environ.get("VARIANTS", "0,16,32,64,96,1,2,3").split(",")]
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,32,64,128,192,1,2,3").split(",")]
     rounds = int(os.environ.get("ROUNDS", "10"))
     cfg = int(os.environ.get("CONFIG", "3"))
     torch.cuda.set_device(0)
