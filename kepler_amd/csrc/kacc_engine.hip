@@ -38,10 +38,12 @@ constexpr int kTree = 256;                   // lanes of the canonical node-tota
 constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
 constexpr int kLoadsPerLane = kRowsLds / kTree;
 constexpr int kUnroll = 2;                   // process rows in flight per lane (generic path)
+constexpr int kSegLoads = 8;                 // segment rows loaded per step (generic path)
 constexpr int kBlock = 256;                  // namespace kernel workgroup
 template <int Z>
 constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 64-row groups
-constexpr int kNsWave = 64;                  // lanes per namespace (namespace_kernel)
+constexpr int kNsLanes = 16;                 // lanes per namespace (namespace_kernel)
+constexpr int kNsUnroll = 4;                 // pods in flight per namespace lane
 
 // Debug variants (kacc_debug_run_variant, timing ablations only; results of a
 // variant != 0 are NOT the reference semantics).
@@ -686,10 +688,17 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
       }
       double delta = 0.0;
       double total = (w & KACC_SLOT_NEW) ? 0.0 : st.ctr_cpu_total[sl];
-      for (uint32_t i = beg - p0; i < end - p0; ++i) {
-        const double di = dcpu[i];
-        delta = delta + di;
-        total = total + di;
+      // rows loaded kSegLoads at a time (independent), added in listing order
+      for (uint32_t i0 = beg - p0; i0 < end - p0; i0 += kSegLoads) {
+        double v[kSegLoads];
+#pragma unroll
+        for (int u = 0; u < kSegLoads; ++u) v[u] = i0 + u < end - p0 ? dcpu[i0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kSegLoads; ++u)
+          if (i0 + u < end - p0) {
+            delta = delta + v[u];
+            total = total + v[u];
+          }
       }
       st.ctr_cpu_delta[sl] = delta;
       st.ctr_cpu_total[sl] = total;
@@ -723,11 +732,25 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
       }
       double delta = 0.0;
       double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
-      for (uint32_t c = beg; c < end; ++c) {
-        const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
-        if (cs >= st.ctr_slots) continue;
-        delta = delta + st.ctr_cpu_delta[cs];
-        total = total + st.ctr_cpu_total[cs];
+      for (uint32_t c0_ = beg; c0_ < end; c0_ += kSegLoads / 2) {
+        constexpr int kU = kSegLoads / 2;
+        uint64_t cs[kU];
+        double cd[kU], ct[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          cs[u] = c0_ + u < end ? (b.ctr_slot[c0_ + u] & KACC_SLOT_MASK) : ~0ull;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const bool ok = cs[u] < st.ctr_slots;
+          cd[u] = ok ? st.ctr_cpu_delta[cs[u]] : 0.0;
+          ct[u] = ok ? st.ctr_cpu_total[cs[u]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (cs[u] < st.ctr_slots) {
+            delta = delta + cd[u];
+            total = total + ct[u];
+          }
       }
       st.pod_cpu_delta[sl] = delta;
       st.pod_cpu_total[sl] = total;
@@ -759,7 +782,10 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
   }
   if constexpr ((V & kVarSkipProcs) == 0) {
     const uint32_t *__restrict__ pslot = b.proc_slot + p0;
-    for (uint32_t base = tid; base < rows; base += kThreads * kUnroll) {
+    // wave-uniform trip count: every lane stays active for the group votes
+    // (__all) below; rows past the node's end are masked per lane
+    for (uint32_t it = 0; it * static_cast<uint32_t>(kThreads * kUnroll) < rows; ++it) {
+      const uint32_t base = tid + it * kThreads * kUnroll;
       double d[kUnroll];
       uint32_t w[kUnroll];
       uint64_t prev[kUnroll][Z];
@@ -770,9 +796,20 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
         w[u] = in ? pslot[r] : 0xffffffffu;
         d[u] = in ? dcpu[r] : 0.0;
       }
+      uint32_t contig = 0;  // bit u: 64-row group u of this wave is transposed
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint64_t sl = w[u] & KACC_SLOT_MASK;
+        if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+          const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
+          const bool mine = (base + u * kThreads) < rows && sl == s0 + (tid & 63) &&
+                            s0 + 64 <= st.proc_slots;
+          if (__all(mine)) {
+            contig |= 1u << u;
+            load_group<Z>(st.proc_energy, s0, prev[u]);
+            continue;
+          }
+        }
         if (sl < st.proc_slots) {
           load_row<Z>(st.proc_energy, sl, prev[u]);
         } else {
@@ -783,6 +820,14 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
         const uint32_t r = base + u * kThreads;
+        if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+          if (contig & (1u << u)) {
+            const uint32_t g = r - (tid & 63);
+            attribute_group<Z, kNT>(a, sh, dcpu + g, pslot + g, uniform_u32(w[u] & KACC_SLOT_MASK),
+                                    prev[u], st.proc_energy, st.proc_power);
+            continue;
+          }
+        }
         if (r >= rows) continue;
         const uint64_t sl = w[u] & KACC_SLOT_MASK;
         if (sl >= st.proc_slots) {
@@ -823,7 +868,7 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
 // e.g. BASELINE config 5's 10–50k-process nodes), dequeued one at a time
 // (one returning atomicAdd per node; load-balanced for skewed fleets).
 template <int Z, int V>
-__global__ __launch_bounds__(kGenThreads) void generic_kernel(const kacc_interval b,
+__global__ __launch_bounds__(kGenThreads, (Z <= 5 ? 4 : 2)) void generic_kernel(const kacc_interval b,
                                                               const DevState st,
                                                               const uint32_t *__restrict__ gen_list,
                                                               uint32_t *__restrict__ gen_ctr) {
@@ -855,9 +900,11 @@ __global__ __launch_bounds__(kGenThreads) void generic_kernel(const kacc_interva
   }
 }
 
-// Namespace totals: one wave per namespace; lane l sums pods l, l+64, ... in
-// CSR order, then the 64 lane sums are halved pairwise (l += l+s, s=32..1).
-// u64 energy sums are order independent; f64 power follows this fixed order.
+// Namespace totals: kNsLanes lanes per namespace (4 namespaces per wave);
+// lane l sums pods l, l+16, ... of its namespace in CSR order (loads issued
+// kNsUnroll at a time, adds in order), then the 16 lane sums are halved
+// pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
+// f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
 template <int Z>
 __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
                                                            const uint32_t *__restrict__ off,
@@ -866,9 +913,9 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
                                                            const double *__restrict__ pp,
                                                            uint64_t pod_slots, uint64_t *out_e,
                                                            double *out_p, uint32_t *err) {
-  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) / kNsWave;
-  const uint32_t lane = threadIdx.x % kNsWave;
-  if (k >= n_ns) return;
+  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) / kNsLanes;
+  const uint32_t lane = threadIdx.x % kNsLanes;
+  const bool active = k < n_ns;  // inactive lanes still join the shuffles
   unsigned long long e[Z];
   double p[Z];
 #pragma unroll
@@ -876,37 +923,49 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
     e[z] = 0;
     p[z] = 0.0;
   }
-  const uint32_t beg = off[k], end = off[k + 1];
-  for (uint32_t j = beg + lane; j < end; j += kNsWave) {
-    const uint64_t s = slots[j] & KACC_SLOT_MASK;
-    if (s >= pod_slots) {
-      raise_err(err, kErrNs);
-      continue;
-    }
-    uint64_t er[Z];
-    load_row<Z>(pe, s, er);
-    double pr[Z];
-    load_row_f64<Z>(pp, s, pr);
+  const uint32_t beg = active ? off[k] : 0u, end = active ? off[k + 1] : 0u;
+  for (uint32_t j0 = beg + lane; j0 < end; j0 += kNsLanes * kNsUnroll) {
+    uint32_t sl[kNsUnroll];
 #pragma unroll
-    for (int z = 0; z < Z; ++z) {
-      e[z] += er[z];
-      p[z] = p[z] + pr[z];
+    for (int u = 0; u < kNsUnroll; ++u) {
+      const uint32_t j = j0 + u * kNsLanes;
+      sl[u] = j < end ? (slots[j] & KACC_SLOT_MASK) : 0xffffffffu;
+    }
+    uint64_t er[kNsUnroll][Z];
+    double pr[kNsUnroll][Z];
+#pragma unroll
+    for (int u = 0; u < kNsUnroll; ++u) {
+      if (sl[u] < pod_slots) {
+        load_row<Z>(pe, sl[u], er[u]);
+        load_row_f64<Z>(pp, sl[u], pr[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kNsUnroll; ++u) {
+      const uint32_t j = j0 + u * kNsLanes;
+      if (j >= end) continue;
+      if (sl[u] >= pod_slots) {
+        raise_err(err, kErrNs);
+        continue;
+      }
+#pragma unroll
+      for (int z = 0; z < Z; ++z) {
+        e[z] += er[u][z];
+        p[z] = p[z] + pr[u][z];
+      }
     }
   }
 #pragma unroll
   for (int z = 0; z < Z; ++z) {
 #pragma unroll
-    for (int sft = kNsWave / 2; sft >= 1; sft >>= 1) {
-      e[z] += __shfl_down(e[z], sft, kNsWave);
-      p[z] = p[z] + __shfl_down(p[z], sft, kNsWave);
+    for (int sft = kNsLanes / 2; sft >= 1; sft >>= 1) {
+      e[z] += __shfl_down(e[z], sft, kNsLanes);
+      p[z] = p[z] + __shfl_down(p[z], sft, kNsLanes);
     }
   }
-  if (lane == 0) {
-#pragma unroll
-    for (int z = 0; z < Z; ++z) {
-      out_e[static_cast<uint64_t>(k) * Z + z] = e[z];
-      out_p[static_cast<uint64_t>(k) * Z + z] = p[z];
-    }
+  if (active && lane == 0) {
+    store_row<Z, false, unsigned long long>(reinterpret_cast<unsigned long long *>(out_e), k, e);
+    store_row<Z, false, double>(out_p, k, p);
   }
 }
 
@@ -1035,7 +1094,7 @@ template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
                      s, s.gen_list, s.gen_ctr);
-  const uint32_t gen_grid = std::min<uint32_t>(b.n_nodes, 256u);
+  const uint32_t gen_grid = std::min<uint32_t>(b.n_nodes, 512u);
   hipLaunchKernelGGL((kacc::generic_kernel<Z, V>), dim3(gen_grid), dim3(kacc::kGenThreads), 0, st,
                      b, s, s.gen_list, s.gen_ctr);
 }
@@ -1081,7 +1140,7 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
 template <int Z>
 void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const kacc_ctx *ctx,
                uint64_t *out_e, double *out_p, hipStream_t st) {
-  const uint32_t per_block = kacc::kBlock / kacc::kNsWave;
+  const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
   const uint32_t grid = (n_ns + per_block - 1) / per_block;
   hipLaunchKernelGGL((kacc::namespace_kernel<Z>), dim3(grid), dim3(kacc::kBlock), 0, st, n_ns, off,
                      slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],

@@ -279,8 +279,8 @@ int kor_interval(kor_state *st, const kacc_interval *b, int sum_mode) {
 // North-star namespace totals: sum of per-pod values grouped by
 // resource.Pod.Namespace (resource/types.go:106-110).  Kepler itself leaves
 // this to PromQL, so there is no Go order to follow; the engine's canonical
-// order is: lane l of 64 sums pods l, l+64, ... of the namespace in list
-// order, then the 64 lane sums are halved pairwise (l += l+s, s = 32..1).
+// order is: lane l of 16 sums pods l, l+16, ... of the namespace in list
+// order, then the 16 lane sums are halved pairwise (l += l+s, s = 8..1).
 // The u64 energy sums are order independent.
 int kor_namespace_totals(const kor_state *st, uint32_t n_ns, const uint32_t *ns_pod_off,
                          const uint32_t *ns_pod_slot, uint64_t *out_energy, double *out_power) {
@@ -288,15 +288,15 @@ int kor_namespace_totals(const kor_state *st, uint32_t n_ns, const uint32_t *ns_
   for (uint32_t k = 0; k < n_ns; ++k) {
     for (uint32_t z = 0; z < Z; ++z) {
       uint64_t e = 0;
-      double lane[64];
-      for (int l = 0; l < 64; ++l) lane[l] = 0.0;
+      double lane[16];
+      for (int l = 0; l < 16; ++l) lane[l] = 0.0;
       for (uint32_t j = ns_pod_off[k]; j < ns_pod_off[k + 1]; ++j) {
         const uint64_t s = ns_pod_slot[j] & KACC_SLOT_MASK;
         e += st->pod_energy[s * Z + z];
-        const uint32_t l = (j - ns_pod_off[k]) & 63u;
+        const uint32_t l = (j - ns_pod_off[k]) & 15u;
         lane[l] = lane[l] + st->pod_power[s * Z + z];
       }
-      for (int sft = 32; sft >= 1; sft >>= 1)
+      for (int sft = 8; sft >= 1; sft >>= 1)
         for (int l = 0; l < sft; ++l) lane[l] = lane[l] + lane[l + sft];
       out_energy[static_cast<uint64_t>(k) * Z + z] = e;
       out_power[static_cast<uint64_t>(k) * Z + z] = lane[0];

@@ -21,3 +21,10 @@ if [ "$1" = "prof" ]; then
   VARIANTS=0 ROUNDS=3 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$R/gpurun_out/pmc_write" -o run -- python "$R/tools/bench_variants.py" > "$R/gpurun_out/pmc_write.log" 2>&1 || exit $?
   echo "pmc done"
 fi
+if [ "$1" = "configs" ] || [ "$2" = "configs" ]; then
+  cd "$R"
+  timeout -k 10 400 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline --json-out gpurun_out/bench_c5.json > gpurun_out/bench_c5.log 2>&1 || exit $?
+  timeout -k 10 400 python bench.py --config 5 --node-order --steps 10 --warmup 2 --no-cpu-baseline --json-out gpurun_out/bench_c5_lpt.json > gpurun_out/bench_c5_lpt.log 2>&1 || exit $?
+  timeout -k 10 400 python bench.py --config 2 --steps 20 --warmup 3 --no-cpu-baseline --json-out gpurun_out/bench_c2.json > gpurun_out/bench_c2.log 2>&1 || exit $?
+  for f in bench_c5 bench_c5_lpt bench_c2; do python -c "import json;d=json.load(open('gpurun_out/$f.json'));print('$f', 'value',d['value'],'kernel_ms',d['kernel_ms'],'frac',d['roofline']['frac'],d['config']['workload'])"; done
+fi
