@@ -36,9 +36,7 @@ namespace kacc {
 
 constexpr int kTree = 256;                   // lanes of the canonical node-total tree
 constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
-constexpr int kLoadsPerLane = kRowsLds / kTree;
-constexpr int kUnroll = 2;                   // process rows in flight per lane (generic path)
-constexpr int kSegLoads = 8;                 // segment rows loaded per step (generic path)
+constexpr int kSegLoads = 8;                 // container rows loaded per step (pod kernel)
 constexpr int kBlock = 256;                  // namespace kernel workgroup
 template <int Z>
 constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 64-row groups
@@ -51,14 +49,20 @@ constexpr int kVarSkipAggregates = 1;  // skip containers / VMs / pods
 constexpr int kVarSkipProcs = 2;       // skip the process attribution pass
 constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
 constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
-constexpr int kVarOcc2 = 16;           // 2 workgroups per CU (no register cap)
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
-constexpr int kVarWide = 64;           // 1024-thread workgroups, 2 rows per lane
 constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
-constexpr int kGenThreads = 512;       // generic (big-node) workgroup
+constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
+constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
+constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk kernel idles)
+constexpr uint32_t kPodGrid = 256;     // deferred-pod kernel workgroups (kBlock threads)
+constexpr int kChunkRows = kRowsLds;   // big-node rows per chunk item
+constexpr int kChunkThreads = 512;     // chunk kernel workgroup
+constexpr int kChunkRpt = kChunkRows / kChunkThreads;
+constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node CPU total)
+constexpr uint32_t kChunkGrid = 512;   // persistent chunk-kernel workgroups (2 per CU resident)
 
 template <int V>
-constexpr int kTpb = (V & kVarWide) ? 1024 : 512;  // threads per workgroup
+constexpr int kTpb = 512;  // threads per workgroup (fast path)
 template <int V>
 constexpr int kRpt = kRowsLds / kTpb<V>;            // fast-path rows per lane
 
@@ -67,6 +71,14 @@ constexpr uint32_t kErrNode = 1u << 0;
 constexpr uint32_t kErrOffsets = 1u << 1;
 constexpr uint32_t kErrSlot = 1u << 2;
 constexpr uint32_t kErrNs = 1u << 3;
+constexpr uint32_t kErrCapacity = 1u << 4;
+
+// One big-node chunk (see big_node_prepare).  ctr_begin / vm_begin / pod_begin:
+// the first container / VM / pod the chunk owns; it owns them up to the next
+// chunk's begin (or the node's end for the last chunk).
+struct ChunkItem {
+  uint32_t node, chunk, nchunks, ctr_begin, vm_begin, pod_begin, pad[2];
+};
 
 struct DevState {
   uint64_t *node_energy_total, *node_active_energy, *node_active_total, *node_idle_total;
@@ -85,8 +97,12 @@ struct DevState {
   double *pod_power, *pod_cpu_delta, *pod_cpu_total;
   uint64_t proc_slots, ctr_slots, vm_slots, pod_slots;
   uint32_t *err;
-  uint32_t *gen_list;  // [nodes] nodes routed to the generic kernel this launch
-  uint32_t *gen_ctr;   // [0] list length, [1] dequeue head, [2] exits (re-armed by the last exit)
+  uint2 *defer;        // [defer_cap] (node, pod) pods left to pod_kernel
+  uint32_t *defer_ctr;  // [0] length; re-armed by interval_kernel
+  uint32_t defer_cap;
+  ChunkItem *items;    // [item_cap] big-node chunks this launch
+  uint32_t *item_ctr;  // [0] length, [1] dequeue head; cleared by pod_kernel
+  uint32_t item_cap;
 };
 
 struct NodeShared {
@@ -182,6 +198,26 @@ struct Attr {
   double nd;       // ProcessTotalCPUTimeDelta
   uint32_t first;  // first*Read variant: EnergyTotal = interval energy, Power 0
 };
+
+// Attr from the node phase's LDS results (block-uniform -> SGPRs).
+template <int Z>
+__device__ __forceinline__ Attr<Z> make_attr(const NodeShared &sh) {
+  Attr<Z> a;
+  a.nd = uniform_f64(sh.node_delta);
+  a.first = uniform_u32(sh.first);
+  a.live = 0;
+  a.live_pod = 0;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    a.aE[z] = uniform_u64(sh.active_energy[z]);
+    a.aP[z] = uniform_f64(sh.active_power[z]);
+    const double pw = uniform_f64(sh.power[z]);
+    const bool ok = a.aE[z] != 0 && a.nd != 0;
+    if (ok && a.aP[z] != 0) a.live |= 1u << z;                       // process.go:124
+    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;  // pod.go:96 / :23
+  }
+  return a;
+}
 
 // process.go:118-148 (and its container/VM/pod twins) for one row.
 template <int Z>
@@ -348,18 +384,20 @@ __device__ __forceinline__ NodeRanges node_ranges(const kacc_interval &b, const 
   return r;
 }
 
+template <int Z, int V>
+__device__ void big_node_prepare(const kacc_interval &b, const DevState &st, uint32_t n,
+                                 const NodeRanges &rg, double *red, NodeShared &sh,
+                                 uint32_t &s_base);
+
 template <int V>
 __device__ __forceinline__ bool fits_fast(const NodeRanges &r) {
   return (V & kVarUnstaged) == 0 && r.p1 - r.p0 <= static_cast<uint32_t>(kRowsLds) &&
          (r.c1 - r.c0) + (r.v1 - r.v0) + (r.q1 - r.q0) <= static_cast<uint32_t>(kTpb<V>);
 }
 
-// Generic path (big nodes / many aggregates): loops, Δ re-read from global.
 template <int Z, int V>
-__global__ __launch_bounds__(kTpb<V>, (V & kVarWide) ? ((Z <= 4) ? 8 : 4)
-                                      : (((V & kVarOcc2) || Z > 4) ? 2 : 6))
-void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restrict__ gen_list,
-                     uint32_t *__restrict__ gen_ctr) {
+__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : 6)
+void interval_kernel(const kacc_interval b, const DevState st) {
   constexpr int kThreads = kTpb<V>;
   constexpr int kRowsPerThread = kRpt<V>;
   constexpr bool kNT = (V & kVarNtStores) != 0;
@@ -371,6 +409,9 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
   __shared__ NodeShared sh;
 
   const int tid = threadIdx.x;
+  // the previous interval's pod_kernel has drained the deferred list; this
+  // interval's chunk_kernel refills it after this kernel
+  if (blockIdx.x == 0 && tid == 0) st.defer_ctr[0] = 0u;
   uint32_t n = blockIdx.x;
   if (b.node_order) n = b.node_order[blockIdx.x];
   if (n >= b.n_nodes) {
@@ -384,8 +425,9 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
     return;
   }
   const NodeRanges rg = node_ranges(b, st, n, tid);
-  if (!fits_fast<V>(rg)) {  // handled by generic_kernel (work list, dequeued)
-    if (tid == 0) gen_list[atomicAdd(gen_ctr, 1u)] = n;
+  if (!fits_fast<V>(rg)) {  // node phase here, the rest in chunk_kernel (+ pod_kernel)
+    __shared__ uint32_t s_base;
+    big_node_prepare<Z, V>(b, st, n, rg, red, sh, s_base);
     return;
   }
   const uint32_t p0 = rg.p0, p1 = rg.p1, c0 = rg.c0, c1 = rg.c1, v0 = rg.v0, v1 = rg.v1,
@@ -570,20 +612,7 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
   }
 
   // ---- E: attribution ------------------------------------------------------------
-  Attr<Z> a;
-  a.nd = uniform_f64(sh.node_delta);
-  a.first = uniform_u32(sh.first);
-  a.live = 0;
-  a.live_pod = 0;
-#pragma unroll
-  for (int z = 0; z < Z; ++z) {
-    a.aE[z] = uniform_u64(sh.active_energy[z]);
-    a.aP[z] = uniform_f64(sh.active_power[z]);
-    const double pw = uniform_f64(sh.power[z]);
-    const bool ok = a.aE[z] != 0 && a.nd != 0;
-    if (ok && a.aP[z] != 0) a.live |= 1u << z;                       // process.go:124
-    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;  // pod.go:96 / :23
-  }
+  const Attr<Z> a = make_attr<Z>(sh);
   if (tid == 0) {  // node scalars of the new snapshot
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
@@ -631,35 +660,169 @@ void interval_kernel(const kacc_interval b, const DevState st, uint32_t *__restr
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
 }
 
+// ======================= big nodes: chunked row passes ==========================
+// A node that does not fit one fast workgroup (> kRowsLds rows or > kTpb
+// aggregates, e.g. BASELINE config 5's 10-50k-process nodes) is cut into
+// kChunkRows-row chunks so that no single node bounds the launch:
+//   interval_kernel  node zones, the canonical node CPU total and the node
+//                    scalars (big_node_prepare), then one ChunkItem per chunk
+//                    naming the first container / VM / pod the chunk owns.  A
+//                    container or VM belongs to the chunk holding its first
+//                    row, a pod to the chunk owning its first container;
+//   chunk_kernel     per chunk, the fast path's phases C-E on the chunk: the
+//                    process rows, the owned containers / VMs (sequential sums;
+//                    rows past the chunk come from global memory) and the owned
+//                    pods whose containers all lie in the chunk (LDS sums).  A
+//                    pod reaching past its chunk goes on the deferred list;
+//   pod_kernel       the deferred pods, one lane each, from the container
+//                    sums chunk_kernel stored (the kernel boundary makes them
+//                    visible across XCDs: no cross-workgroup wait anywhere).
+// Every sum keeps its sequential / canonical-tree order, so results are
+// bit-identical to one workgroup handling the whole node.
 template <int Z, int V>
-__device__ void generic_node(const kacc_interval &b, const DevState &st, const uint32_t n,
-                             const uint32_t p0, const uint32_t p1, const uint32_t c0,
-                             const uint32_t c1, const uint32_t v0, const uint32_t v1,
-                             const uint32_t q0, const uint32_t q1, double *red, NodeShared &sh) {
-  constexpr bool kNT = (V & kVarNtStores) != 0;
-  constexpr int kThreads = kGenThreads;
+__device__ void big_node_prepare(const kacc_interval &b, const DevState &st, const uint32_t n,
+                                 const NodeRanges &rg, double *red, NodeShared &sh,
+                                 uint32_t &s_base) {
+  constexpr int kThreads = kTpb<V>;
+  constexpr uint32_t kGen = kThreads - kTree;  // lanes generating chunk items
+  constexpr int kScan = 4;                     // segments per generating lane per step
   const int tid = threadIdx.x;
-  const uint32_t rows = p1 - p0;
-  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
-
-  // ---- B: ProcessTotalCPUTimeDelta, lanes < 256 stream the rows from HBM ----
+  const uint32_t p0 = rg.p0, p1 = rg.p1, rows = p1 - p0;
+  const uint32_t nch = rows ? (rows + kChunkRows - 1) / kChunkRows : 1u;
+  if (tid == 0) s_base = (V & kVarBigNoAtomic) ? n + p0 / kChunkRows : atomicAdd(st.item_ctr, nch);
+  if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
+  __syncthreads();
+  const uint32_t base = s_base;
+  const bool fits = base + nch <= st.item_cap && base + nch >= base;  // host sizes the list
+  if (!fits && tid == 0) raise_err(st.err, kErrCapacity);
+  const bool given = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) != 0;
   if (tid < kTree) {
-    double s = 0.0;
-    for (uint32_t base = 0; base < rows; base += kRowsLds) {
-      double v[kLoadsPerLane];
+    // ---- B: ProcessTotalCPUTimeDelta; lane l sums rows l, l+256, ... ---------
+    // software-pipelined: the next kTotLoads rows are in flight while the
+    // current ones are added (latency, not bandwidth, bounds one node's sum)
+    if (!given && (V & kVarBigNoTotal) == 0) {
+      const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
+      double s = 0.0;
+      double v[kTotLoads];
 #pragma unroll
-      for (int k = 0; k < kLoadsPerLane; ++k) {
-        const uint32_t i = base + tid + k * kTree;
+      for (int k = 0; k < kTotLoads; ++k) {
+        const uint32_t i = tid + k * kTree;
         v[k] = i < rows ? dcpu[i] : 0.0;
       }
+      for (uint32_t r0 = 0; r0 < rows; r0 += kTree * kTotLoads) {
+        double nx[kTotLoads];
 #pragma unroll
-      for (int k = 0; k < kLoadsPerLane; ++k)
-        if (base + tid + k * kTree < rows) s = s + v[k];
+        for (int k = 0; k < kTotLoads; ++k) {
+          const uint32_t i = r0 + kTree * kTotLoads + tid + k * kTree;
+          nx[k] = i < rows ? dcpu[i] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kTotLoads; ++k)
+          if (r0 + tid + k * kTree < rows) s = s + v[k];
+#pragma unroll
+        for (int k = 0; k < kTotLoads; ++k) v[k] = nx[k];
+      }
+      red[tid] = s;
     }
-    red[tid] = s;
+  } else if (fits) {
+    // ---- chunk items, concurrently with the sum (the other kGen lanes) --------
+    // A segment belongs to the chunk holding its first row (rows are
+    // [containers][VMs][rest]); a pod to the chunk owning its first container.
+    // Segment i is the first one owned by chunks (key(i-1), key(i)].
+    const uint32_t g = static_cast<uint32_t>(tid) - kTree;
+    ChunkItem *__restrict__ items = st.items + base;
+    const uint32_t c0 = rg.c0, c1 = rg.c1, v0 = rg.v0, v1 = rg.v1, q0 = rg.q0, q1 = rg.q1;
+    auto clampr = [&](uint32_t x) { return min(max(x, p0), p1); };
+    auto clampc = [&](uint32_t x) { return min(max(x, c0), c1); };
+    auto chunk_of = [&](uint32_t start) -> int {
+      return static_cast<int>(min((start - p0) / kChunkRows, nch - 1));
+    };
+    // first row of container c given ctr_proc_end[c - 1] (p0 for c0)
+    const uint32_t ctr_rows_end = c1 > c0 ? clampr(b.ctr_proc_end[c1 - 1]) : p0;
+    // segment i (owner chunk kc, its predecessor's kp) begins chunks kp+1..kc
+    auto mark = [&](uint32_t i, int kc, int kp, uint32_t ChunkItem::*field) {
+      if (kc < kp) raise_err(st.err, kErrOffsets);
+      for (int k = kp + 1; k <= kc; ++k) items[k].*field = i;
+    };
+    // containers: start(c) = c == c0 ? p0 : end[c-1]
+    for (uint32_t cb = c0 + g; cb < ((V & kVarBigNoScan) ? c0 : c1); cb += kGen * kScan) {
+      uint32_t e1[kScan], e2[kScan];
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t c = cb + u * kGen;
+        e1[u] = (c < c1 && c > c0) ? b.ctr_proc_end[c - 1] : p0;
+        e2[u] = (c < c1 && c > c0 + 1) ? b.ctr_proc_end[c - 2] : p0;
+      }
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t c = cb + u * kGen;
+        if (c >= c1) continue;
+        mark(c, chunk_of(clampr(e1[u])), c > c0 ? chunk_of(clampr(e2[u])) : -1,
+             &ChunkItem::ctr_begin);
+      }
+    }
+    // VMs: start(v) = v == v0 ? ctr_rows_end : vm_end[v-1]
+    for (uint32_t vb = v0 + g; vb < ((V & kVarBigNoScan) ? v0 : v1); vb += kGen * kScan) {
+      uint32_t e1[kScan], e2[kScan];
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t v = vb + u * kGen;
+        e1[u] = (v < v1 && v > v0) ? b.vm_proc_end[v - 1] : ctr_rows_end;
+        e2[u] = (v < v1 && v > v0 + 1) ? b.vm_proc_end[v - 2] : ctr_rows_end;
+      }
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t v = vb + u * kGen;
+        if (v >= v1) continue;
+        mark(v, chunk_of(clampr(e1[u])), v > v0 ? chunk_of(clampr(e2[u])) : -1,
+             &ChunkItem::vm_begin);
+      }
+    }
+    // pods: first container f(q) = q == q0 ? c0 : pod_end[q-1]; key = key of
+    // container f(q), or the last chunk when the pod starts past the containers
+    if constexpr ((V & (kVarSkipAggregates | kVarBigNoScan)) == 0) {
+      for (uint32_t qb = q0 + g; qb < q1; qb += kGen * kScan) {
+        uint32_t f1[kScan], f2[kScan], s1[kScan], s2[kScan];
+#pragma unroll
+        for (int u = 0; u < kScan; ++u) {
+          const uint32_t q = qb + u * kGen;
+          f1[u] = (q < q1 && q > q0) ? clampc(b.pod_ctr_end[q - 1]) : c0;
+          f2[u] = (q < q1 && q > q0 + 1) ? clampc(b.pod_ctr_end[q - 2]) : c0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScan; ++u) {
+          s1[u] = (f1[u] > c0 && f1[u] < c1) ? b.ctr_proc_end[f1[u] - 1] : p0;
+          s2[u] = (f2[u] > c0 && f2[u] < c1) ? b.ctr_proc_end[f2[u] - 1] : p0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScan; ++u) {
+          const uint32_t q = qb + u * kGen;
+          if (q >= q1) continue;
+          const int kc = f1[u] < c1 ? chunk_of(clampr(s1[u])) : static_cast<int>(nch - 1);
+          const int kp = q == q0 ? -1 : f2[u] < c1 ? chunk_of(clampr(s2[u])) : static_cast<int>(nch - 1);
+          mark(q, kc, kp, &ChunkItem::pod_begin);
+        }
+      }
+    }
+    // chunks after the last segment's owner own none of that kind
+    const int kl_ctr = c1 > c0 ? chunk_of(c1 - 1 > c0 ? clampr(b.ctr_proc_end[c1 - 2]) : p0) : -1;
+    const int kl_vm = v1 > v0 ? chunk_of(v1 - 1 > v0 ? clampr(b.vm_proc_end[v1 - 2]) : ctr_rows_end) : -1;
+    int kl_pod = -1;
+    if (q1 > q0) {
+      const uint32_t f = q1 - 1 > q0 ? clampc(b.pod_ctr_end[q1 - 2]) : c0;
+      kl_pod = f < c1 ? chunk_of(f > c0 ? clampr(b.ctr_proc_end[f - 1]) : p0) : static_cast<int>(nch - 1);
+    }
+    for (uint32_t k = g; k < nch; k += kGen) {
+      items[k].node = n;
+      items[k].chunk = k;
+      items[k].nchunks = nch;
+      if (static_cast<int>(k) > kl_ctr) items[k].ctr_begin = c1;
+      if (static_cast<int>(k) > kl_vm) items[k].vm_begin = v1;
+      if (static_cast<int>(k) > kl_pod) items[k].pod_begin = q1;
+    }
   }
   __syncthreads();
-  if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
+  if (given) {
     if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
   } else {
     if (tid < 128) red[tid] = red[tid] + red[tid + 128];
@@ -671,138 +834,100 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
       if (tid == 0) sh.node_delta = x;
     }
   }
-
-  if constexpr ((V & kVarSkipAggregates) == 0) {
-    // ---- C: containers and VMs ----------------------------------------------
-    const uint32_t ctr_rows_end = c1 > c0 ? b.ctr_proc_end[c1 - 1] : p0;
-    for (uint32_t c = c0 + tid; c < c1; c += kThreads) {
-      uint32_t beg = c == c0 ? p0 : b.ctr_proc_end[c - 1];
-      uint32_t end = b.ctr_proc_end[c];
-      const uint32_t w = b.ctr_slot[c];
-      const uint64_t sl = w & KACC_SLOT_MASK;
-      if (beg < p0 || end < beg || end > p1 || sl >= st.ctr_slots) {
-        raise_err(st.err, sl >= st.ctr_slots ? kErrSlot : kErrOffsets);
-        if (sl >= st.ctr_slots) continue;
-        beg = max(min(beg, p1), p0);
-        end = max(min(end, p1), beg);
-      }
-      double delta = 0.0;
-      double total = (w & KACC_SLOT_NEW) ? 0.0 : st.ctr_cpu_total[sl];
-      // rows loaded kSegLoads at a time (independent), added in listing order
-      for (uint32_t i0 = beg - p0; i0 < end - p0; i0 += kSegLoads) {
-        double v[kSegLoads];
-#pragma unroll
-        for (int u = 0; u < kSegLoads; ++u) v[u] = i0 + u < end - p0 ? dcpu[i0 + u] : 0.0;
-#pragma unroll
-        for (int u = 0; u < kSegLoads; ++u)
-          if (i0 + u < end - p0) {
-            delta = delta + v[u];
-            total = total + v[u];
-          }
-      }
-      st.ctr_cpu_delta[sl] = delta;
-      st.ctr_cpu_total[sl] = total;
-    }
-    for (uint32_t v = v0 + tid; v < v1; v += kThreads) {
-      uint32_t beg = v == v0 ? ctr_rows_end : b.vm_proc_end[v - 1];
-      uint32_t end = b.vm_proc_end[v];
-      const uint64_t sl = b.vm_slot[v] & KACC_SLOT_MASK;
-      if (beg < p0 || end < beg || end > p1 || sl >= st.vm_slots) {
-        raise_err(st.err, sl >= st.vm_slots ? kErrSlot : kErrOffsets);
-        if (sl >= st.vm_slots) continue;
-        beg = max(min(beg, p1), p0);
-        end = max(min(end, p1), beg);
-      }
-      st.vm_cpu_delta[sl] = end > beg ? dcpu[end - 1 - p0] : 0.0;
-    }
-  }
   __syncthreads();
-  if constexpr ((V & kVarSkipAggregates) == 0) {
-    // ---- D: pods --------------------------------------------------------------
-    for (uint32_t q = q0 + tid; q < q1; q += kThreads) {
-      uint32_t beg = q == q0 ? c0 : b.pod_ctr_end[q - 1];
-      uint32_t end = b.pod_ctr_end[q];
-      const uint32_t w = b.pod_slot[q];
-      const uint64_t sl = w & KACC_SLOT_MASK;
-      if (beg < c0 || end < beg || end > c1 || sl >= st.pod_slots) {
-        raise_err(st.err, sl >= st.pod_slots ? kErrSlot : kErrOffsets);
-        if (sl >= st.pod_slots) continue;
-        beg = max(min(beg, c1), c0);
-        end = max(min(end, c1), beg);
-      }
-      double delta = 0.0;
-      double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
-      for (uint32_t c0_ = beg; c0_ < end; c0_ += kSegLoads / 2) {
-        constexpr int kU = kSegLoads / 2;
-        uint64_t cs[kU];
-        double cd[kU], ct[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-          cs[u] = c0_ + u < end ? (b.ctr_slot[c0_ + u] & KACC_SLOT_MASK) : ~0ull;
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const bool ok = cs[u] < st.ctr_slots;
-          cd[u] = ok ? st.ctr_cpu_delta[cs[u]] : 0.0;
-          ct[u] = ok ? st.ctr_cpu_total[cs[u]] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-          if (cs[u] < st.ctr_slots) {
-            delta = delta + cd[u];
-            total = total + ct[u];
-          }
-      }
-      st.pod_cpu_delta[sl] = delta;
-      st.pod_cpu_total[sl] = total;
-    }
-  }
-  __syncthreads();
-
-  // ---- E: attribution ------------------------------------------------------------
-  Attr<Z> a;
-  a.nd = uniform_f64(sh.node_delta);
-  a.first = uniform_u32(sh.first);
-  a.live = 0;
-  a.live_pod = 0;
-#pragma unroll
-  for (int z = 0; z < Z; ++z) {
-    a.aE[z] = uniform_u64(sh.active_energy[z]);
-    a.aP[z] = uniform_f64(sh.active_power[z]);
-    const double pw = uniform_f64(sh.power[z]);
-    const bool ok = a.aE[z] != 0 && a.nd != 0;
-    if (ok && a.aP[z] != 0) a.live |= 1u << z;
-    if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;
-  }
-  if (tid == 0) {
+  if (tid == 0) {  // node scalars of the new snapshot (as the fast path)
+    const bool first = sh.first != 0;
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
-    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];
-    st.node_cpu_delta[n] = a.nd;
-    st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+    st.node_usage_ratio[n] = first ? 0.0 : b.node_usage_ratio[n];
+    st.node_cpu_delta[n] = sh.node_delta;
+    st.node_status[n] = first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
-  if constexpr ((V & kVarSkipProcs) == 0) {
-    const uint32_t *__restrict__ pslot = b.proc_slot + p0;
-    // wave-uniform trip count: every lane stays active for the group votes
-    // (__all) below; rows past the node's end are masked per lane
-    for (uint32_t it = 0; it * static_cast<uint32_t>(kThreads * kUnroll) < rows; ++it) {
-      const uint32_t base = tid + it * kThreads * kUnroll;
-      double d[kUnroll];
-      uint32_t w[kUnroll];
-      uint64_t prev[kUnroll][Z];
+}
+
+// Node-uniform attribution parameters written by the node phase, back into LDS.
+template <int Z>
+__device__ __forceinline__ void node_params_to_lds(const DevState &st, uint32_t n, int tid,
+                                                   NodeShared &sh) {
+  if (tid < Z) {
+    const uint64_t i = static_cast<uint64_t>(n) * Z + tid;
+    sh.active_energy[tid] = st.node_active_energy[i];
+    sh.active_power[tid] = st.node_active_power[i];
+    sh.power[tid] = st.node_power[i];
+  }
+  if (tid == 0) {
+    sh.node_delta = st.node_cpu_delta[n];
+    sh.first = st.node_status[n] == KACC_NODE_FIRST_READ ? 1u : 0u;
+  }
+}
+
+template <int Z, int V>
+__global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(const kacc_interval b,
+                                                                           const DevState st) {
+  constexpr int kThreads = kChunkThreads;
+  constexpr int kR = kChunkRpt;
+  constexpr bool kNT = (V & kVarNtStores) != 0;
+  constexpr bool kT = kTransposed<Z> && (V & kVarNoTranspose) == 0;
+  constexpr bool kAgg = (V & kVarSkipAggregates) == 0;
+  __shared__ double s_d[kChunkRows];
+  __shared__ uint32_t s_w[kChunkRows];
+  __shared__ double s_cd[kThreads];  // owned containers' Δ (first kThreads of them)
+  __shared__ double s_ct[kThreads];  // and running CPU totals
+  __shared__ NodeShared sh;
+  __shared__ uint32_t s_next[2];
+  const int tid = threadIdx.x;
+  const uint32_t utid = static_cast<uint32_t>(tid);
+  const uint32_t count =
+      min(__hip_atomic_load(st.item_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), st.item_cap);
+  uint32_t idx = blockIdx.x;  // first item static, the rest dequeued
+  for (uint32_t parity = 0; idx < count; parity ^= 1u) {
+    if (tid == 0) s_next[parity] = atomicAdd(st.item_ctr + 1, 1u) + gridDim.x;
+    const ChunkItem *it = st.items + idx;
+    const uint32_t n = uniform_u32(it->node);
+    const uint32_t k = uniform_u32(it->chunk);
+    const uint32_t nch = uniform_u32(it->nchunks);
+    if (n >= b.n_nodes) {  // corrupt item: cannot happen unless the list overflowed
+      if (tid == 0) raise_err(st.err, kErrCapacity);
+      __syncthreads();
+      idx = uniform_u32(s_next[parity]);
+      continue;
+    }
+    const NodeRanges rg = node_ranges(b, st, n, tid);
+    const bool last = k + 1 >= nch;
+    const uint32_t lo = min(rg.p0 + min(k, nch) * static_cast<uint32_t>(kChunkRows), rg.p1);
+    const uint32_t hi = last ? rg.p1 : min(lo + static_cast<uint32_t>(kChunkRows), rg.p1);
+    const uint32_t rows = hi - lo;
+    const uint32_t cb = min(max(uniform_u32(it->ctr_begin), rg.c0), rg.c1);
+    const uint32_t ce = max(min(last ? rg.c1 : uniform_u32(it[1].ctr_begin), rg.c1), cb);
+    const uint32_t vb = min(max(uniform_u32(it->vm_begin), rg.v0), rg.v1);
+    const uint32_t ve = max(min(last ? rg.v1 : uniform_u32(it[1].vm_begin), rg.v1), vb);
+    const uint32_t qb = min(max(uniform_u32(it->pod_begin), rg.q0), rg.q1);
+    const uint32_t qe = max(min(last ? rg.q1 : uniform_u32(it[1].pod_begin), rg.q1), qb);
+    const uint32_t nca = kAgg ? ce - cb : 0u;
+    const uint32_t ncv = kAgg ? nca + (ve - vb) : 0u;  // containers + VMs
+    const uint32_t nagg = kAgg ? ncv + (qe - qb) : 0u;  // + pods
+
+    // ---- loads: rows, their previous totals, one owned aggregate per lane -----
+    const double *__restrict__ dcpu = b.proc_cpu_delta + lo;
+    const uint32_t *__restrict__ pslot = b.proc_slot + lo;
+    double d[kR];
+    uint32_t w[kR];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t r = base + u * kThreads;
-        const bool in = r < rows;
-        w[u] = in ? pslot[r] : 0xffffffffu;
-        d[u] = in ? dcpu[r] : 0.0;
-      }
-      uint32_t contig = 0;  // bit u: 64-row group u of this wave is transposed
+    for (int u = 0; u < kR; ++u) {
+      const uint32_t r = utid + u * kThreads;
+      const bool in = r < rows;
+      d[u] = in ? dcpu[r] : 0.0;
+      w[u] = in ? pslot[r] : 0xffffffffu;
+    }
+    uint64_t prev[kR][Z];
+    uint32_t contig = 0;
+    if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < kR; ++u) {
         const uint64_t sl = w[u] & KACC_SLOT_MASK;
-        if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+        if constexpr (kT) {
           const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
-          const bool mine = (base + u * kThreads) < rows && sl == s0 + (tid & 63) &&
+          const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
                             s0 + 64 <= st.proc_slots;
           if (__all(mine)) {
             contig |= 1u << u;
@@ -817,86 +942,263 @@ __device__ void generic_node(const kacc_interval &b, const DevState &st, const u
           for (int z = 0; z < Z; ++z) prev[u][z] = 0;
         }
       }
+    }
+    // aggregate j of this chunk: containers [cb, ce), VMs [vb, ve), pods [qb, qe)
+    const uint32_t ctr_rows_end = rg.c1 > rg.c0 ? b.ctr_proc_end[rg.c1 - 1] : rg.p0;
+    auto agg = [&](uint32_t j, uint32_t &beg, uint32_t &end, uint32_t &wd) -> uint32_t {
+      if (j < nca) {
+        const uint32_t c = cb + j;
+        beg = c == rg.c0 ? rg.p0 : b.ctr_proc_end[c - 1];
+        end = b.ctr_proc_end[c];
+        wd = b.ctr_slot[c];
+        return 1u;
+      }
+      if (j < ncv) {
+        const uint32_t v = vb + (j - nca);
+        beg = v == rg.v0 ? ctr_rows_end : b.vm_proc_end[v - 1];
+        end = b.vm_proc_end[v];
+        wd = b.vm_slot[v];
+        return 2u;
+      }
+      const uint32_t q = qb + (j - ncv);
+      beg = q == rg.q0 ? rg.c0 : b.pod_ctr_end[q - 1];
+      end = b.pod_ctr_end[q];
+      wd = b.pod_slot[q];
+      return 3u;
+    };
+    auto cap_of = [&](uint32_t role) {
+      return role == 1 ? st.ctr_slots : role == 2 ? st.vm_slots : st.pod_slots;
+    };
+    auto energy_of = [&](uint32_t role) {
+      return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy;
+    };
+    auto power_of = [&](uint32_t role) {
+      return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
+    };
+    uint32_t a_role = 0, a_beg = 0, a_end = 0, a_w = 0xffffffffu;
+    if (utid < nagg) a_role = agg(utid, a_beg, a_end, a_w);
+    const uint32_t a_s = a_w & KACC_SLOT_MASK;
+    const bool a_ok = a_role != 0 && a_s < cap_of(a_role);
+    uint64_t a_prev[Z];
+    double a_total = 0.0;
+    if (a_ok) {
+      load_row<Z>(energy_of(a_role), a_s, a_prev);
+      if (a_role != 2 && !(a_w & KACC_SLOT_NEW))
+        a_total = (a_role == 1 ? st.ctr_cpu_total : st.pod_cpu_total)[a_s];
+    } else {
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const uint32_t r = base + u * kThreads;
-        if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+      for (int z = 0; z < Z; ++z) a_prev[z] = 0;
+    }
+    if (a_role != 0 && !a_ok) raise_err(st.err, kErrSlot);
+    node_params_to_lds<Z>(st, n, tid, sh);
+#pragma unroll
+    for (int u = 0; u < kR; ++u) {
+      const uint32_t r = utid + u * kThreads;
+      if (r < rows) {
+        s_d[r] = d[u];
+        s_w[r] = w[u];
+      }
+    }
+    __syncthreads();
+    const Attr<Z> a = make_attr<Z>(sh);
+
+    auto agg_out = [&](uint32_t role, uint32_t wd, double delta, const uint64_t (&pv)[Z]) {
+      const uint64_t s = wd & KACC_SLOT_MASK;
+      uint64_t E[Z];
+      double P[Z];
+      attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, delta, (wd & KACC_SLOT_NEW) != 0, pv, E, P);
+      store_row<Z, kNT, uint64_t>(energy_of(role), s, E);
+      store_row<Z, kNT, double>(power_of(role), s, P);
+    };
+    // ---- C: owned containers / VMs (informer.go:223-273) ------------------------
+    auto segment = [&](uint32_t role, uint32_t beg, uint32_t end, uint32_t wd, bool ok,
+                       double &total) -> double {
+      if (beg < rg.p0 || end < beg || end > rg.p1) {
+        raise_err(st.err, kErrOffsets);
+        beg = max(min(beg, rg.p1), rg.p0);
+        end = max(min(end, rg.p1), beg);
+      }
+      auto delta_at = [&](uint32_t i) -> double {
+        return (i >= lo && i < hi) ? s_d[i - lo] : b.proc_cpu_delta[i];
+      };
+      double delta = 0.0;
+      if (role == 1) {
+        for (uint32_t i = beg; i < end; ++i) {
+          const double di = delta_at(i);
+          delta = delta + di;
+          total = total + di;
+        }
+      } else {
+        delta = end > beg ? delta_at(end - 1) : 0.0;  // informer.go:445, last one wins
+      }
+      if (ok) {
+        const uint64_t s = wd & KACC_SLOT_MASK;
+        if (role == 1) {
+          st.ctr_cpu_delta[s] = delta;
+          st.ctr_cpu_total[s] = total;
+        } else {
+          st.vm_cpu_delta[s] = delta;
+        }
+      }
+      return delta;
+    };
+    double a_delta = 0.0;
+    if (a_role == 1 || a_role == 2) {
+      a_delta = segment(a_role, a_beg, a_end, a_w, a_ok, a_total);
+      if (a_role == 1) {
+        s_cd[utid] = a_ok ? a_delta : 0.0;
+        s_ct[utid] = a_ok ? a_total : 0.0;
+      }
+    }
+    __syncthreads();
+    // ---- D: owned pods whose containers are all in s_cd / s_ct ---------------
+    bool defer = false;
+    if (a_role == 3) {
+      uint32_t beg = a_beg, end = a_end;
+      if (beg < rg.c0 || end < beg || end > rg.c1) {
+        raise_err(st.err, kErrOffsets);
+        beg = max(min(beg, rg.c1), rg.c0);
+        end = max(min(end, rg.c1), beg);
+      }
+      if (end <= ce && end - cb <= static_cast<uint32_t>(kThreads) && beg >= cb) {
+        for (uint32_t c = beg - cb; c < end - cb; ++c) {
+          a_delta = a_delta + s_cd[c];
+          a_total = a_total + s_ct[c];  // quirk: the container's running total
+        }
+        if (a_ok) {
+          st.pod_cpu_delta[a_s] = a_delta;
+          st.pod_cpu_total[a_s] = a_total;
+        }
+      } else {
+        defer = true;  // pod_kernel, after every chunk's containers are stored
+      }
+    }
+    // ---- E: aggregates, then process rows (process.go:118-148) ------------------
+    if (a_ok && !defer) agg_out(a_role, a_w, a_delta, a_prev);
+    if (defer && a_ok) {
+      const uint32_t i = atomicAdd(st.defer_ctr, 1u);
+      if (i < st.defer_cap)
+        st.defer[i] = make_uint2(n, qb + (utid - ncv));
+      else
+        raise_err(st.err, kErrCapacity);
+    }
+    if constexpr ((V & kVarSkipProcs) == 0) {
+#pragma unroll
+      for (int u = 0; u < kR; ++u) {
+        const uint32_t r = utid + u * kThreads;
+        if constexpr (kT) {
           if (contig & (1u << u)) {
             const uint32_t g = r - (tid & 63);
-            attribute_group<Z, kNT>(a, sh, dcpu + g, pslot + g, uniform_u32(w[u] & KACC_SLOT_MASK),
+            attribute_group<Z, kNT>(a, sh, s_d + g, s_w + g, uniform_u32(s_w[g] & KACC_SLOT_MASK),
                                     prev[u], st.proc_energy, st.proc_power);
             continue;
           }
         }
         if (r >= rows) continue;
-        const uint64_t sl = w[u] & KACC_SLOT_MASK;
+        const uint32_t wk = s_w[r];
+        const uint64_t sl = wk & KACC_SLOT_MASK;
         if (sl >= st.proc_slots) {
           raise_err(st.err, kErrSlot);
           continue;
         }
         uint64_t E[Z];
         double P[Z];
-        attribute_row<Z>(a, a.live, d[u], (w[u] & KACC_SLOT_NEW) != 0, prev[u], E, P);
+        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E, P);
         store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
         store_row<Z, kNT, double>(st.proc_power, sl, P);
       }
     }
-  }
-  if constexpr ((V & kVarSkipAggregates) == 0) {
-    for (uint32_t c = c0 + tid; c < c1; c += kThreads) {
-      const uint32_t w = b.ctr_slot[c];
-      if ((w & KACC_SLOT_MASK) >= st.ctr_slots) continue;
-      attribute_slot<Z, kNT>(a, a.live, st.ctr_cpu_delta[w & KACC_SLOT_MASK], w, st.ctr_energy,
-                             st.ctr_power);
+    // aggregates beyond one per lane (chunks of mostly empty containers):
+    // containers / VMs here, their pods always deferred
+    for (uint32_t j = kThreads + utid; j < nagg; j += kThreads) {
+      uint32_t beg, end, wd;
+      const uint32_t role = agg(j, beg, end, wd);
+      const uint64_t s = wd & KACC_SLOT_MASK;
+      const bool ok = s < cap_of(role);
+      if (!ok) {
+        raise_err(st.err, kErrSlot);
+        continue;
+      }
+      if (role == 3) {
+        const uint32_t i = atomicAdd(st.defer_ctr, 1u);
+        if (i < st.defer_cap)
+          st.defer[i] = make_uint2(n, qb + (j - ncv));
+        else
+          raise_err(st.err, kErrCapacity);
+        continue;
+      }
+      uint64_t pv[Z];
+      load_row<Z>(energy_of(role), s, pv);
+      double total = (role == 1 && !(wd & KACC_SLOT_NEW)) ? st.ctr_cpu_total[s] : 0.0;
+      const double delta = segment(role, beg, end, wd, true, total);
+      agg_out(role, wd, delta, pv);
     }
-    for (uint32_t v = v0 + tid; v < v1; v += kThreads) {
-      const uint32_t w = b.vm_slot[v];
-      if ((w & KACC_SLOT_MASK) >= st.vm_slots) continue;
-      attribute_slot<Z, kNT>(a, a.live, st.vm_cpu_delta[w & KACC_SLOT_MASK], w, st.vm_energy,
-                             st.vm_power);
-    }
-    for (uint32_t q = q0 + tid; q < q1; q += kThreads) {
-      const uint32_t w = b.pod_slot[q];
-      if ((w & KACC_SLOT_MASK) >= st.pod_slots) continue;
-      attribute_slot<Z, kNT>(a, a.live_pod, st.pod_cpu_delta[w & KACC_SLOT_MASK], w,
-                             st.pod_energy, st.pod_power);
-    }
+    __syncthreads();  // LDS reused by the next item; s_next[parity] written
+    idx = uniform_u32(s_next[parity]);
   }
 }
 
-// Nodes that do not fit a fast workgroup (> 2048 rows or > kTpb aggregates,
-// e.g. BASELINE config 5's 10–50k-process nodes), dequeued one at a time
-// (one returning atomicAdd per node; load-balanced for skewed fleets).
+// Deferred pods (informer.go:275-326 + pod.go:46-131), one lane each: ΔCPU and
+// the running-total quirk summed over the pod's containers in batch order from
+// the tables chunk_kernel wrote, then attribution (pod.go:96 guards on Power).
+// Also re-arms the chunk list for the next interval (chunk_kernel has ended);
+// the deferred list itself is re-armed by the next interval_kernel.
 template <int Z, int V>
-__global__ __launch_bounds__(kGenThreads, (Z <= 5 ? 4 : 2)) void generic_kernel(const kacc_interval b,
-                                                              const DevState st,
-                                                              const uint32_t *__restrict__ gen_list,
-                                                              uint32_t *__restrict__ gen_ctr) {
-  __shared__ double red[kTree];
-  __shared__ NodeShared sh;
-  __shared__ uint32_t s_idx;
+__global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, const DevState st) {
+  constexpr bool kNT = (V & kVarNtStores) != 0;
   const int tid = threadIdx.x;
-  const uint32_t count = __hip_atomic_load(gen_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (;;) {
-    if (tid == 0) s_idx = count ? atomicAdd(gen_ctr + 1, 1u) : count;
-    __syncthreads();
-    const uint32_t idx = s_idx;
-    __syncthreads();
-    if (idx >= count) break;
-    const uint32_t n = gen_list[idx];
-    const NodeRanges rg = node_ranges(b, st, n, tid);
-    if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
-    generic_node<Z, V>(b, st, n, rg.p0, rg.p1, rg.c0, rg.c1, rg.v0, rg.v1, rg.q0, rg.q1, red, sh);
-    __syncthreads();  // LDS (red, sh) reused by the next node
+  if (blockIdx.x == 0 && tid == 0) {
+    st.item_ctr[0] = 0u;
+    st.item_ctr[1] = 0u;
   }
-  // The last workgroup to leave re-arms the list for the next launch (no
-  // per-launch memset): [0] length, [1] dequeue head, [2] exit count.
-  if (tid == 0) {
-    if (atomicAdd(gen_ctr + 2, 1u) == gridDim.x - 1) {
-      __hip_atomic_store(gen_ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gen_ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(gen_ctr + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t count = min(st.defer_ctr[0], st.defer_cap);
+  for (uint32_t i = blockIdx.x * kBlock + tid; i < count; i += gridDim.x * kBlock) {
+    const uint2 e = st.defer[i];
+    const uint32_t n = e.x, q = e.y;
+    if (n >= b.n_nodes || q >= b.n_pods) {
+      raise_err(st.err, kErrCapacity);
+      continue;
     }
+    const NodeRanges rg = node_ranges(b, st, n, 1);
+    uint32_t beg = q == rg.q0 ? rg.c0 : b.pod_ctr_end[q - 1];
+    uint32_t end = b.pod_ctr_end[q];
+    beg = max(min(beg, rg.c1), rg.c0);  // offsets were checked by chunk_kernel
+    end = max(min(end, rg.c1), beg);
+    const uint32_t w = b.pod_slot[q];
+    const uint64_t sl = w & KACC_SLOT_MASK;  // < pod_slots (checked before deferral)
+    uint64_t prev[Z];
+    load_row<Z>(st.pod_energy, sl, prev);
+    double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
+    double delta = 0.0;
+    for (uint32_t c = beg; c < end; ++c) {
+      const uint64_t cs = b.ctr_slot[c] & KACC_SLOT_MASK;
+      if (cs >= st.ctr_slots) continue;  // contributes 0, as s_cd / s_ct
+      delta = delta + st.ctr_cpu_delta[cs];
+      total = total + st.ctr_cpu_total[cs];
+    }
+    st.pod_cpu_delta[sl] = delta;
+    st.pod_cpu_total[sl] = total;
+    // this lane's node parameters (per lane: deferred pods of many nodes)
+    Attr<Z> a;
+    a.nd = st.node_cpu_delta[n];
+    a.first = st.node_status[n] == KACC_NODE_FIRST_READ ? 1u : 0u;
+    a.live = 0;
+    a.live_pod = 0;
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      const uint64_t iz = static_cast<uint64_t>(n) * Z + z;
+      a.aE[z] = st.node_active_energy[iz];
+      a.aP[z] = st.node_active_power[iz];
+      const double pw = st.node_power[iz];
+      const bool ok = a.aE[z] != 0 && a.nd != 0;
+      if (ok && a.aP[z] != 0) a.live |= 1u << z;
+      if (ok && (a.first ? a.aP[z] : pw) != 0) a.live_pod |= 1u << z;
+    }
+    uint64_t E[Z];
+    double P[Z];
+    attribute_row<Z>(a, a.live_pod, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
+    store_row<Z, kNT, uint64_t>(st.pod_energy, sl, E);
+    store_row<Z, kNT, double>(st.pod_power, sl, P);
   }
 }
 
@@ -1001,8 +1303,11 @@ struct kacc_ctx {
   void *tables[KACC_T_COUNT] = {};
   uint64_t counts[KACC_T_COUNT] = {};
   uint32_t *d_err = nullptr;
-  uint32_t *d_gen_list = nullptr;
-  uint32_t *d_gen_ctr = nullptr;
+  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
+  kacc::ChunkItem *d_items = nullptr;
+  uint32_t item_cap = 0;
+  uint2 *d_defer = nullptr;
+  uint32_t defer_cap = 0;
   std::string err;
 };
 
@@ -1082,21 +1387,26 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.vm_slots = ctx->cfg.vm_slots;
   s.pod_slots = ctx->cfg.pod_slots;
   s.err = ctx->d_err;
-  s.gen_list = ctx->d_gen_list;
-  s.gen_ctr = ctx->d_gen_ctr;
+  s.items = ctx->d_items;
+  s.item_ctr = ctx->d_ctr;
+  s.item_cap = ctx->item_cap;
+  s.defer = ctx->d_defer;
+  s.defer_ctr = ctx->d_ctr + 2;
+  s.defer_cap = ctx->defer_cap;
   return s;
 }
 
-// One interval = reset the big-node work list, the fast kernel (one workgroup
-// per node; oversized nodes are appended to the list) and the generic kernel
-// that drains the list.
+// One interval = the fast kernel (one workgroup per node; oversized nodes get
+// their node phase there and are cut into chunk items), the chunk kernel and
+// the deferred-pod kernel (both exit at once when no node was oversized).
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
-                     s, s.gen_list, s.gen_ctr);
-  const uint32_t gen_grid = std::min<uint32_t>(b.n_nodes, 512u);
-  hipLaunchKernelGGL((kacc::generic_kernel<Z, V>), dim3(gen_grid), dim3(kacc::kGenThreads), 0, st,
-                     b, s, s.gen_list, s.gen_ctr);
+                     s);
+  const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
+  hipLaunchKernelGGL((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
+                     b, s);
+  hipLaunchKernelGGL((kacc::pod_kernel<Z, V>), dim3(kacc::kPodGrid), dim3(kacc::kBlock), 0, st, b, s);
 }
 
 void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
@@ -1123,16 +1433,12 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 3: launch_zv<4, 3>(b, s, st); return true;
     case 4: launch_zv<4, 4>(b, s, st); return true;
     case 8: launch_zv<4, 8>(b, s, st); return true;
-    case 9: launch_zv<4, 9>(b, s, st); return true;
-    case 16: launch_zv<4, 16>(b, s, st); return true;
     case 32: launch_zv<4, 32>(b, s, st); return true;
-    case 48: launch_zv<4, 48>(b, s, st); return true;
-    case 17: launch_zv<4, 17>(b, s, st); return true;
-    case 18: launch_zv<4, 18>(b, s, st); return true;
-    case 64: launch_zv<4, 64>(b, s, st); return true;
-    case 96: launch_zv<4, 96>(b, s, st); return true;
     case 128: launch_zv<4, 128>(b, s, st); return true;
-    case 192: launch_zv<4, 192>(b, s, st); return true;
+    case 256: launch_zv<4, 256>(b, s, st); return true;
+    case 512: launch_zv<4, 512>(b, s, st); return true;
+    case 768: launch_zv<4, 768>(b, s, st); return true;
+    case 1024: launch_zv<4, 1024>(b, s, st); return true;
     default: return false;
   }
 }
@@ -1146,6 +1452,33 @@ void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const 
                      slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
                      (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p,
                      ctx->d_err);
+}
+
+// Chunk-item list sized for the worst case of a batch (every node oversized,
+// plus one partial chunk per node) and the deferred-pod list for every pod.
+// Grown (synchronously, between intervals) only when a batch is larger than
+// the capacities suggested at kacc_create.
+int ensure_items(kacc_ctx *ctx, uint64_t nodes, uint64_t procs, uint64_t pods) {
+  const uint64_t need = nodes + (procs + kacc::kChunkRows - 1) / kacc::kChunkRows + 1;
+  const uint64_t need_defer = std::max<uint64_t>(pods, 1);
+  if (need > 0xffffffffull || need_defer > 0xffffffffull)
+    return fail(ctx, KACC_EINVAL, "batch too large for the chunk lists");
+  if (need > ctx->item_cap || need_defer > ctx->defer_cap) KACC_HIP(ctx, hipDeviceSynchronize());
+  if (need > ctx->item_cap) {
+    if (ctx->d_items) KACC_HIP(ctx, hipFree(ctx->d_items));
+    ctx->d_items = nullptr;
+    ctx->item_cap = 0;
+    KACC_HIP(ctx, hipMalloc(&ctx->d_items, need * sizeof(kacc::ChunkItem)));
+    ctx->item_cap = static_cast<uint32_t>(need);
+  }
+  if (need_defer > ctx->defer_cap) {
+    if (ctx->d_defer) KACC_HIP(ctx, hipFree(ctx->d_defer));
+    ctx->d_defer = nullptr;
+    ctx->defer_cap = 0;
+    KACC_HIP(ctx, hipMalloc(&ctx->d_defer, need_defer * sizeof(uint2)));
+    ctx->defer_cap = static_cast<uint32_t>(need_defer);
+  }
+  return KACC_OK;
 }
 
 int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
@@ -1230,12 +1563,11 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
     }
   }
   if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_gen_list, std::max<uint64_t>(cfg->nodes, 1) * sizeof(uint32_t))) !=
-          hipSuccess ||
-      (e = hipMalloc(&ctx->d_gen_ctr, 16)) != hipSuccess) {
+      (e = hipMalloc(&ctx->d_ctr, 16)) != hipSuccess) {
     fail(ctx, KACC_ENOMEM, "hipMalloc work words: %s", hipGetErrorString(e));
     return bail(KACC_ENOMEM);
   }
+  if ((rc = ensure_items(ctx, cfg->nodes, cfg->proc_slots, cfg->pod_slots)) != KACC_OK) return bail(rc);
   if ((rc = kacc_reset(ctx)) != KACC_OK) return bail(rc);
   *out = ctx;
   return KACC_OK;
@@ -1248,8 +1580,9 @@ void kacc_destroy(kacc_ctx *ctx) {
   for (int t = 0; t < KACC_T_COUNT; ++t)
     if (ctx->tables[t]) (void)hipFree(ctx->tables[t]);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
-  if (ctx->d_gen_list) (void)hipFree(ctx->d_gen_list);
-  if (ctx->d_gen_ctr) (void)hipFree(ctx->d_gen_ctr);
+  if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
+  if (ctx->d_items) (void)hipFree(ctx->d_items);
+  if (ctx->d_defer) (void)hipFree(ctx->d_defer);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1268,7 +1601,7 @@ int kacc_reset(kacc_ctx *ctx) {
                                  std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
                                  ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
-  KACC_HIP(ctx, hipMemsetAsync(ctx->d_gen_ctr, 0, 16, ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return KACC_OK;
 }
@@ -1279,6 +1612,7 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK || b->n_nodes == 0) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   launch(ctx->cfg.zones, *b, dev_state(ctx), st);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
@@ -1293,7 +1627,7 @@ int kacc_sync(kacc_ctx *ctx, void *stream) {
   KACC_HIP(ctx, hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     KACC_HIP(ctx, hipMemset(ctx->d_err, 0, sizeof(uint32_t)));
-    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace)", err);
+    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list)", err);
   }
   return KACC_OK;
 }
@@ -1420,6 +1754,7 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
     KACC_HIP(ctx, hipMemcpyAsync(bt->bufs[i].second, bt->bufs[i].first, bt->sizes[i],
                                  hipMemcpyHostToDevice, ctx->stream));
   }
+  if ((rc = ensure_items(ctx, dv.n_nodes, dv.n_procs, dv.n_pods)) != KACC_OK) return rc;
   launch(ctx->cfg.zones, dv, dev_state(ctx), ctx->stream);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
@@ -1521,6 +1856,7 @@ int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, 
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK || b->n_nodes == 0) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   if (!launch_variant(ctx->cfg.zones, variant, *b, dev_state(ctx), st))
     return fail(ctx, KACC_EINVAL, "variant %d not built for Z=%u", variant, ctx->cfg.zones);
   KACC_HIP(ctx, hipGetLastError());

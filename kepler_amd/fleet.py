@@ -184,6 +184,42 @@ def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
     )
 
 
+def layout_from_sizes(zones: int, nodes, seed: int = SEED, shuffle_slots: bool = False) -> FleetLayout:
+    """Layout with explicit per-node segment sizes (edge-case fleets).
+
+    ``nodes`` is a list of dicts: ``rows`` (processes), ``ctr`` (processes per
+    container, listing order), ``vm`` (processes per VM) and ``pod``
+    (containers per pod; pods take containers from the front, the rest stay
+    pod-less).  Rows are laid out [container procs][VM procs][rest].
+    """
+    rng = np.random.default_rng(seed)
+    proc_off, ctr_off, vm_off, pod_off = [0], [0], [0], [0]
+    ctr_end, vm_end, pod_end = [], [], []
+    for nd in nodes:
+        base, cbase = proc_off[-1], ctr_off[-1]
+        ctr, vm, pod = list(nd.get("ctr", [])), list(nd.get("vm", [])), list(nd.get("pod", []))
+        rows = int(nd["rows"])
+        assert sum(ctr) + sum(vm) <= rows and sum(pod) <= len(ctr)
+        ctr_end += list(base + np.cumsum(ctr, dtype=np.int64)) if ctr else []
+        vm_end += list(base + sum(ctr) + np.cumsum(vm, dtype=np.int64)) if vm else []
+        pod_end += list(cbase + np.cumsum(pod, dtype=np.int64)) if pod else []
+        proc_off.append(base + rows)
+        ctr_off.append(cbase + len(ctr))
+        vm_off.append(vm_off[-1] + len(vm))
+        pod_off.append(pod_off[-1] + len(pod))
+    n_procs, n_ctrs, n_vms, n_pods = proc_off[-1], ctr_off[-1], vm_off[-1], pod_off[-1]
+    slots = [(rng.permutation(k) if shuffle_slots else np.arange(k)) for k in (n_procs, n_ctrs, n_vms, n_pods)]
+    u32 = lambda a: np.ascontiguousarray(a, dtype=np.uint32)  # noqa: E731
+    n_ns = max(len(nodes), 1)
+    return FleetLayout(
+        zones=zones, n_nodes=len(nodes),
+        proc_off=u32(proc_off), ctr_off=u32(ctr_off), vm_off=u32(vm_off), pod_off=u32(pod_off),
+        ctr_proc_end=u32(ctr_end), vm_proc_end=u32(vm_end), pod_ctr_end=u32(pod_end),
+        proc_slot=u32(slots[0]), ctr_slot=u32(slots[1]), vm_slot=u32(slots[2]), pod_slot=u32(slots[3]),
+        pod_ns=u32(rng.integers(0, n_ns, size=n_pods)), n_namespaces=n_ns,
+    )
+
+
 def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None) -> FleetLayout:
     """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed)."""
     if config == 1:  # single node, 500 procs -> 50 containers -> 20 pods, package+dram

@@ -128,6 +128,37 @@ def test_random_fleet_bit_exact(name, kw):
         np.testing.assert_allclose(eng.table(f"{kind}_power"), lst.state[f"{kind}_power"], rtol=1e-12, atol=1e-6)
 
 
+def _chunk_edge_nodes():
+    """Big-node chunking edges (chunks of 2048 rows, <= 512 aggregates per lane
+    pass): segments and pods straddling chunks, a container longer than a
+    chunk, > 512 (empty) containers owned by one chunk, empty pods at the end,
+    a node with no rows but > 512 aggregates, and a fast-path node beside them."""
+    rng = np.random.default_rng(21)
+    # 1: 7000 rows; containers of 7 straddle chunk boundaries; pods of 3-5 containers
+    c1 = [7] * 700
+    p1 = list(rng.integers(3, 6, size=150))
+    # 2: one 4500-row container (3 chunks), 600 empty containers in chunk 2, pods over all
+    c2 = [4500] + [0] * 600 + [10] * 20
+    p2 = [1, 300, 200, 100, 5, 0, 0]
+    # 3: no rows, 700 empty containers, 5 empty VMs, 200 pods (> 512 aggregates)
+    c3 = [0] * 700
+    # 4: VMs straddling chunks, pod-less containers after the pods
+    c4 = [30] * 100
+    return [
+        dict(rows=7000, ctr=c1, vm=[40, 40, 40], pod=p1),
+        dict(rows=4700, ctr=c2, vm=[], pod=p2),
+        dict(rows=0, ctr=c3, vm=[0] * 5, pod=[3] * 200 + [0, 0]),
+        dict(rows=9000, ctr=c4, vm=[700] * 5 + [1] * 100, pod=[2] * 20),
+        dict(rows=900, ctr=[9] * 80, vm=[3], pod=[4] * 20),
+    ]
+
+
+@pytest.mark.parametrize("zones,shuffle", [(4, False), (3, True), (8, False)])
+def test_big_node_chunk_edges(zones, shuffle):
+    layout = fleet.layout_from_sizes(zones, _chunk_edge_nodes(), seed=5, shuffle_slots=shuffle)
+    run_both(layout, dict(churn=0.05, zero_ratio_frac=0.1), 4, node_order=shuffle, seed=7)
+
+
 def test_wrapping_fake_meter_and_node_order():
     layout = fleet.make_layout(40, [0, 1, 2, 3, 500, 2000, 64, 65] * 5, 2, seed=3, shuffle_slots=True)
     run_both(layout, dict(max_energy=fleet.MAX_ENERGY_FAKE, churn=0.1), 5, node_order=True, seed=5)

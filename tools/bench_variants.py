@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """Interleaved timing of interval-kernel ablation variants on config 3 (one process).
 
-Variants (kacc_debug.h): 0 production, 1 skip aggregates, 2 skip processes,
-3 node phases only, 4 unstaged, 8 non-temporal stores, 9 = 1|8.
+Variants (kacc_debug.h, bits of kacc::kVar*): 0 production, 1 skip aggregates,
+2 skip processes, 3 node phases only, 4 unstaged (every node on the chunked
+big-node path), 8 non-temporal stores, 32 no 64-row-group transpose, 128 late
+aggregate loads, 256 / 512 / 768 big nodes without the CPU-total pass / the
+segment-owner scan / both, 1024 big nodes without the item-list atomic.
 Also times the namespace kernel.  Prints a JSON summary.
 """
 import json
@@ -21,7 +24,7 @@ def main():
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
-    variants = [int(x) for x in os.environ.get("VARIANTS", "0,32,64,128,192,1,2,3").split(",")]
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,32,128,1,2,3").split(",")]
     rounds = int(os.environ.get("ROUNDS", "10"))
     cfg = int(os.environ.get("CONFIG", "3"))
     torch.cuda.set_device(0)

@@ -23,8 +23,19 @@ if [ "$1" = "prof" ]; then
 fi
 if [ "$1" = "configs" ] || [ "$2" = "configs" ]; then
   cd "$R"
+  CONFIG=5 VARIANTS=${C5_VARIANTS:-0,32,1,2} ROUNDS=6 timeout -k 10 300 python tools/bench_variants.py > gpurun_out/variants_c5.json 2> gpurun_out/variants_c5.err || exit $?
+  python -c "import json;d=json.load(open('gpurun_out/variants_c5.json'));print('c5 variants', {k:round(v['median_ms'],4) for k,v in d['variants'].items()})"
   timeout -k 10 400 python bench.py --config 5 --steps 10 --warmup 2 --no-cpu-baseline --json-out gpurun_out/bench_c5.json > gpurun_out/bench_c5.log 2>&1 || exit $?
   timeout -k 10 400 python bench.py --config 5 --node-order --steps 10 --warmup 2 --no-cpu-baseline --json-out gpurun_out/bench_c5_lpt.json > gpurun_out/bench_c5_lpt.log 2>&1 || exit $?
   timeout -k 10 400 python bench.py --config 2 --steps 20 --warmup 3 --no-cpu-baseline --json-out gpurun_out/bench_c2.json > gpurun_out/bench_c2.log 2>&1 || exit $?
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_c5" -o run -- python "$R/bench.py" --config 5 --steps 10 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof_c5.log" 2>&1 || exit $?
+  cd "$R"
+  python - <<'PY'
+import csv, glob
+for f in glob.glob('gpurun_out/prof_c5/**/*kernel_stats.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        print('c5prof', r['Name'][:60], r['Calls'], r['AverageNs'])
+PY
   for f in bench_c5 bench_c5_lpt bench_c2; do python -c "import json;d=json.load(open('gpurun_out/$f.json'));print('$f', 'value',d['value'],'kernel_ms',d['kernel_ms'],'frac',d['roofline']['frac'],d['config']['workload'])"; done
 fi
