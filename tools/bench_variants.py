@@ -24,6 +24,8 @@ def main():
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
+    if os.environ.get("KACC_LIB"):  # A/B of another build of the engine
+        accel.load(os.environ["KACC_LIB"])
     variants = [int(x) for x in os.environ.get("VARIANTS", "0,32,128,1,2,3").split(",")]
     rounds = int(os.environ.get("ROUNDS", "10"))
     cfg = int(os.environ.get("CONFIG", "3"))

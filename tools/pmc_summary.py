@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into pmc_traffic.json.
+
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR SOURCE_LABEL OUT.json [CONFIG]
+
+FETCH_SIZE is doubled (MI355X_MICROARCH.md §HBM: gfx950 tallies 128-B streaming
+reads at 64 B); both counters are KiB.  Per launch of kacc::interval_kernel<Z,0>.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def values(d, counter, kernel="interval_kernel<4, 0>"):
+    out = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                out.append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    fdir, wdir, label, out = sys.argv[1:5]
+    cfg = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    from kepler_amd import accel, fleet
+
+    layout = fleet.config_layout(cfg)
+    s = layout.sizes()
+    alg = accel.interval_bytes(layout.zones, *[s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
+    fv, wv = values(fdir, "FETCH_SIZE"), values(wdir, "WRITE_SIZE")
+    if not fv or not wv:
+        raise SystemExit("no interval_kernel counter rows found")
+    fm, wm = statistics.median(fv), statistics.median(wv)
+    res = {
+        f"config{cfg}": {
+            "n_procs": s["n_procs"],
+            "kernel": "kacc::interval_kernel<4,0>",
+            "fetch_size_kib_median": fm,
+            "write_size_kib_median": wm,
+            "hbm_bytes_per_launch": (2.0 * fm + wm) * 1024.0,
+            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+            "tools/bench_variants.py (VARIANTS=0 ROUNDS=3); FETCH_SIZE doubled per "
+            "MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B streaming reads at 64 B); values in KiB",
+            "algorithmic_bytes_per_launch": alg,
+            "source": label,
+            "raw_kib": {"FETCH_SIZE": fv, "WRITE_SIZE": wv},
+        }
+    }
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    r = res[f"config{cfg}"]
+    print(f"traffic {r['hbm_bytes_per_launch']/1e9:.3f} GB/launch vs algorithmic {alg/1e9:.3f} GB")
+
+
+if __name__ == "__main__":
+    main()
