@@ -142,7 +142,7 @@ def main():
         return t
 
     step_tensors = [make(k) for k in range(n_steps)]
-    step_ivs = [interval_from_tensors(t, sizes) for t in step_tensors]
+    step_ivs = [interval_from_tensors(t, sizes, layout.fast_flag()) for t in step_tensors]
     prime_t = to_device(prime)
     acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
     acc.sync(stream)

@@ -74,6 +74,15 @@ extern "C" {
 /* kacc_interval.flags */
 #define KACC_F_NODE_CPU_DELTA_GIVEN 0x1u /* use node_cpu_delta[] instead of the
                                              on-device sum (mock informers)     */
+#define KACC_F_FAST_NODES 0x2u /* caller guarantees every node has at most
+                                   KACC_FAST_MAX_PROCS process rows and at most
+                                   KACC_FAST_MAX_AGGREGATES containers+VMs+pods:
+                                   the big-node (chunk / deferred-pod) launches
+                                   are skipped.  A node that does not fit is not
+                                   computed and raises KACC_ERANGE (bit 32).
+                                   kacc_batch_submit sets it by itself.       */
+#define KACC_FAST_MAX_PROCS 2048u
+#define KACC_FAST_MAX_AGGREGATES 512u
 
 typedef struct kacc_ctx kacc_ctx;
 

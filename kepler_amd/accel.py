@@ -35,6 +35,9 @@ KACC_NODE_OK = 0
 KACC_NODE_FIRST_READ = 1
 KACC_NODE_SKIPPED = 2
 KACC_F_NODE_CPU_DELTA_GIVEN = 0x1
+KACC_F_FAST_NODES = 0x2
+KACC_FAST_MAX_PROCS = 2048
+KACC_FAST_MAX_AGGREGATES = 512
 
 # kacc_table enum, in header order: (name, numpy dtype)
 TABLES = [

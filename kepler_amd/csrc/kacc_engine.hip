@@ -72,6 +72,9 @@ constexpr uint32_t kErrOffsets = 1u << 1;
 constexpr uint32_t kErrSlot = 1u << 2;
 constexpr uint32_t kErrNs = 1u << 3;
 constexpr uint32_t kErrCapacity = 1u << 4;
+constexpr uint32_t kErrBigNode = 1u << 5;  // oversized node under KACC_F_FAST_NODES
+static_assert(kRowsLds == KACC_FAST_MAX_PROCS && kTpb<0> == KACC_FAST_MAX_AGGREGATES,
+              "KACC_FAST_* must match the fast path's capacity");
 
 // One big-node chunk (see big_node_prepare).  ctr_begin / vm_begin / pod_begin:
 // the first container / VM / pod the chunk owns; it owns them up to the next
@@ -426,6 +429,10 @@ void interval_kernel(const kacc_interval b, const DevState st) {
   }
   const NodeRanges rg = node_ranges(b, st, n, tid);
   if (!fits_fast<V>(rg)) {  // node phase here, the rest in chunk_kernel (+ pod_kernel)
+    if (b.flags & KACC_F_FAST_NODES) {  // the caller promised no such node: no launch follows
+      if (tid == 0) raise_err(st.err, kErrBigNode);
+      return;
+    }
     __shared__ uint32_t s_base;
     big_node_prepare<Z, V>(b, st, n, rg, red, sh, s_base);
     return;
@@ -1398,11 +1405,13 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
 
 // One interval = the fast kernel (one workgroup per node; oversized nodes get
 // their node phase there and are cut into chunk items), the chunk kernel and
-// the deferred-pod kernel (both exit at once when no node was oversized).
+// the deferred-pod kernel (both exit at once when no node was oversized; not
+// launched at all under KACC_F_FAST_NODES).
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
                      s);
+  if (b.flags & KACC_F_FAST_NODES) return;
   const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
   hipLaunchKernelGGL((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
                      b, s);
@@ -1497,7 +1506,7 @@ int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
     return fail(ctx, KACC_EINVAL, "required row array is NULL");
   if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
     return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
-  if (b->flags & ~KACC_F_NODE_CPU_DELTA_GIVEN)
+  if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES))
     return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
   return KACC_OK;
 }
@@ -1519,6 +1528,17 @@ int check_slots(kacc_ctx *ctx, const char *name, const uint32_t *w, uint32_t n, 
     seen[s] = 1;
   }
   return KACC_OK;
+}
+
+// Every node fits the fast path (host batch, offsets already validated).
+bool all_nodes_fast(const kacc_interval &b) {
+  for (uint32_t n = 0; n < b.n_nodes; ++n) {
+    const uint32_t rows = b.proc_off[n + 1] - b.proc_off[n];
+    const uint32_t agg = (b.ctr_off[n + 1] - b.ctr_off[n]) + (b.vm_off[n + 1] - b.vm_off[n]) +
+                         (b.pod_off[n + 1] - b.pod_off[n]);
+    if (rows > KACC_FAST_MAX_PROCS || agg > KACC_FAST_MAX_AGGREGATES) return false;
+  }
+  return true;
 }
 
 }  // namespace
@@ -1627,7 +1647,7 @@ int kacc_sync(kacc_ctx *ctx, void *stream) {
   KACC_HIP(ctx, hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     KACC_HIP(ctx, hipMemset(ctx->d_err, 0, sizeof(uint32_t)));
-    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list)", err);
+    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list 32=oversized node under KACC_F_FAST_NODES)", err);
   }
   return KACC_OK;
 }
@@ -1744,7 +1764,7 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (rc != KACC_OK) return rc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   kacc_interval dv = bt->dev;
-  dv.flags = bt->host.flags;
+  dv.flags = bt->host.flags | (all_nodes_fast(bt->host) ? KACC_F_FAST_NODES : 0u);
   // honour optional arrays the caller switched off
   if (!bt->host.node_status) dv.node_status = nullptr;
   if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;

@@ -90,6 +90,16 @@ class FleetLayout:
             pod_slots=max(int(self.pod_slot.max(initial=0)) + 1, 1),
         )
 
+    def fast_flag(self) -> int:
+        """KACC_F_FAST_NODES when every node fits the fast path, else 0."""
+        from .accel import KACC_F_FAST_NODES, KACC_FAST_MAX_AGGREGATES, KACC_FAST_MAX_PROCS
+
+        rows = np.diff(self.proc_off.astype(np.int64))
+        agg = (np.diff(self.ctr_off.astype(np.int64)) + np.diff(self.vm_off.astype(np.int64))
+               + np.diff(self.pod_off.astype(np.int64)))
+        fits = bool(np.all(rows <= KACC_FAST_MAX_PROCS) and np.all(agg <= KACC_FAST_MAX_AGGREGATES))
+        return KACC_F_FAST_NODES if fits else 0
+
     def static_arrays(self) -> Dict[str, np.ndarray]:
         return dict(proc_off=self.proc_off, ctr_off=self.ctr_off, vm_off=self.vm_off,
                     pod_off=self.pod_off, ctr_proc_end=self.ctr_proc_end,

@@ -91,7 +91,7 @@ def run_both(layout, sim_kwargs, n_intervals, node_order=False, seed=1):
         a = sim.next_interval()
         if node_order:
             a["node_order"] = layout.node_order_heaviest_first()
-        eng.interval(a, layout.sizes(), 0)
+        eng.interval(a, layout.sizes(), layout.fast_flag())  # skip empty big-node launches when possible
         ora.interval(a, layout.sizes())
         lst.interval(a, layout.sizes())
         for name, _ in accel.TABLES:
@@ -112,6 +112,19 @@ FLEETS = [
     ("z2-many-aggregates", dict(n_nodes=5, procs_per_node=[600, 700, 800, 2000, 300], zones=2,
                                 procs_per_ctr=1, ctrs_per_pod=1.0, vm_frac=0.05)),
 ]
+
+
+def test_fast_flag_rejects_oversized_node():
+    """KACC_F_FAST_NODES is a promise: an oversized node raises KACC_ERANGE, nothing faults."""
+    layout = fleet.make_layout(3, [100, 2049, 5], 4, seed=5)
+    assert layout.fast_flag() == 0
+    eng = EngineBackend(layout.zones, layout.capacities())
+    a = fleet.FleetSim(layout, seed=5).next_interval()
+    with pytest.raises(accel.AccelError) as ei:
+        eng.interval(a, layout.sizes(), accel.KACC_F_FAST_NODES)
+    assert ei.value.code == accel.KACC_ERANGE
+    # the same batch without the promise runs (and the context is usable again)
+    eng.interval(a, layout.sizes(), 0)
 
 
 @pytest.mark.parametrize("name,kw", FLEETS, ids=[f[0] for f in FLEETS])

@@ -42,7 +42,8 @@ def main():
     # distinct input sets cycled like bench.py (no cache reuse between launches)
     n_distinct = int(os.environ.get("DISTINCT", "4"))
     dev = [to_device(sim.next_interval()) for _ in range(n_distinct)]
-    ivs = [interval_from_tensors(a, layout.sizes()) for a in dev]
+    flag = 0 if os.environ.get("KACC_LIB") else layout.fast_flag()  # older builds reject the flag
+    ivs = [interval_from_tensors(a, layout.sizes(), flag) for a in dev]
     it = ivs[0]
     Z = layout.zones
     sizes = layout.sizes()
