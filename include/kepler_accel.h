@@ -234,6 +234,57 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *ns_pod_o
                           const uint32_t *ns_pod_slot, uint64_t *out_energy, double *out_power,
                           void *stream);
 
+/* ---- slot join: workload IDs -> slot words on the device ------------------
+ * SURVEY §8f row 1, the step before the path.  Replaces, for a whole fleet,
+ * the per-row string-keyed lookups of the previous snapshot that decide
+ * "new workload or running total" (process.go:132-138 prev.Processes[pid],
+ * container.go:126, vm.go:96, pod.go:106) and the informer's terminated sets
+ * (informer.go:206-212 processes, :236-246 containers, :260-270 VMs,
+ * :311-322 pods) whose prev entries feed the terminated trackers
+ * (process.go:87-99, container.go:80-90, vm.go:55-65, pod.go:56-66).
+ *
+ * One slot map per workload kind.  Node n owns the slot range
+ * [slot_off[n], slot_off[n+1]) of that kind's state tables and a private
+ * device hash table (load <= 1/2) of its live IDs.  kacc_slot_join() takes
+ * the IDs of the node's rows in batch order and, per node:
+ *   - a live ID keeps its slot (slot word without KACC_SLOT_NEW);
+ *   - an ID that was not live at the node's previous processed interval gets
+ *     the lowest slot of its range that was free at the start of this call,
+ *     new rows taking slots in row order (KACC_SLOT_NEW set) — deterministic;
+ *   - an ID live before but absent now is terminated: (key, slot) is appended
+ *     to the term_* list (node segments in any order) and its slot is NOT
+ *     reused before the next call, so the tracker can still read its final
+ *     values (the reference reads them from prev, process.go:90-99);
+ *   - a node with KACC_NODE_READ_ERROR is skipped (map unchanged), as the
+ *     reference skips Refresh when calculateNodePower fails (monitor.go:399-410).
+ * Errors (duplicate ID in a node, KACC_KEY_EMPTY, more live IDs than the
+ * node's range, term list overflow) are raised as KACC_ERANGE at kacc_sync;
+ * the affected rows get slot word 0xffffffff.                                */
+typedef enum kacc_kind {
+  KACC_KIND_PROC = 0, /* key: PID (pid_t) — process.go:120 StringID */
+  KACC_KIND_CTR = 1,  /* key: 64-bit ID of the container ID string   */
+  KACC_KIND_VM = 2,   /* key: 64-bit ID of the VM ID string          */
+  KACC_KIND_POD = 3   /* key: 64-bit ID of the pod UID               */
+} kacc_kind;
+#define KACC_KEY_EMPTY 0xffffffffffffffffull /* reserved, never a valid key */
+
+typedef struct kacc_slotmap kacc_slotmap;
+/* slot_off: HOST [n_nodes + 1], monotonic, slot_off[n_nodes] <= the kind's
+ * slot capacity in kacc_config.  The map starts empty.                       */
+int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const uint32_t *slot_off,
+                        kacc_slotmap **out);
+void kacc_slotmap_destroy(kacc_slotmap *m);
+int kacc_slotmap_reset(kacc_slotmap *m); /* forget every ID (PowerMonitor restart) */
+/* Device pointers, asynchronous on `stream` (NULL = the context's stream).
+ * n_rows = row_off[n_nodes] (the batch's n_procs / n_ctrs / n_vms / n_pods);
+ * row_off [n_nodes+1]: the batch's proc_off / ctr_off / vm_off / pod_off;
+ * keys [n_rows]; node_status [n_nodes] or NULL; out_slot [n_rows] (may be the
+ * batch's *_slot array); term_key/term_slot [term_cap]; *term_count is set to
+ * the number of terminated IDs (entries past term_cap are dropped + ERANGE).  */
+int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
+                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
+                   uint32_t *term_slot, uint32_t *term_count, uint32_t term_cap, void *stream);
+
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

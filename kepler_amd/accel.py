@@ -35,6 +35,8 @@ KACC_NODE_OK = 0
 KACC_NODE_FIRST_READ = 1
 KACC_NODE_SKIPPED = 2
 KACC_F_NODE_CPU_DELTA_GIVEN = 0x1
+KACC_KIND_PROC, KACC_KIND_CTR, KACC_KIND_VM, KACC_KIND_POD = 0, 1, 2, 3
+KACC_KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
 KACC_F_FAST_NODES = 0x2
 KACC_FAST_MAX_PROCS = 2048
 KACC_FAST_MAX_AGGREGATES = 512
@@ -71,6 +73,10 @@ TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)
 EXPORTS = [
+    "kacc_slotmap_create",
+    "kacc_slotmap_destroy",
+    "kacc_slotmap_reset",
+    "kacc_slot_join",
     "kacc_abi_version",
     "kacc_create",
     "kacc_destroy",
@@ -212,6 +218,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
+    lib.kacc_slotmap_create.argtypes = [c_void_p, c_int, c_uint32, c_void_p, POINTER(c_void_p)]
+    lib.kacc_slotmap_destroy.argtypes = [c_void_p]
+    lib.kacc_slotmap_destroy.restype = None
+    lib.kacc_slotmap_reset.argtypes = [c_void_p]
+    lib.kacc_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
     if lib.kacc_abi_version() != KACC_ABI_VERSION:
         raise ImportError("libkepler_accel ABI version mismatch")
     _lib = lib
@@ -338,6 +350,44 @@ class Accel:
         self._check(self.lib.kacc_namespace_totals(
             self.ctx, n_ns, c_void_p(ns_pod_off_ptr), c_void_p(ns_pod_slot_ptr),
             c_void_p(out_energy_ptr), c_void_p(out_power_ptr), c_void_p(stream or None)))
+
+
+class SlotMap:
+    """Device slot join of one workload kind (kacc_slotmap, kacc_slot_join).
+
+    Node n owns slots [slot_off[n], slot_off[n+1]) of the kind's state tables.
+    ``join`` takes device pointers (torch ``data_ptr()``) and runs on ``stream``.
+    """
+
+    def __init__(self, accel: Accel, kind: int, slot_off: np.ndarray):
+        self.accel = accel
+        self.lib = accel.lib
+        off = np.ascontiguousarray(slot_off, dtype=np.uint32)
+        h = c_void_p()
+        accel._check(self.lib.kacc_slotmap_create(accel.ctx, kind, off.size - 1, off.ctypes.data, ctypes.byref(h)))
+        self.handle = h
+        self.n_nodes = off.size - 1
+
+    def reset(self) -> None:
+        self.accel._check(self.lib.kacc_slotmap_reset(self.handle))
+
+    def join(self, n_rows: int, row_off_ptr: int, keys_ptr: int, node_status_ptr: int, out_slot_ptr: int,
+             term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, term_cap: int, stream: int = 0) -> None:
+        self.accel._check(self.lib.kacc_slot_join(
+            self.handle, n_rows, c_void_p(row_off_ptr), c_void_p(keys_ptr or None),
+            c_void_p(node_status_ptr or None), c_void_p(out_slot_ptr), c_void_p(term_key_ptr or None),
+            c_void_p(term_slot_ptr or None), c_void_p(term_count_ptr), term_cap, c_void_p(stream or None)))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.kacc_slotmap_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 @dataclass

@@ -31,12 +31,12 @@
 #include "../../include/kepler_accel.h"
 #include "kacc_debug.h"
 #include "kacc_device.hpp"
+#include "kacc_internal.hpp"
 
 namespace kacc {
 
 constexpr int kTree = 256;                   // lanes of the canonical node-total tree
 constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per node (16 KiB)
-constexpr int kSegLoads = 8;                 // container rows loaded per step (pod kernel)
 constexpr int kBlock = 256;                  // namespace kernel workgroup
 template <int Z>
 constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 64-row groups
@@ -1303,31 +1303,7 @@ const TableDesc kTables[KACC_T_COUNT] = {
 
 }  // namespace
 
-struct kacc_ctx {
-  int device = 0;
-  kacc_config cfg{};
-  hipStream_t stream = nullptr;
-  void *tables[KACC_T_COUNT] = {};
-  uint64_t counts[KACC_T_COUNT] = {};
-  uint32_t *d_err = nullptr;
-  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
-  kacc::ChunkItem *d_items = nullptr;
-  uint32_t item_cap = 0;
-  uint2 *d_defer = nullptr;
-  uint32_t defer_cap = 0;
-  std::string err;
-};
-
-struct kacc_batch {
-  kacc_interval host{};
-  kacc_interval dev{};
-  std::vector<std::pair<void *, void *>> bufs;  // {pinned host, device}
-  std::vector<size_t> sizes;
-};
-
-namespace {
-
-int fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
+int kacc_fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -1340,13 +1316,9 @@ int fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
   return code;
 }
 
-#define KACC_HIP(ctx, call)                                                              \
-  do {                                                                                   \
-    hipError_t e_ = (call);                                                              \
-    if (e_ != hipSuccess)                                                                \
-      return fail((ctx), e_ == hipErrorOutOfMemory ? KACC_ENOMEM : KACC_EHIP, "%s: %s", \
-                  #call, hipGetErrorString(e_));                                         \
-  } while (0)
+namespace {
+
+#define fail kacc_fail
 
 uint64_t table_count(const kacc_config &c, int t) {
   const TableDesc &d = kTables[t];

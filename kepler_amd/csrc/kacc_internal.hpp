@@ -1,0 +1,50 @@
+// Internal host-side definitions shared by the engine's translation units
+// (kacc_engine.hip: interval path, kacc_join.hip: slot join + terminated
+// tracker).  Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/kepler_accel.h"
+
+namespace kacc {
+struct ChunkItem;
+}
+
+struct kacc_ctx {
+  int device = 0;
+  kacc_config cfg{};
+  hipStream_t stream = nullptr;
+  void *tables[KACC_T_COUNT] = {};
+  uint64_t counts[KACC_T_COUNT] = {};
+  uint32_t *d_err = nullptr;
+  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
+  kacc::ChunkItem *d_items = nullptr;
+  uint32_t item_cap = 0;
+  uint2 *d_defer = nullptr;
+  uint32_t defer_cap = 0;
+  std::string err;
+};
+
+struct kacc_batch {
+  kacc_interval host{};
+  kacc_interval dev{};
+  std::vector<std::pair<void *, void *>> bufs;  // {pinned host, device}
+  std::vector<size_t> sizes;
+};
+
+// Records the message on ctx (or the thread's create error when ctx is NULL)
+// and returns code.
+int kacc_fail(kacc_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));
+
+#define KACC_HIP(ctx, call)                                                                   \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return kacc_fail((ctx), e_ == hipErrorOutOfMemory ? KACC_ENOMEM : KACC_EHIP, "%s: %s", \
+                       #call, hipGetErrorString(e_));                                         \
+  } while (0)

@@ -379,3 +379,55 @@ def subset_interval(a: Dict[str, np.ndarray], nodes: np.ndarray, zones: int):
         maps[kind] = orig
     sizes = dict(n_nodes=len(nodes), n_procs=len(pidx), n_ctrs=len(cidx), n_vms=len(vidx), n_pods=len(qidx))
     return out, sizes, maps
+
+
+@dataclass
+class KeyedChurn:
+    """Per-row workload IDs with churn, for the slot join (kacc_slot_join).
+
+    Row r of node n holds one live ID; each interval a ``churn`` fraction of
+    rows is taken over by a new ID (the old one terminates), as PIDs turn over
+    in /proc.  IDs are node-local PIDs (``kind='proc'``) or random 64-bit IDs
+    (container / VM / pod string IDs hashed by the packer).
+    """
+
+    row_off: np.ndarray
+    seed: int = SEED
+    churn: float = 0.02
+    kind: str = "proc"
+    _rng: np.random.Generator = field(init=False, repr=False)
+
+    def __post_init__(self):
+        self._rng = np.random.default_rng(self.seed ^ 0x4A4F494E)
+        off = self.row_off.astype(np.int64)
+        n_rows = int(off[-1])
+        self.node_of_row = np.repeat(np.arange(len(off) - 1), np.diff(off))
+        if self.kind == "proc":
+            # node-local PIDs: distinct per node, ascending-ish like /proc
+            local = np.arange(n_rows) - off[self.node_of_row]
+            self.keys = (300 + 3 * local + self._rng.integers(0, 3, size=n_rows)).astype(np.uint64)
+            self.next_pid = np.full(len(off) - 1, 1 << 22, dtype=np.int64)
+        else:
+            self.keys = self._new_ids(n_rows)
+
+    def _new_ids(self, k: int) -> np.ndarray:
+        x = self._rng.integers(0, 2**63 - 1, size=k, dtype=np.int64).astype(np.uint64)
+        return x * np.uint64(2) + np.uint64(1) - np.uint64(2) * (x == np.uint64(2**63 - 1))
+
+    def next_keys(self) -> np.ndarray:
+        """Advance one interval (churned rows get new IDs); returns the keys."""
+        born = np.flatnonzero(self._rng.random(self.keys.size) < self.churn)
+        if born.size:
+            if self.kind == "proc":
+                nodes = self.node_of_row[born]
+                # new PIDs, increasing per node (never reused within the run)
+                order = np.argsort(nodes, kind="stable")
+                nb = nodes[order]
+                first = np.r_[0, np.flatnonzero(np.diff(nb)) + 1]
+                rank = np.arange(nb.size) - np.repeat(first, np.diff(np.r_[first, nb.size]))
+                pids = self.next_pid[nb] + rank
+                np.add.at(self.next_pid, nb, 1)
+                self.keys[born[order]] = pids.astype(np.uint64)
+            else:
+                self.keys[born] = self._new_ids(born.size)
+        return self.keys.copy()

@@ -1,0 +1,92 @@
+// ORACLE — TEST INFRASTRUCTURE ONLY (see kepler_oracle.h).
+//
+// CPU restatement of the slot join (include/kepler_accel.h kacc_slot_join)
+// in terms of the reference's own data structures: per node, the set of IDs
+// of the previous snapshot is a map (Go: prev.Processes keyed by PID string,
+// process.go:132-138; prev.Containers / VirtualMachines / Pods by ID,
+// container.go:126, vm.go:96, pod.go:106), and the terminated set is
+// "cached before, not running now" (informer.go:206-212 for processes,
+// :236-246 containers, :260-270 VMs, :311-322 pods).  The slot numbering rule
+// is the engine's own (the reference has no slots): a new ID takes the lowest
+// slot of its node's range not held by any ID of the previous set, new rows
+// taking slots in row order.
+#include <cstdint>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "kepler_oracle.h"
+
+struct kor_slotmap {
+  std::vector<uint32_t> slot_off;
+  std::vector<std::unordered_map<uint64_t, uint32_t>> live;  // per node: ID -> slot
+};
+
+extern "C" {
+
+kor_slotmap *kor_slotmap_create(uint32_t n_nodes, const uint32_t *slot_off) {
+  auto *m = new kor_slotmap;
+  m->slot_off.assign(slot_off, slot_off + n_nodes + 1);
+  m->live.resize(n_nodes);
+  return m;
+}
+
+void kor_slotmap_destroy(kor_slotmap *m) { delete m; }
+
+int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
+                  const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
+                  uint32_t *term_slot, uint32_t term_cap, uint32_t *term_count) {
+  const uint32_t N = static_cast<uint32_t>(m->live.size());
+  uint32_t nt = 0;
+  int rc = KACC_OK;
+  for (uint32_t n = 0; n < N; ++n) {
+    if (node_status && (node_status[n] & KACC_NODE_READ_ERROR)) continue;  // Refresh skipped
+    const uint32_t r0 = row_off[n], r1 = row_off[n + 1];
+    if (r1 > n_rows || r0 > r1) return KACC_EINVAL;
+    const uint32_t s0 = m->slot_off[n], S = m->slot_off[n + 1] - s0;
+    auto &prev = m->live[n];
+    std::vector<uint8_t> used(S, 0);
+    for (const auto &kv : prev) used[kv.second] = 1;  // held until the next interval
+    std::unordered_map<uint64_t, uint32_t> cur;
+    cur.reserve(r1 - r0);
+    uint32_t next_free = 0;
+    for (uint32_t r = r0; r < r1; ++r) {
+      const uint64_t k = keys[r];
+      if (k == KACC_KEY_EMPTY || cur.count(k)) {
+        out_slot[r] = 0xffffffffu;
+        rc = KACC_ERANGE;
+        continue;
+      }
+      auto it = prev.find(k);
+      if (it != prev.end()) {  // running total continues (process.go:134-137)
+        out_slot[r] = s0 + it->second;
+        cur.emplace(k, it->second);
+        continue;
+      }
+      while (next_free < S && used[next_free]) ++next_free;
+      if (next_free >= S) {
+        out_slot[r] = 0xffffffffu;
+        rc = KACC_ERANGE;
+        continue;
+      }
+      used[next_free] = 1;
+      out_slot[r] = (s0 + next_free) | KACC_SLOT_NEW;
+      cur.emplace(k, next_free);
+    }
+    for (const auto &kv : prev) {
+      if (cur.count(kv.first)) continue;
+      if (nt < term_cap) {
+        term_key[nt] = kv.first;
+        term_slot[nt] = s0 + kv.second;
+      } else {
+        rc = KACC_ERANGE;
+      }
+      ++nt;
+    }
+    prev.swap(cur);
+  }
+  *term_count = nt;
+  return rc;
+}
+
+}  // extern "C"

@@ -56,6 +56,12 @@ def load():
     lib.kor_aggregated_max.restype = c_uint64
     lib.kor_aggregated_energy.argtypes = [c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]
     lib.kor_aggregated_energy.restype = c_uint64
+    lib.kor_slotmap_create.argtypes = [c_uint32, c_void_p]
+    lib.kor_slotmap_create.restype = c_void_p
+    lib.kor_slotmap_destroy.argtypes = [c_void_p]
+    lib.kor_slotmap_destroy.restype = None
+    lib.kor_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_uint32, c_void_p]
     lib.kor_gf_create.argtypes = [c_uint32]
     lib.kor_gf_create.restype = c_void_p
     lib.kor_gf_destroy.argtypes = [c_void_p]
@@ -163,3 +169,35 @@ class AggregatedZone:
         return int(self.lib.kor_aggregated_energy(self.n, r.ctypes.data, self.sub_max.ctypes.data,
                                                   self.last.ctypes.data, self.seen.ctypes.data,
                                                   self.current.ctypes.data, self.max))
+
+
+class OracleSlotMap:
+    """CPU restatement of kacc_slot_join (oracle/kor_join.cpp)."""
+
+    def __init__(self, slot_off: np.ndarray):
+        self.lib = load()
+        self.off = np.ascontiguousarray(slot_off, dtype=np.uint32)
+        self.h = self.lib.kor_slotmap_create(self.off.size - 1, self.off.ctypes.data)
+
+    def join(self, row_off, keys, node_status=None, term_cap=None):
+        """Returns (rc, out_slot, term_key, term_slot) on host arrays."""
+        row_off = np.ascontiguousarray(row_off, dtype=np.uint32)
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        n_rows = int(row_off[-1])
+        out = np.zeros(max(n_rows, 1), dtype=np.uint32)
+        cap = int(self.off[-1]) if term_cap is None else term_cap
+        tk = np.zeros(max(cap, 1), dtype=np.uint64)
+        ts = np.zeros(max(cap, 1), dtype=np.uint32)
+        cnt = np.zeros(1, dtype=np.uint32)
+        st = None if node_status is None else np.ascontiguousarray(node_status, dtype=np.uint32)
+        rc = self.lib.kor_slot_join(self.h, n_rows, row_off.ctypes.data, keys.ctypes.data if keys.size else None,
+                                    None if st is None else st.ctypes.data, out.ctypes.data, tk.ctypes.data,
+                                    ts.ctypes.data, cap, cnt.ctypes.data)
+        n = min(int(cnt[0]), cap)
+        return rc, out[:n_rows], tk[:n], ts[:n]
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.lib.kor_slotmap_destroy(self.h)
+        except Exception:
+            pass

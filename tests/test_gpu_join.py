@@ -1,0 +1,144 @@
+"""Device slot join (kacc_slot_join) against the oracle — MI355X only.
+
+Slot words are integer results: bit-exact against oracle/kor_join.cpp, which
+is itself checked against a Go-map restatement on CPU (test_join_oracle.py).
+The terminated list is a set (node segments land in any order; the
+reference iterates a Go map, informer.go:206-212 / process.go:89): compared
+sorted.  The end-to-end test feeds the joined slot words to the interval
+kernel and checks every state table against the oracle fed the oracle's.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from kepler_amd import accel, fleet
+from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+from oracle.oracle import Oracle, OracleSlotMap
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_ready():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    accel.load()
+    torch.cuda.set_stream(torch.cuda.Stream())
+
+
+class GpuJoin:
+    def __init__(self, acc, kind, slot_off):
+        self.acc = acc
+        self.m = accel.SlotMap(acc, kind, slot_off)
+        cap = int(slot_off[-1])
+        self.cap = max(cap, 1)
+        self.tk = torch.zeros(self.cap, dtype=torch.int64, device="cuda")
+        self.ts = torch.zeros(self.cap, dtype=torch.int32, device="cuda")
+        self.cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def join(self, row_off, keys, status=None, out=None, sync=True):
+        d_off = torch.from_numpy(row_off.astype(np.int32)).cuda()
+        d_keys = torch.from_numpy(keys.view(np.int64)).cuda()
+        d_st = None if status is None else torch.from_numpy(status.astype(np.int32)).cuda()
+        n_rows = int(row_off[-1])
+        if out is None:
+            out = torch.zeros(max(n_rows, 1), dtype=torch.int32, device="cuda")
+        s = current_stream_handle()
+        self.m.join(n_rows, d_off.data_ptr(), d_keys.data_ptr(), 0 if d_st is None else d_st.data_ptr(),
+                    out.data_ptr(), self.tk.data_ptr(), self.ts.data_ptr(), self.cnt.data_ptr(), self.cap, s)
+        if not sync:
+            return out
+        self.acc.sync(s)
+        n = min(int(self.cnt.item()), self.cap)
+        got = out[:n_rows].cpu().numpy().view(np.uint32)
+        term = sorted(zip(self.tk[:n].cpu().numpy().view(np.uint64).tolist(),
+                          self.ts[:n].cpu().numpy().view(np.uint32).tolist()))
+        return got, term
+
+
+def caps_for(slot_off):
+    n = int(slot_off[-1])
+    return dict(nodes=len(slot_off) - 1, proc_slots=max(n, 1), ctr_slots=max(n, 1), vm_slots=1, pod_slots=1)
+
+
+JOIN_FLEETS = [
+    ("tiny", [0, 1, 2, 17, 64], 0.2, "proc"),
+    ("config3-like", [2000] * 24, 0.02, "proc"),
+    ("lds-edge", [2700, 2731, 2184, 1820], 0.05, "proc"),  # 4096-bucket LDS path boundary
+    ("big-nodes", [10000, 50000, 3, 0, 12000], 0.03, "proc"),  # global-table path
+    ("container-ids", [250, 180, 0, 520], 0.1, "ctr"),
+]
+
+
+@pytest.mark.parametrize("name,sizes,churn,kind", JOIN_FLEETS, ids=[f[0] for f in JOIN_FLEETS])
+def test_join_bit_exact(name, sizes, churn, kind):
+    row_off = np.r_[0, np.cumsum(sizes)].astype(np.uint32)
+    slot_off = np.r_[0, np.cumsum([int(s * 1.2) + 4 for s in sizes])].astype(np.uint32)
+    acc = accel.Accel(1, **caps_for(slot_off))
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC if kind == "proc" else accel.KACC_KIND_CTR, slot_off)
+    ora = OracleSlotMap(slot_off)
+    sim = fleet.KeyedChurn(row_off, seed=7, churn=churn, kind=kind)
+    rng = np.random.default_rng(2)
+    for it in range(5):
+        keys = sim.next_keys()
+        status = None
+        if it >= 2:
+            status = np.where(rng.random(len(sizes)) < 0.2, accel.KACC_NODE_READ_ERROR, 0).astype(np.uint32)
+        rc, want, tk, ts = ora.join(row_off, keys, status)
+        assert rc == 0
+        got, term = gpu.join(row_off, keys, status)
+        if status is not None:  # rows of skipped nodes are not produced by either side
+            keep = np.repeat(status == 0, np.diff(row_off.astype(np.int64)))
+            got, want = got[keep], want[keep]
+        np.testing.assert_array_equal(got, want, err_msg=f"interval {it}")
+        assert term == sorted(zip(tk.tolist(), ts.tolist())), f"interval {it}"
+
+
+def test_join_errors_raise_erange():
+    slot_off = np.array([0, 8, 10], dtype=np.uint32)
+    acc = accel.Accel(1, **caps_for(slot_off))
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, slot_off)
+    row_off = np.array([0, 3, 6], dtype=np.uint32)
+    with pytest.raises(accel.AccelError) as ei:  # duplicate ID in node 0; 4 IDs for 2 slots... in node 1
+        gpu.join(row_off, np.array([5, 5, 6, 1, 2, 3], dtype=np.uint64))
+    assert ei.value.code == accel.KACC_ERANGE
+    gpu.m.reset()
+    with pytest.raises(accel.AccelError):
+        gpu.join(row_off, np.array([1, accel.KACC_KEY_EMPTY, 2, 1, 2, 3], dtype=np.uint64))
+    gpu.m.reset()  # and a valid batch afterwards
+    got, term = gpu.join(np.array([0, 3, 5], dtype=np.uint32), np.array([1, 2, 3, 7, 8], dtype=np.uint64))
+    np.testing.assert_array_equal(got & 0x7FFFFFFF, [0, 1, 2, 8, 9])
+    assert term == []
+
+
+def test_join_feeds_interval_bit_exact():
+    """Keyed fleet: device join -> interval kernel == oracle join -> oracle interval."""
+    layout = fleet.make_layout(12, [1500, 2000, 40, 0, 700, 2048] * 2, 4, seed=21)
+    sizes = layout.sizes()
+    P = layout.n_procs
+    proc_slot_off = np.r_[0, np.cumsum(np.diff(layout.proc_off.astype(np.int64)) * 5 // 4 + 8)].astype(np.uint32)
+    caps = layout.capacities()
+    caps["proc_slots"] = int(proc_slot_off[-1])
+    acc = accel.Accel(layout.zones, **caps)
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, proc_slot_off)
+    ojoin = OracleSlotMap(proc_slot_off)
+    ora = Oracle(layout.zones, **caps)
+    sim = fleet.FleetSim(layout, seed=21, churn=0.0, read_error_frac=0.1)
+    keys_sim = fleet.KeyedChurn(layout.proc_off, seed=21, churn=0.04)
+    stream = current_stream_handle()
+    for it in range(4):
+        a = sim.next_interval()
+        keys = keys_sim.next_keys()
+        # CPU deltas restart for new IDs (informer.go:518: prevTotal 0 for a new PID)
+        _, want_slots, _, _ = ojoin.join(layout.proc_off, keys, a["node_status"])
+        a_ora = dict(a)
+        a_ora["proc_slot"] = want_slots
+        t = to_device(a)
+        out = t["proc_slot"]  # the join writes the batch's slot words in place
+        gpu.join(layout.proc_off, keys, a["node_status"], out=out, sync=False)
+        acc.run_interval(interval_from_tensors(t, sizes, layout.fast_flag()), stream)
+        acc.sync(stream)
+        ora.interval(a_ora, sizes)
+        for name, _ in accel.TABLES:
+            np.testing.assert_array_equal(acc.download(name), ora.state[name], err_msg=f"interval {it} {name}")
+    assert P > 0
