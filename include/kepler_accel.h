@@ -245,32 +245,36 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *ns_pod_o
  *
  * One slot map per workload kind.  Node n owns the slot range
  * [slot_off[n], slot_off[n+1]) of that kind's state tables and a private
- * device hash table (load <= 1/2) of its live IDs.  kacc_slot_join() takes
+ * device hash table (load <= 2/3) of its live IDs.  kacc_slot_join() takes
  * the IDs of the node's rows in batch order and, per node:
  *   - a live ID keeps its slot (slot word without KACC_SLOT_NEW);
  *   - an ID that was not live at the node's previous processed interval gets
  *     the lowest slot of its range that was free at the start of this call,
  *     new rows taking slots in row order (KACC_SLOT_NEW set) — deterministic;
- *   - an ID live before but absent now is terminated: (key, slot) is appended
- *     to the term_* list (node segments in any order) and its slot is NOT
+ *   - an ID live before but absent now is terminated: (key, slot) goes to the
+ *     node's segment of the term_* arrays, in slot order, and its slot is NOT
  *     reused before the next call, so the tracker can still read its final
  *     values (the reference reads them from prev, process.go:90-99);
  *   - a node with KACC_NODE_READ_ERROR is skipped (map unchanged), as the
  *     reference skips Refresh when calculateNodePower fails (monitor.go:399-410).
- * Errors (duplicate ID in a node, KACC_KEY_EMPTY, more live IDs than the
- * node's range, term list overflow) are raised as KACC_ERANGE at kacc_sync;
- * the affected rows get slot word 0xffffffff.                                */
+ * Keys: KACC_KIND_PROC takes uint32_t PIDs (resource.Process.PID, a Linux
+ * pid <= pid_max = 2^22; 0xfffffffe/0xffffffff reserved); the other kinds take
+ * uint64_t IDs (the packer's 64-bit IDs of the container / VM / pod ID
+ * strings; the two top values reserved).  Errors (duplicate ID in a node, a
+ * reserved key, more live IDs than the node's range) are raised as
+ * KACC_ERANGE at kacc_sync; the affected rows get slot word 0xffffffff.      */
 typedef enum kacc_kind {
-  KACC_KIND_PROC = 0, /* key: PID (pid_t) — process.go:120 StringID */
-  KACC_KIND_CTR = 1,  /* key: 64-bit ID of the container ID string   */
-  KACC_KIND_VM = 2,   /* key: 64-bit ID of the VM ID string          */
-  KACC_KIND_POD = 3   /* key: 64-bit ID of the pod UID               */
+  KACC_KIND_PROC = 0, /* key: uint32_t PID — process.go:120 StringID        */
+  KACC_KIND_CTR = 1,  /* key: uint64_t ID of the container ID string        */
+  KACC_KIND_VM = 2,   /* key: uint64_t ID of the VM ID string               */
+  KACC_KIND_POD = 3   /* key: uint64_t ID of the pod UID                    */
 } kacc_kind;
-#define KACC_KEY_EMPTY 0xffffffffffffffffull /* reserved, never a valid key */
+#define KACC_KEY_EMPTY 0xffffffffffffffffull /* reserved (u32 keys: 0xffffffff) */
+#define KACC_KEY_TOMB 0xfffffffffffffffeull  /* reserved (u32 keys: 0xfffffffe) */
 
 typedef struct kacc_slotmap kacc_slotmap;
 /* slot_off: HOST [n_nodes + 1], monotonic, slot_off[n_nodes] <= the kind's
- * slot capacity in kacc_config.  The map starts empty.                       */
+ * slot capacity in kacc_config, each range <= 131072 slots.  Starts empty.   */
 int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const uint32_t *slot_off,
                         kacc_slotmap **out);
 void kacc_slotmap_destroy(kacc_slotmap *m);
@@ -278,12 +282,15 @@ int kacc_slotmap_reset(kacc_slotmap *m); /* forget every ID (PowerMonitor restar
 /* Device pointers, asynchronous on `stream` (NULL = the context's stream).
  * n_rows = row_off[n_nodes] (the batch's n_procs / n_ctrs / n_vms / n_pods);
  * row_off [n_nodes+1]: the batch's proc_off / ctr_off / vm_off / pod_off;
- * keys [n_rows]; node_status [n_nodes] or NULL; out_slot [n_rows] (may be the
- * batch's *_slot array); term_key/term_slot [term_cap]; *term_count is set to
- * the number of terminated IDs (entries past term_cap are dropped + ERANGE).  */
-int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
+ * keys [n_rows] (uint32_t for KACC_KIND_PROC, else uint64_t); node_status
+ * [n_nodes] or NULL; out_slot [n_rows] (may be the batch's *_slot array).
+ * Terminated IDs, per node: term_count[n] of them, at positions
+ * [slot_off[n], slot_off[n] + term_count[n]) of term_key (uint64_t) and
+ * term_slot (both sized slot_off[n_nodes]), ascending by slot.  term_count of
+ * a skipped node is set to 0.                                                */
+int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                   uint32_t *term_slot, uint32_t *term_count, uint32_t term_cap, void *stream);
+                   uint32_t *term_slot, uint32_t *term_count, void *stream);
 
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */

@@ -223,7 +223,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_slotmap_destroy.restype = None
     lib.kacc_slotmap_reset.argtypes = [c_void_p]
     lib.kacc_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]
+                                   c_void_p, c_void_p, c_void_p, c_void_p]
     if lib.kacc_abi_version() != KACC_ABI_VERSION:
         raise ImportError("libkepler_accel ABI version mismatch")
     _lib = lib
@@ -372,11 +372,12 @@ class SlotMap:
         self.accel._check(self.lib.kacc_slotmap_reset(self.handle))
 
     def join(self, n_rows: int, row_off_ptr: int, keys_ptr: int, node_status_ptr: int, out_slot_ptr: int,
-             term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, term_cap: int, stream: int = 0) -> None:
+             term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, stream: int = 0) -> None:
+        """term_key / term_slot: [slot_off[-1]], term_count: [n_nodes] (per-node segments)."""
         self.accel._check(self.lib.kacc_slot_join(
             self.handle, n_rows, c_void_p(row_off_ptr), c_void_p(keys_ptr or None),
-            c_void_p(node_status_ptr or None), c_void_p(out_slot_ptr), c_void_p(term_key_ptr or None),
-            c_void_p(term_slot_ptr or None), c_void_p(term_count_ptr), term_cap, c_void_p(stream or None)))
+            c_void_p(node_status_ptr or None), c_void_p(out_slot_ptr), c_void_p(term_key_ptr),
+            c_void_p(term_slot_ptr), c_void_p(term_count_ptr), c_void_p(stream or None)))
 
     def close(self) -> None:
         if self.handle:

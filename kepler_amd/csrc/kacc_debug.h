@@ -12,6 +12,12 @@ extern "C" {
  * 9 = 1|8.  Variants != 0 do not compute the reference semantics.          */
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream, int variant);
 
+/* Slot join timing ablation: stop_after = k returns after phase k (1 load,
+ * 2 lookups, 3 terminated, 4 allocation, 5 inserts); 0 = the full join.    */
+int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
+                            uint32_t *out_slot, uint64_t *term_key, uint32_t *term_slot,
+                            uint32_t *term_count, void *stream, uint32_t stop_after);
+
 #ifdef __cplusplus
 }
 #endif

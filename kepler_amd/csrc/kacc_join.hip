@@ -7,49 +7,58 @@
 // 236-246, 260-270, 311-322); terminated workloads found in the previous
 // snapshot go to the terminated trackers (process.go:87-99).  Here a fleet
 // interval does both for every node in one launch: one workgroup per node,
-// the node's live-ID hash table (key u64 -> node-relative slot) rebuilt from
-// the current rows every interval (no tombstones), ping-ponged between two
-// device buffers.  A node whose table fits 4096 buckets (<= 2730 slots) works
-// on an LDS copy; bigger nodes work on the global table directly.
+// over the node's private open-addressing table of live IDs (key -> node-
+// relative slot, linear probing, load <= 2/3), updated in place: terminated
+// IDs become tombstones, new IDs claim empty or tombstone buckets, and only
+// the buckets that changed are written back.  When live + tombstones pass
+// 3/4 of the table it is rebuilt from the current rows.  PIDs are u32 keys
+// packed with their slot in one 8-B bucket; 64-bit IDs use a key array and a
+// slot array.  A node whose table has <= 4096 buckets (<= 2730 slots) works on
+// an LDS copy with its rows' keys in registers; bigger nodes work on the
+// global table.
 //
 // Per node, in order:
-//   1  mark the slots held by the previous table (used bitmap, LDS)
-//   2  look every row's key up: found -> its slot, bucket marked seen
-//   3  unseen buckets = terminated IDs -> (key, slot) list
-//   4  rows not found take the lowest free slots in row order (block scan)
-//   5  the new table = exactly the current rows, written to the other buffer
-// Slots of terminated IDs are marked used in step 1, so they are not handed
-// out before the next interval: the tracker still reads their final values.
+//   1  load the table (LDS) and the rows' keys
+//   2  used-slot bitmap of the live IDs; look every row up (seen-slot bitmap)
+//   3  live IDs whose slot was not seen = terminated: the node's segment of
+//      the (key, slot) list in slot order (bitmap prefix, no global atomic),
+//      bucket -> tombstone
+//   4  rows not found take the lowest slots free at step 2, in row order
+//   5  new IDs claim buckets; a re-probe flags an ID given twice in a node
+//   6  write back the changed buckets (or rebuild the table)
+// Terminated slots are in the step-2 bitmap, so they are not handed out
+// before the next interval: the tracker still reads their final values.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
 #include <vector>
 
+#include "kacc_debug.h"
 #include "kacc_internal.hpp"
 
 namespace kacc {
 namespace join {
 
 constexpr int kThreads = 512;
-constexpr uint32_t kLdsBuckets = 4096;        // small-node table in LDS
-constexpr uint32_t kMaxRange = 131072;        // slots per node (bitmap words in LDS)
-constexpr uint32_t kWords = kMaxRange / 32;   // big-node bitmap words
+constexpr uint32_t kLdsBuckets = 4096;           // small-node table in LDS
+constexpr int kRpl = 6;                          // small-node rows per lane (contiguous)
+constexpr uint32_t kSmallRows = kRpl * kThreads;
+constexpr uint32_t kMaxRange = 131072;           // slots per node
+constexpr uint32_t kWords = kMaxRange / 32;      // big-node slot bitmap words
 constexpr uint32_t kSmallWords = (kLdsBuckets * 2 / 3 + 31) / 32 + 1;
-constexpr uint32_t kSeen = 0x80000000u;       // bucket slot field: matched this interval
-constexpr uint16_t kSeen16 = 0x8000u;
-constexpr uint32_t kInvalid = 0xffffffffu;    // slot word of a row in error
-constexpr uint32_t kPending = 0xfffffffeu;    // row not found yet (step 2 -> 4)
+constexpr uint32_t kInvalid = 0xffffffffu;       // slot word of a row in error
+constexpr uint32_t kPending = 0xfffffffeu;       // row not found (step 2 -> 4)
 
 constexpr uint32_t kErrOffsets = 1u << 1;
-constexpr uint32_t kErrKey = 1u << 6;       // KACC_KEY_EMPTY or duplicate ID in a node
-constexpr uint32_t kErrRange = 1u << 7;     // more live IDs than the node's slot range
-constexpr uint32_t kErrTermCap = 1u << 8;   // terminated list overflow
+constexpr uint32_t kErrKey = 1u << 6;      // reserved key or an ID given twice in a node
+constexpr uint32_t kErrRange = 1u << 7;    // more live IDs than the node's slot range
 
 struct Args {
-  uint32_t n_nodes, n_rows, term_cap, pad;
+  uint32_t n_nodes, n_rows;
+  uint32_t stop_after;  // timing ablation (kacc_debug_join_variant): 0 = full join
   const uint32_t *row_off;
-  const uint64_t *keys;
+  const void *keys;
   const uint32_t *node_status;
   uint32_t *out_slot;
   uint64_t *term_key;
@@ -57,22 +66,96 @@ struct Args {
   uint32_t *term_count;
   const uint32_t *slot_off;  // [N+1]
   const uint64_t *hoff;      // [N+1] bucket offsets (each node a power of two)
-  uint64_t *hkeys[2];
-  uint32_t *hslots[2];
-  uint8_t *parity;           // [N] which buffer holds the node's live table
+  uint64_t *ent;             // u32 keys: packed (key << 32 | slot); u64 keys: the keys
+  uint32_t *slots;           // u64 keys: the slots
   uint32_t *err;
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finalizer
-  x ^= x >> 30;
-  x *= 0xbf58476d1ce4e5b9ull;
-  x ^= x >> 27;
-  x *= 0x94d049bb133111ebull;
-  x ^= x >> 31;
-  return x;
+// Fibonacci hashing: the top log2(H) bits of fold(k) * 2^32/phi (PIDs are
+// near-sequential; 64-bit IDs are already hashed by the packer).
+template <typename K>
+__device__ __forceinline__ uint32_t bucket(K k, uint32_t shift) {
+  uint32_t x = static_cast<uint32_t>(k);
+  if constexpr (sizeof(K) == 8) x ^= static_cast<uint32_t>(static_cast<uint64_t>(k) >> 32);
+  return (x * 0x9E3779B1u) >> shift;
 }
 
-// Exclusive block-wide scan of v (512 threads = 8 waves); *total = sum.
+// Bucket views over generic (LDS or global) pointers.  raw(b) is the word a
+// claim compares: the packed entry (u32 keys) or the key (u64 keys).
+template <typename K>
+struct Tab;
+template <>
+struct Tab<uint32_t> {
+  static constexpr uint32_t kEmpty = 0xffffffffu, kTomb = 0xfffffffeu;
+  uint64_t *e;
+  __device__ uint64_t raw(uint32_t b) const { return e[b]; }
+  __device__ static uint32_t key_of(uint64_t r) { return static_cast<uint32_t>(r >> 32); }
+  __device__ uint32_t key(uint32_t b) const { return key_of(e[b]); }
+  __device__ uint32_t slot(uint32_t b) const { return static_cast<uint32_t>(e[b]); }
+  __device__ void tomb(uint32_t b) const { e[b] = static_cast<uint64_t>(kTomb) << 32; }
+  __device__ bool claim(uint32_t b, uint64_t seen, uint32_t k, uint32_t s) const {
+    const unsigned long long v = (static_cast<unsigned long long>(k) << 32) | s;
+    return atomicCAS(reinterpret_cast<unsigned long long *>(e + b), seen, v) == seen;
+  }
+  __device__ void clear(uint32_t b) const { e[b] = ~0ull; }
+};
+template <>
+struct Tab<uint64_t> {
+  static constexpr uint64_t kEmpty = ~0ull, kTomb = ~0ull - 1;
+  uint64_t *k;
+  uint32_t *s;
+  __device__ uint64_t raw(uint32_t b) const { return k[b]; }
+  __device__ static uint64_t key_of(uint64_t r) { return r; }
+  __device__ uint64_t key(uint32_t b) const { return k[b]; }
+  __device__ uint32_t slot(uint32_t b) const { return s[b]; }
+  __device__ void tomb(uint32_t b) const { k[b] = kTomb; }
+  __device__ bool claim(uint32_t b, uint64_t seen, uint64_t kk, uint32_t ss) const {
+    if (atomicCAS(reinterpret_cast<unsigned long long *>(k + b), seen, kk) != seen) return false;
+    s[b] = ss;
+    return true;
+  }
+  __device__ void clear(uint32_t b) const { k[b] = kEmpty; }
+};
+
+template <typename K>
+__device__ __forceinline__ bool is_live(uint64_t raw) {
+  const auto k = Tab<K>::key_of(raw);
+  return k != Tab<K>::kEmpty && k != Tab<K>::kTomb;
+}
+
+// Linear-probing operations shared by both kernels (hmask = H - 1).
+template <typename K>
+struct Probe {
+  Tab<K> t;
+  uint32_t shift, hmask, H;
+  // bucket holding k, or ~0u (stops at the first empty bucket, skips tombstones)
+  __device__ uint32_t find(K k) const {
+    uint32_t b = bucket(k, shift);
+    for (uint32_t p = 0; p < H; ++p, b = (b + 1) & hmask) {
+      const K kk = static_cast<K>(t.key(b));
+      if (kk == k) return b;
+      if (kk == Tab<K>::kEmpty) break;
+    }
+    return ~0u;
+  }
+  // claim the first empty or tombstone bucket on k's path; returns it (or ~0u)
+  __device__ uint32_t insert(K k, uint32_t rel) const {
+    uint32_t b = bucket(k, shift);
+    for (uint32_t p = 0; p < H;) {
+      const uint64_t raw = t.raw(b);
+      const K kk = static_cast<K>(Tab<K>::key_of(raw));
+      if (kk == Tab<K>::kEmpty || kk == Tab<K>::kTomb) {
+        if (t.claim(b, raw, k, rel)) return b;
+        continue;  // lost the race for this bucket: look at it again
+      }
+      ++p;
+      b = (b + 1) & hmask;
+    }
+    return ~0u;
+  }
+};
+
+// Exclusive block-wide scan of v (512 threads = 8 waves); total = sum.
 __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *s_wave, uint32_t &total) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t x = v;
@@ -95,124 +178,423 @@ __device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *s_wave, uin
   return base + x - v;
 }
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
 // Position of the j-th (0-based) set bit of w (w has more than j set bits).
 __device__ __forceinline__ uint32_t select_bit(uint32_t w, uint32_t j) {
   for (uint32_t i = 0; i < j; ++i) w &= w - 1;
   return static_cast<uint32_t>(__builtin_ctz(w));
 }
 
+// Node geometry shared by both kernels; false when this kernel skips the node.
+struct NodeView {
+  uint64_t hb;
+  uint32_t H, S, s0, r0, r1, shift;
+};
 template <bool kSmall>
-__global__ __launch_bounds__(kThreads) void join_kernel(const Args a) {
-  __shared__ uint64_t s_keys[kSmall ? kLdsBuckets : 1];
-  __shared__ uint16_t s_slots[kSmall ? kLdsBuckets : 1];
-  __shared__ uint32_t s_used[kSmall ? kSmallWords : kWords];  // used-slot bitmap
-  __shared__ uint32_t s_wpre[kSmall ? kSmallWords : kWords];  // free slots before word w
-  __shared__ uint32_t s_wave[kThreads / 64];
-  __shared__ uint32_t s_cnt, s_cnt2, s_base;
-
-  const uint32_t n = blockIdx.x;
-  const int tid = threadIdx.x;
-  if (n >= a.n_nodes) return;
-  if (a.node_status && (a.node_status[n] & KACC_NODE_READ_ERROR)) return;  // map unchanged
-  const uint64_t hb = a.hoff[n];
-  const uint32_t H = static_cast<uint32_t>(a.hoff[n + 1] - hb);
-  if ((H <= kLdsBuckets) != kSmall) return;  // the other instance handles this node
-  const uint32_t s0 = a.slot_off[n];
-  const uint32_t S = a.slot_off[n + 1] - s0;
-  uint32_t r0 = a.row_off[n], r1 = a.row_off[n + 1];
-  if (r1 > a.n_rows || r0 > r1) {
-    if (tid == 0) atomicOr(a.err, kErrOffsets);
-    r1 = min(r1, a.n_rows);
-    r0 = min(r0, r1);
+__device__ __forceinline__ bool node_view(const Args &a, uint32_t n, NodeView &v) {
+  if (a.node_status && (a.node_status[n] & KACC_NODE_READ_ERROR)) {  // map unchanged
+    if (kSmall && threadIdx.x == 0) a.term_count[n] = 0u;
+    return false;
   }
-  const uint32_t par = a.parity[n] & 1u;
-  uint64_t *__restrict__ Ak = a.hkeys[par] + hb;
-  uint32_t *__restrict__ As = a.hslots[par] + hb;
-  uint64_t *__restrict__ Bk = a.hkeys[par ^ 1u] + hb;
-  uint32_t *__restrict__ Bs = a.hslots[par ^ 1u] + hb;
-  const uint32_t W = (S + 31) / 32;
-  const uint32_t hmask = H - 1;
+  v.hb = a.hoff[n];
+  v.H = static_cast<uint32_t>(a.hoff[n + 1] - v.hb);
+  v.r0 = a.row_off[n];
+  v.r1 = a.row_off[n + 1];
+  if (v.r1 > a.n_rows || v.r0 > v.r1) {
+    if (kSmall && threadIdx.x == 0) atomicOr(a.err, kErrOffsets);
+    v.r1 = min(v.r1, a.n_rows);
+    v.r0 = min(v.r0, v.r1);
+  }
+  if ((v.H <= kLdsBuckets && v.r1 - v.r0 <= kSmallRows) != kSmall) return false;
+  v.s0 = a.slot_off[n];
+  v.S = a.slot_off[n + 1] - v.s0;
+  v.shift = 32u - static_cast<uint32_t>(__builtin_ctz(v.H));
+  return true;
+}
 
-  // ---- 1: previous table (LDS copy for small nodes), used bitmap -------------
-  for (uint32_t w = tid; w < W; w += kThreads) s_used[w] = 0u;
-  if constexpr (kSmall) {
-    for (uint32_t b = tid; b < H; b += kThreads) {
-      s_keys[b] = Ak[b];
-      s_slots[b] = static_cast<uint16_t>(As[b]);
+// ============================ small nodes (LDS) ====================================
+// Table in LDS, rows' keys / slot words in registers (lane owns kRpl
+// consecutive rows), per-slot marks in LDS written with plain stores:
+// s_used[s] (slot held at the start), s_seen[s] = 1 + the row that found s
+// (a second finder of the same ID sees another row there: duplicate).
+constexpr uint32_t kSmallSlots = kSmallWords * 32;
+constexpr uint32_t kNewCap = 512;  // new rows handled as a compact list
+
+template <typename K>
+__global__ __launch_bounds__(kThreads) void join_small(const Args a) {
+  using T = Tab<K>;
+  constexpr bool kWide = sizeof(K) == 8;
+  __shared__ uint64_t s_ent[kLdsBuckets];              // entries (u32 keys) / keys (u64)
+  __shared__ uint32_t s_slot[kWide ? kLdsBuckets : 1];  // slots (u64 keys)
+  __shared__ __attribute__((aligned(16))) uint8_t s_used[kSmallSlots];
+  __shared__ __attribute__((aligned(16))) uint16_t s_seen[kSmallSlots];
+  __shared__ uint32_t s_fmask[kSmallWords], s_tmask[kSmallWords];  // free / terminated bits
+  __shared__ uint32_t s_wpre[kSmallWords];                          // (free << 16 | term) before w
+  __shared__ uint16_t s_free[kNewCap];                              // the first free slots
+  __shared__ K s_newkey[kNewCap];
+  __shared__ uint8_t s_newbad[kNewCap];
+  __shared__ uint32_t s_dirty[kLdsBuckets / 32];
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint32_t s_occ;
+
+  const uint32_t n = blockIdx.x, tid = threadIdx.x;
+  if (n >= a.n_nodes) return;
+  NodeView v;
+  if (!node_view<true>(a, n, v)) return;
+  const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H;
+  const uint32_t W = (S + 31) / 32;
+  const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
+  T G, L;
+  if constexpr (kWide) {
+    G.k = a.ent + v.hb;
+    G.s = a.slots + v.hb;
+    L.k = s_ent;
+    L.s = s_slot;
+  } else {
+    G.e = a.ent + v.hb;
+    L.e = s_ent;
+  }
+  auto lslot = [&](uint32_t b) -> uint32_t { return L.slot(b); };
+  const Probe<K> pr{L, v.shift, H - 1, H};
+
+  // ---- 1: table -> LDS, keys -> registers, marks cleared ---------------------------
+  for (uint32_t b = tid; b < H; b += kThreads) {
+    if constexpr (kWide) {
+      s_ent[b] = G.k[b];
+      s_slot[b] = G.s[b];
+    } else {
+      s_ent[b] = G.e[b];
     }
   }
-  if (tid == 0) {
-    s_cnt = 0u;
-    s_cnt2 = 0u;
+  for (uint32_t i = tid; i < W * 32; i += kThreads) {
+    s_used[i] = 0;
+    s_seen[i] = 0;
+  }
+  for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
+  if (tid == 0) s_occ = 0u;
+  K key[kRpl];
+  uint32_t res[kRpl];
+#pragma unroll
+  for (int j = 0; j < kRpl; ++j) {
+    const uint32_t r = tid * kRpl + j;
+    key[j] = r < R ? keys[r] : T::kEmpty;
   }
   __syncthreads();
-  auto tkey = [&](uint32_t b) -> uint64_t {
-    if constexpr (kSmall) return s_keys[b];
-    else return Ak[b];
-  };
-  auto tslot = [&](uint32_t b) -> uint32_t {  // node-relative slot, seen bit stripped
-    if constexpr (kSmall) return s_slots[b] & ~kSeen16;
-    else return As[b] & ~kSeen;
-  };
+
+  // ---- 2: held slots; lookups --------------------------------------------------------
   for (uint32_t b = tid; b < H; b += kThreads) {
-    if (tkey(b) == KACC_KEY_EMPTY) continue;
-    const uint32_t s = tslot(b);
+    if (!is_live<K>(L.raw(b))) continue;
+    const uint32_t sl = lslot(b);
+    if (sl < S) s_used[sl] = 1;
+  }
+#pragma unroll
+  for (int j = 0; j < kRpl; ++j) {
+    const uint32_t r = tid * kRpl + j;
+    res[j] = kInvalid;
+    if (r >= R) continue;
+    const K k = key[j];
+    if (k == T::kEmpty || k == T::kTomb) {
+      atomicOr(a.err, kErrKey);
+      continue;
+    }
+    const uint32_t b = pr.find(k);
+    if (b == ~0u) {
+      res[j] = kPending;
+      continue;
+    }
+    const uint32_t sl = lslot(b);
+    if (sl >= S) continue;
+    s_seen[sl] = static_cast<uint16_t>(r + 1);
+    res[j] = s0 + sl;
+  }
+  __syncthreads();
+  uint32_t mine = 0;  // new rows of this lane
+#pragma unroll
+  for (int j = 0; j < kRpl; ++j) {
+    const uint32_t r = tid * kRpl + j;
+    if (res[j] == kPending) {
+      ++mine;
+    } else if (res[j] != kInvalid && s_seen[res[j] - s0] != r + 1) {  // ID on two rows
+      atomicOr(a.err, kErrKey);
+      res[j] = kInvalid;
+    }
+  }
+
+  // ---- 3: per-word free / terminated bits and their prefixes -------------------------
+  uint32_t packed = 0;
+  if (tid < W) {
+    uint32_t used = 0, seen = 0;
+    const uint32_t *u4 = reinterpret_cast<const uint32_t *>(s_used + tid * 32);
+    const uint2 *s4 = reinterpret_cast<const uint2 *>(s_seen + tid * 32);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // slots 4q .. 4q+3 of the word
+      const uint32_t x = u4[q];
+      const uint2 y = s4[q];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) used |= ((x >> (8 * i)) & 1u) << (4 * q + i);
+      seen |= (((y.x & 0xffffu) != 0) ? 1u : 0u) << (4 * q);
+      seen |= (((y.x >> 16) != 0) ? 1u : 0u) << (4 * q + 1);
+      seen |= (((y.y & 0xffffu) != 0) ? 1u : 0u) << (4 * q + 2);
+      seen |= (((y.y >> 16) != 0) ? 1u : 0u) << (4 * q + 3);
+    }
+    const uint32_t valid = (tid + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
+    const uint32_t fm = ~used & valid, tm = used & ~seen & valid;
+    s_fmask[tid] = fm;
+    s_tmask[tid] = tm;
+    packed = (static_cast<uint32_t>(__popc(fm)) << 16) | static_cast<uint32_t>(__popc(tm));
+  }
+  uint32_t ptot, ntot;
+  const uint32_t pex = block_scan(packed, s_wave, ptot);
+  const uint32_t rank0 = block_scan(mine, s_wave, ntot);  // this lane's first new-row rank
+  if (tid < W) s_wpre[tid] = pex;
+  const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot;
+  if (tid == 0) a.term_count[n] = n_term;
+  __syncthreads();
+
+  // ---- 4: terminated list (slot order) + tombstones; the first free slots ------------
+  if (n_term) {
+    for (uint32_t b = tid; b < H; b += kThreads) {
+      if (!is_live<K>(L.raw(b))) continue;
+      const uint32_t sl = lslot(b);
+      if (sl >= S) continue;
+      const uint32_t w = sl >> 5, bit = 1u << (sl & 31);
+      const uint32_t tm = s_tmask[w];
+      if (!(tm & bit)) continue;
+      const uint32_t pos = s0 + (s_wpre[w] & 0xffffu) + __popc(tm & (bit - 1u));
+      a.term_key[pos] = static_cast<uint64_t>(L.key(b));
+      a.term_slot[pos] = s0 + sl;
+      L.tomb(b);
+      atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+    }
+  }
+  const uint32_t want = min(min(n_new, total_free), kNewCap);
+  if (tid < W) {
+    uint32_t p = s_wpre[tid] >> 16;
+    for (uint32_t fm = s_fmask[tid]; fm && p < want; fm &= fm - 1, ++p)
+      s_free[p] = static_cast<uint16_t>(tid * 32 + __builtin_ctz(fm));
+  }
+  __syncthreads();
+
+  // ---- 5: new rows take slots in row order ------------------------------------------
+  auto take_slow = [&](uint32_t q) -> uint32_t {  // q-th free slot, q >= kNewCap
+    uint32_t lo = 0, hi = W;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if ((s_wpre[mid] >> 16) <= q) lo = mid; else hi = mid;
+    }
+    return lo * 32 + select_bit(s_fmask[lo], q - (s_wpre[lo] >> 16));
+  };
+  const bool compact = n_new <= kNewCap;
+  uint32_t q = rank0;
+  uint32_t rk[kRpl];
+#pragma unroll
+  for (int j = 0; j < kRpl; ++j) {
+    rk[j] = ~0u;
+    if (res[j] != kPending) continue;
+    if (q >= total_free) {
+      atomicOr(a.err, kErrRange);
+      res[j] = kInvalid;
+      ++q;
+      continue;
+    }
+    const uint32_t sl = q < kNewCap ? s_free[q] : take_slow(q);
+    res[j] = (s0 + sl) | KACC_SLOT_NEW;
+    rk[j] = q;
+    if (compact) {
+      s_newkey[q] = key[j];
+      s_newbad[q] = 0;
+    }
+    ++q;
+  }
+  __syncthreads();
+
+  // ---- 6: inserts (one lane per new row), then a re-probe flags an ID twice ---------
+  const uint32_t n_ins = min(n_new, total_free);
+  if (compact) {
+    for (uint32_t i = tid; i < n_ins; i += kThreads) {
+      const uint32_t b = pr.insert(s_newkey[i], s_free[i]);
+      if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n_ins; i += kThreads) {
+      const uint32_t b = pr.find(s_newkey[i]);
+      if (b == ~0u || lslot(b) != s_free[i]) s_newbad[i] = 1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j)
+      if (rk[j] != ~0u && s_newbad[rk[j]]) {
+        atomicOr(a.err, kErrKey);
+        res[j] = kInvalid;
+      }
+  } else {  // first interval / mass churn: each lane inserts its own rows
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j) {
+      if (rk[j] == ~0u) continue;
+      const uint32_t b = pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0);
+      if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j) {
+      if (rk[j] == ~0u) continue;
+      const uint32_t b = pr.find(key[j]);
+      if (b == ~0u || lslot(b) != (res[j] & KACC_SLOT_MASK) - s0) {
+        atomicOr(a.err, kErrKey);
+        res[j] = kInvalid;
+      }
+    }
+  }
+
+  // ---- 7: occupancy; write back the changed buckets (or rebuild); slot words --------
+  {
+    uint32_t occ = 0;
+    for (uint32_t b = tid; b < H; b += kThreads) occ += L.key(b) != T::kEmpty ? 1u : 0u;
+    occ = wave_sum(occ);
+    if ((tid & 63) == 0) atomicAdd(&s_occ, occ);
+  }
+  __syncthreads();
+  const bool rebuild = s_occ * 4 > H * 3;  // tombstones crowd the table
+  if (rebuild) {
+    for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j) {
+      if (res[j] != kInvalid) pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0);
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < H; b += kThreads) {
+      if constexpr (kWide) {
+        G.k[b] = s_ent[b];
+        G.s[b] = s_slot[b];
+      } else {
+        G.e[b] = s_ent[b];
+      }
+    }
+  } else {
+    for (uint32_t w = tid; w < H / 32; w += kThreads) {
+      for (uint32_t d = s_dirty[w]; d; d &= d - 1) {
+        const uint32_t b = w * 32 + __builtin_ctz(d);
+        if constexpr (kWide) {
+          G.k[b] = s_ent[b];
+          G.s[b] = s_slot[b];
+        } else {
+          G.e[b] = s_ent[b];
+        }
+      }
+    }
+  }
+  uint32_t *__restrict__ out = a.out_slot + v.r0;
+#pragma unroll
+  for (int j = 0; j < kRpl; ++j)
+    if (tid * kRpl + j < R) out[tid * kRpl + j] = res[j];
+}
+
+// ============================ big nodes (global table) =============================
+// Same steps on the node's table in global memory; per-slot bitmaps in LDS
+// (slot ranges up to kMaxRange); rows processed in chunks of kThreads.
+template <typename K>
+__global__ __launch_bounds__(kThreads) void join_big(const Args a) {
+  using T = Tab<K>;
+  __shared__ uint32_t s_used[kWords];  // slots held by live IDs
+  __shared__ uint32_t s_seen[kWords];  // slots of rows found
+  __shared__ uint32_t s_wpre[kWords];  // free slots before word w
+  __shared__ uint32_t s_tpre[kWords];  // terminated before word w
+  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint32_t s_occ;
+
+  const uint32_t n = blockIdx.x, tid = threadIdx.x;
+  if (n >= a.n_nodes) return;
+  NodeView v;
+  if (!node_view<false>(a, n, v)) return;
+  const uint32_t r0 = v.r0, r1 = v.r1, S = v.S, s0 = v.s0, H = v.H;
+  const uint32_t W = (S + 31) / 32;
+  const K *__restrict__ keys = static_cast<const K *>(a.keys);
+  T L;
+  if constexpr (sizeof(K) == 8) {
+    L.k = a.ent + v.hb;
+    L.s = a.slots + v.hb;
+  } else {
+    L.e = a.ent + v.hb;
+  }
+  const Probe<K> pr{L, v.shift, H - 1, H};
+  auto bit_set = [](uint32_t *bm, uint32_t i) {
+    return (atomicOr(&bm[i >> 5], 1u << (i & 31)) >> (i & 31)) & 1u;
+  };
+
+  // ---- 1-2: bitmaps, held slots, lookups ----------------------------------------------
+  for (uint32_t w = tid; w < W; w += kThreads) {
+    s_used[w] = 0u;
+    s_seen[w] = 0u;
+  }
+  if (tid == 0) s_occ = 0u;
+  __syncthreads();
+  if (a.stop_after == 1) return;
+  for (uint32_t b = tid; b < H; b += kThreads) {
+    if (!is_live<K>(L.raw(b))) continue;
+    const uint32_t s = L.slot(b);
     if (s < S) atomicOr(&s_used[s >> 5], 1u << (s & 31));
   }
-  // ---- 2: lookups (a bucket's seen bit has one writer: keys are unique) -------
   for (uint32_t r = r0 + tid; r < r1; r += kThreads) {
-    const uint64_t k = a.keys[r];
+    const K k = keys[r];
     uint32_t out = kPending;
-    if (k == KACC_KEY_EMPTY) {
+    if (k == T::kEmpty || k == T::kTomb) {
       atomicOr(a.err, kErrKey);
       out = kInvalid;
     } else {
-      uint32_t b = static_cast<uint32_t>(mix64(k)) & hmask;
-      for (uint32_t probe = 0; probe < H; ++probe, b = (b + 1) & hmask) {
-        const uint64_t kk = tkey(b);
-        if (kk == KACC_KEY_EMPTY) break;
-        if (kk == k) {
-          uint32_t s;
-          if constexpr (kSmall) {
-            s = s_slots[b] & ~kSeen16;
-            s_slots[b] = static_cast<uint16_t>(s | kSeen16);
-          } else {
-            s = As[b] & ~kSeen;
-            As[b] = s | kSeen;
-          }
-          out = s < S ? s0 + s : kInvalid;
-          break;
+      const uint32_t b = pr.find(k);
+      if (b != ~0u) {
+        const uint32_t s = L.slot(b);
+        if (s >= S) {
+          out = kInvalid;
+        } else if (bit_set(s_seen, s)) {  // the same ID on two rows of the node
+          atomicOr(a.err, kErrKey);
+          out = kInvalid;
+        } else {
+          out = s0 + s;
         }
       }
     }
     a.out_slot[r] = out;
   }
   __syncthreads();
-  // ---- 3: terminated = previous IDs not matched ------------------------------
-  auto terminated = [&](uint32_t b) -> bool {
-    if (tkey(b) == KACC_KEY_EMPTY) return false;
-    if constexpr (kSmall) return (s_slots[b] & kSeen16) == 0;
-    else return (As[b] & kSeen) == 0u;
-  };
-  for (uint32_t b = tid; b < H; b += kThreads)
-    if (terminated(b)) atomicAdd(&s_cnt, 1u);
+  if (a.stop_after == 2) return;
+
+  // ---- 3: terminated = held slots not seen, listed in slot order; tombstones --------
+  uint32_t carry = 0;
+  for (uint32_t w0 = 0; w0 < W; w0 += kThreads) {
+    const uint32_t w = w0 + tid;
+    const uint32_t t = w < W ? __popc(s_used[w] & ~s_seen[w]) : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_scan(t, s_wave, tot);
+    if (w < W) s_tpre[w] = carry + ex;
+    carry += tot;
+  }
+  if (tid == 0) a.term_count[n] = carry;
   __syncthreads();
-  if (tid == 0) s_base = s_cnt ? atomicAdd(a.term_count, s_cnt) : 0u;
-  __syncthreads();
-  if (s_cnt) {
+  if (carry) {
     for (uint32_t b = tid; b < H; b += kThreads) {
-      if (!terminated(b)) continue;
-      const uint32_t i = s_base + atomicAdd(&s_cnt2, 1u);
-      if (i < a.term_cap) {
-        a.term_key[i] = tkey(b);
-        a.term_slot[i] = s0 + tslot(b);
-      } else {
-        atomicOr(a.err, kErrTermCap);
-      }
+      if (!is_live<K>(L.raw(b))) continue;
+      const uint32_t s = L.slot(b);
+      if (s >= S) continue;
+      const uint32_t w = s >> 5, bit = 1u << (s & 31);
+      const uint32_t term = s_used[w] & ~s_seen[w];
+      if (!(term & bit)) continue;
+      const uint32_t pos = s0 + s_tpre[w] + __popc(term & (bit - 1u));
+      a.term_key[pos] = static_cast<uint64_t>(L.key(b));
+      a.term_slot[pos] = s0 + s;
+      L.tomb(b);
     }
   }
-  // ---- 4: free-slot prefix per bitmap word, then new rows in row order --------
-  uint32_t carry = 0;
+  if (a.stop_after == 3) return;
+
+  // ---- 4: free slots (held at step 2), new rows in row order -------------------------
+  carry = 0;
   for (uint32_t w0 = 0; w0 < W; w0 += kThreads) {
     const uint32_t w = w0 + tid;
     uint32_t f = 0;
@@ -227,68 +609,64 @@ __global__ __launch_bounds__(kThreads) void join_kernel(const Args a) {
   }
   const uint32_t total_free = carry;
   __syncthreads();
+  auto take = [&](uint32_t q) -> uint32_t {  // q-th free slot, as a slot word
+    if (q >= total_free) {
+      atomicOr(a.err, kErrRange);
+      return kInvalid;
+    }
+    uint32_t lo = 0, hi = W;  // last word with s_wpre[w] <= q
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) / 2;
+      if (s_wpre[mid] <= q) lo = mid; else hi = mid;
+    }
+    const uint32_t valid = (lo + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
+    return (s0 + lo * 32 + select_bit(~s_used[lo] & valid, q - s_wpre[lo])) | KACC_SLOT_NEW;
+  };
   uint32_t taken = 0;
   for (uint32_t c0 = r0; c0 < r1; c0 += kThreads) {
     const uint32_t r = c0 + tid;
     const bool isnew = r < r1 && a.out_slot[r] == kPending;
     uint32_t tot;
     const uint32_t q = taken + block_scan(isnew ? 1u : 0u, s_wave, tot);
-    if (isnew) {
-      if (q < total_free) {
-        uint32_t lo = 0, hi = W;  // last word with s_wpre[w] <= q
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) / 2;
-          if (s_wpre[mid] <= q) lo = mid; else hi = mid;
-        }
-        const uint32_t valid = (lo + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
-        const uint32_t s = lo * 32 + select_bit(~s_used[lo] & valid, q - s_wpre[lo]);
-        a.out_slot[r] = (s0 + s) | KACC_SLOT_NEW;
-      } else {
-        atomicOr(a.err, kErrRange);
-        a.out_slot[r] = kInvalid;
-      }
-    }
+    if (isnew) a.out_slot[r] = take(q);
     taken += tot;
   }
-  // ---- 5: the new table holds exactly the current rows -----------------------
-  __syncthreads();  // step 3 done reading the previous table (LDS is reused)
-  for (uint32_t b = tid; b < H; b += kThreads) {
-    if constexpr (kSmall) s_keys[b] = KACC_KEY_EMPTY;
-    else Bk[b] = KACC_KEY_EMPTY;
+  __syncthreads();  // step 3's tombstones are in place
+  if (a.stop_after == 4) return;
+
+  // ---- 5: new IDs claim buckets; a re-probe flags an ID given twice ------------------
+  for (uint32_t r = r0 + tid; r < r1; r += kThreads) {
+    const uint32_t w = a.out_slot[r];
+    if (w != kInvalid && (w & KACC_SLOT_NEW)) pr.insert(keys[r], (w & KACC_SLOT_MASK) - s0);
   }
   __syncthreads();
   for (uint32_t r = r0 + tid; r < r1; r += kThreads) {
     const uint32_t w = a.out_slot[r];
-    if (w == kInvalid) continue;
-    const uint32_t rel = (w & KACC_SLOT_MASK) - s0;
-    const uint64_t k = a.keys[r];
-    uint32_t b = static_cast<uint32_t>(mix64(k)) & hmask;
-    for (uint32_t probe = 0; probe < H; ++probe, b = (b + 1) & hmask) {
-      uint64_t prev;
-      if constexpr (kSmall) prev = atomicCAS(reinterpret_cast<unsigned long long *>(&s_keys[b]),
-                                             KACC_KEY_EMPTY, static_cast<unsigned long long>(k));
-      else prev = atomicCAS(reinterpret_cast<unsigned long long *>(&Bk[b]), KACC_KEY_EMPTY,
-                            static_cast<unsigned long long>(k));
-      if (prev == KACC_KEY_EMPTY) {
-        if constexpr (kSmall) s_slots[b] = static_cast<uint16_t>(rel);
-        else Bs[b] = rel;
-        break;
-      }
-      if (prev == k) {  // the same ID twice in one node
-        atomicOr(a.err, kErrKey);
-        a.out_slot[r] = kInvalid;
-        break;
-      }
+    if (w == kInvalid || !(w & KACC_SLOT_NEW)) continue;
+    const uint32_t b = pr.find(keys[r]);
+    if (b == ~0u || L.slot(b) != (w & KACC_SLOT_MASK) - s0) {
+      atomicOr(a.err, kErrKey);
+      a.out_slot[r] = kInvalid;
     }
+  }
+  if (a.stop_after == 5) return;
+
+  // ---- 6: occupancy; rebuild when tombstones crowd the table -------------------------
+  {
+    uint32_t occ = 0;
+    for (uint32_t b = tid; b < H; b += kThreads) occ += L.key(b) != T::kEmpty ? 1u : 0u;
+    occ = wave_sum(occ);
+    if ((tid & 63) == 0) atomicAdd(&s_occ, occ);
   }
   __syncthreads();
-  if constexpr (kSmall) {
-    for (uint32_t b = tid; b < H; b += kThreads) {
-      Bk[b] = s_keys[b];
-      Bs[b] = s_slots[b];
+  if (s_occ * 4 > H * 3) {
+    for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
+    __syncthreads();
+    for (uint32_t r = r0 + tid; r < r1; r += kThreads) {
+      const uint32_t w = a.out_slot[r];
+      if (w != kInvalid) pr.insert(keys[r], (w & KACC_SLOT_MASK) - s0);
     }
   }
-  if (tid == 0) a.parity[n] = static_cast<uint8_t>(par ^ 1u);
 }
 
 }  // namespace join
@@ -304,9 +682,9 @@ struct kacc_slotmap {
   uint64_t buckets = 0;
   uint32_t *d_slot_off = nullptr;
   uint64_t *d_hoff = nullptr;
-  uint64_t *d_keys[2] = {};
-  uint32_t *d_slots[2] = {};
-  uint8_t *d_parity = nullptr;
+  bool has_big = false;         // some node's table exceeds the LDS size
+  uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
+  uint32_t *d_slots = nullptr;  // 64-bit IDs only
 };
 
 namespace {
@@ -348,6 +726,8 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
       return kacc_fail(ctx, KACC_EINVAL, "node %u slot range %u > %u", n, S, kacc::join::kMaxRange);
     hoff[n + 1] = hoff[n] + node_buckets(S);
   }
+  bool has_big = false;
+  for (uint32_t n = 0; n < n_nodes; ++n) has_big |= hoff[n + 1] - hoff[n] > kacc::join::kLdsBuckets;
   if (n_nodes && slot_off[n_nodes] > cap)
     return kacc_fail(ctx, KACC_EINVAL, "slot_off[n] = %u exceeds the kind's slot capacity %llu",
                      slot_off[n_nodes], (unsigned long long)cap);
@@ -357,6 +737,7 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
   m->kind = kind;
   m->n_nodes = n_nodes;
   m->buckets = hoff[n_nodes];
+  m->has_big = has_big;
   auto bail = [&](hipError_t e) {
     kacc_slotmap_destroy(m);
     return kacc_fail(ctx, e == hipErrorOutOfMemory ? KACC_ENOMEM : KACC_EHIP, "slot map allocation: %s",
@@ -366,11 +747,8 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
   const size_t nb = std::max<uint64_t>(m->buckets, 1);
   if ((e = hipMalloc(&m->d_slot_off, 4ull * (n_nodes + 1))) != hipSuccess) return bail(e);
   if ((e = hipMalloc(&m->d_hoff, 8ull * (n_nodes + 1))) != hipSuccess) return bail(e);
-  if ((e = hipMalloc(&m->d_parity, std::max<uint32_t>(n_nodes, 1))) != hipSuccess) return bail(e);
-  for (int p = 0; p < 2; ++p) {
-    if ((e = hipMalloc(&m->d_keys[p], 8 * nb)) != hipSuccess) return bail(e);
-    if ((e = hipMalloc(&m->d_slots[p], 4 * nb)) != hipSuccess) return bail(e);
-  }
+  if ((e = hipMalloc(&m->d_ent, 8 * nb)) != hipSuccess) return bail(e);
+  if (kind != KACC_KIND_PROC && (e = hipMalloc(&m->d_slots, 4 * nb)) != hipSuccess) return bail(e);
   if (n_nodes) {
     if ((e = hipMemcpy(m->d_slot_off, slot_off, 4ull * (n_nodes + 1), hipMemcpyHostToDevice)) != hipSuccess)
       return bail(e);
@@ -392,11 +770,8 @@ void kacc_slotmap_destroy(kacc_slotmap *m) {
   (void)hipStreamSynchronize(m->ctx->stream);
   (void)hipFree(m->d_slot_off);
   (void)hipFree(m->d_hoff);
-  (void)hipFree(m->d_parity);
-  for (int p = 0; p < 2; ++p) {
-    (void)hipFree(m->d_keys[p]);
-    (void)hipFree(m->d_slots[p]);
-  }
+  (void)hipFree(m->d_ent);
+  (void)hipFree(m->d_slots);
   delete m;
 }
 
@@ -405,28 +780,46 @@ int kacc_slotmap_reset(kacc_slotmap *m) {
   kacc_ctx *ctx = m->ctx;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   const size_t nb = std::max<uint64_t>(m->buckets, 1);
-  for (int p = 0; p < 2; ++p) KACC_HIP(ctx, hipMemsetAsync(m->d_keys[p], 0xff, 8 * nb, ctx->stream));
-  KACC_HIP(ctx, hipMemsetAsync(m->d_parity, 0, std::max<uint32_t>(m->n_nodes, 1), ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(m->d_ent, 0xff, 8 * nb, ctx->stream));  // every bucket empty
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return KACC_OK;
 }
 
-int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
+static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
+                     const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
+                     uint32_t *term_slot, uint32_t *term_count, void *stream, uint32_t stop_after);
+
+int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                   uint32_t *term_slot, uint32_t *term_count, uint32_t term_cap, void *stream) {
+                   uint32_t *term_slot, uint32_t *term_count, void *stream) {
+  return slot_join(m, n_rows, row_off, keys, node_status, out_slot, term_key, term_slot, term_count,
+                   stream, 0u);
+}
+
+int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
+                            uint32_t *out_slot, uint64_t *term_key, uint32_t *term_slot,
+                            uint32_t *term_count, void *stream, uint32_t stop_after) {
+  return slot_join(m, n_rows, row_off, keys, nullptr, out_slot, term_key, term_slot, term_count,
+                   stream, stop_after);
+}
+
+}  // extern "C"
+
+static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
+                     const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
+                     uint32_t *term_slot, uint32_t *term_count, void *stream, uint32_t stop_after) {
   if (!m) return KACC_EINVAL;
   kacc_ctx *ctx = m->ctx;
   if (!m->n_nodes) return KACC_OK;
-  if (!row_off || !out_slot || !term_count || (term_cap && (!term_key || !term_slot)))
+  if (!row_off || !out_slot || !term_count || !term_key || !term_slot)
     return kacc_fail(ctx, KACC_EINVAL, "slot join: NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if (n_rows && !keys) return kacc_fail(ctx, KACC_EINVAL, "slot join: keys is NULL");
-  KACC_HIP(ctx, hipMemsetAsync(term_count, 0, 4, st));
   kacc::join::Args a{};
   a.n_nodes = m->n_nodes;
   a.n_rows = n_rows;
-  a.term_cap = term_cap;
+  a.stop_after = stop_after;
   a.row_off = row_off;
   a.keys = keys;
   a.node_status = node_status;
@@ -436,16 +829,20 @@ int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, co
   a.term_count = term_count;
   a.slot_off = m->d_slot_off;
   a.hoff = m->d_hoff;
-  for (int p = 0; p < 2; ++p) {
-    a.hkeys[p] = m->d_keys[p];
-    a.hslots[p] = m->d_slots[p];
-  }
-  a.parity = m->d_parity;
+  a.ent = m->d_ent;
+  a.slots = m->d_slots;
   a.err = ctx->d_err;
-  hipLaunchKernelGGL((kacc::join::join_kernel<true>), dim3(m->n_nodes), dim3(kacc::join::kThreads), 0, st, a);
-  hipLaunchKernelGGL((kacc::join::join_kernel<false>), dim3(m->n_nodes), dim3(kacc::join::kThreads), 0, st, a);
+  using namespace kacc::join;
+  const dim3 grid(m->n_nodes), block(kThreads);
+  if (m->kind == KACC_KIND_PROC) {
+    hipLaunchKernelGGL((join_small<uint32_t>), grid, block, 0, st, a);
+    if (m->has_big) hipLaunchKernelGGL((join_big<uint32_t>), grid, block, 0, st, a);
+  } else {
+    hipLaunchKernelGGL((join_small<uint64_t>), grid, block, 0, st, a);
+    if (m->has_big) hipLaunchKernelGGL((join_big<uint64_t>), grid, block, 0, st, a);
+  }
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
 
-}  // extern "C"
+

@@ -84,13 +84,14 @@ void kor_gf_destroy(kor_gofaithful *g);
 int kor_gf_interval(kor_gofaithful *g, kor_state *st, const kacc_interval *b);
 
 /* Slot join restatement (kor_join.cpp): same contract as kacc_slot_join on
- * host arrays; returns 0, or KACC_ERANGE after an error row / overflow.     */
+ * host arrays (term_* sized slot_off[n], term_count [n_nodes]); returns 0, or
+ * KACC_ERANGE after an error row.                                          */
 typedef struct kor_slotmap kor_slotmap;
 kor_slotmap *kor_slotmap_create(uint32_t n_nodes, const uint32_t *slot_off);
 void kor_slotmap_destroy(kor_slotmap *m);
 int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                  uint32_t *term_slot, uint32_t term_cap, uint32_t *term_count);
+                  uint32_t *term_slot, uint32_t *term_count);
 
 #ifdef __cplusplus
 }

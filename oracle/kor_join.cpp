@@ -10,6 +10,7 @@
 // is the engine's own (the reference has no slots): a new ID takes the lowest
 // slot of its node's range not held by any ID of the previous set, new rows
 // taking slots in row order.
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <unordered_map>
@@ -35,11 +36,11 @@ void kor_slotmap_destroy(kor_slotmap *m) { delete m; }
 
 int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                  uint32_t *term_slot, uint32_t term_cap, uint32_t *term_count) {
+                  uint32_t *term_slot, uint32_t *term_count) {
   const uint32_t N = static_cast<uint32_t>(m->live.size());
-  uint32_t nt = 0;
   int rc = KACC_OK;
   for (uint32_t n = 0; n < N; ++n) {
+    term_count[n] = 0;
     if (node_status && (node_status[n] & KACC_NODE_READ_ERROR)) continue;  // Refresh skipped
     const uint32_t r0 = row_off[n], r1 = row_off[n + 1];
     if (r1 > n_rows || r0 > r1) return KACC_EINVAL;
@@ -52,7 +53,7 @@ int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, cons
     uint32_t next_free = 0;
     for (uint32_t r = r0; r < r1; ++r) {
       const uint64_t k = keys[r];
-      if (k == KACC_KEY_EMPTY || cur.count(k)) {
+      if (k == KACC_KEY_EMPTY || k == KACC_KEY_TOMB || cur.count(k)) {
         out_slot[r] = 0xffffffffu;
         rc = KACC_ERANGE;
         continue;
@@ -73,19 +74,18 @@ int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, cons
       out_slot[r] = (s0 + next_free) | KACC_SLOT_NEW;
       cur.emplace(k, next_free);
     }
-    for (const auto &kv : prev) {
-      if (cur.count(kv.first)) continue;
-      if (nt < term_cap) {
-        term_key[nt] = kv.first;
-        term_slot[nt] = s0 + kv.second;
-      } else {
-        rc = KACC_ERANGE;
-      }
-      ++nt;
+    // terminated (informer.go:206-212): the node's segment, ascending by slot
+    std::vector<std::pair<uint32_t, uint64_t>> term;
+    for (const auto &kv : prev)
+      if (!cur.count(kv.first)) term.emplace_back(kv.second, kv.first);
+    std::sort(term.begin(), term.end());
+    for (size_t i = 0; i < term.size(); ++i) {
+      term_key[s0 + i] = term[i].second;
+      term_slot[s0 + i] = s0 + term[i].first;
     }
+    term_count[n] = static_cast<uint32_t>(term.size());
     prev.swap(cur);
   }
-  *term_count = nt;
   return rc;
 }
 

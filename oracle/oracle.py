@@ -61,7 +61,7 @@ def load():
     lib.kor_slotmap_destroy.argtypes = [c_void_p]
     lib.kor_slotmap_destroy.restype = None
     lib.kor_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                  c_void_p, c_void_p, c_uint32, c_void_p]
+                                  c_void_p, c_void_p, c_void_p]
     lib.kor_gf_create.argtypes = [c_uint32]
     lib.kor_gf_create.restype = c_void_p
     lib.kor_gf_destroy.argtypes = [c_void_p]
@@ -179,22 +179,30 @@ class OracleSlotMap:
         self.off = np.ascontiguousarray(slot_off, dtype=np.uint32)
         self.h = self.lib.kor_slotmap_create(self.off.size - 1, self.off.ctypes.data)
 
-    def join(self, row_off, keys, node_status=None, term_cap=None):
-        """Returns (rc, out_slot, term_key, term_slot) on host arrays."""
+    def join(self, row_off, keys, node_status=None):
+        """Returns (rc, out_slot, term_key, term_slot, term_count) on host arrays;
+        node n's terminated IDs are term_*[slot_off[n] : slot_off[n] + term_count[n]]."""
         row_off = np.ascontiguousarray(row_off, dtype=np.uint32)
         keys = np.ascontiguousarray(keys, dtype=np.uint64)
         n_rows = int(row_off[-1])
         out = np.zeros(max(n_rows, 1), dtype=np.uint32)
-        cap = int(self.off[-1]) if term_cap is None else term_cap
-        tk = np.zeros(max(cap, 1), dtype=np.uint64)
-        ts = np.zeros(max(cap, 1), dtype=np.uint32)
-        cnt = np.zeros(1, dtype=np.uint32)
+        cap = max(int(self.off[-1]), 1)
+        tk = np.zeros(cap, dtype=np.uint64)
+        ts = np.zeros(cap, dtype=np.uint32)
+        cnt = np.zeros(max(self.off.size - 1, 1), dtype=np.uint32)
         st = None if node_status is None else np.ascontiguousarray(node_status, dtype=np.uint32)
         rc = self.lib.kor_slot_join(self.h, n_rows, row_off.ctypes.data, keys.ctypes.data if keys.size else None,
                                     None if st is None else st.ctypes.data, out.ctypes.data, tk.ctypes.data,
-                                    ts.ctypes.data, cap, cnt.ctypes.data)
-        n = min(int(cnt[0]), cap)
-        return rc, out[:n_rows], tk[:n], ts[:n]
+                                    ts.ctypes.data, cnt.ctypes.data)
+        return rc, out[:n_rows], tk, ts, cnt[: self.off.size - 1]
+
+    def terminated(self, tk, ts, cnt):
+        """Flatten the per-node segments to a list of (key, slot)."""
+        out = []
+        for n, c in enumerate(cnt.tolist()):
+            s0 = int(self.off[n])
+            out += list(zip(tk[s0:s0 + c].tolist(), ts[s0:s0 + c].tolist()))
+        return out
 
     def __del__(self):  # pragma: no cover
         try:

@@ -29,30 +29,39 @@ def gpu_ready():
 class GpuJoin:
     def __init__(self, acc, kind, slot_off):
         self.acc = acc
+        self.kind = kind
         self.m = accel.SlotMap(acc, kind, slot_off)
-        cap = int(slot_off[-1])
-        self.cap = max(cap, 1)
-        self.tk = torch.zeros(self.cap, dtype=torch.int64, device="cuda")
-        self.ts = torch.zeros(self.cap, dtype=torch.int32, device="cuda")
-        self.cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self.slot_off = slot_off
+        cap = max(int(slot_off[-1]), 1)
+        self.tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        self.ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
+        self.cnt = torch.zeros(max(len(slot_off) - 1, 1), dtype=torch.int32, device="cuda")
 
     def join(self, row_off, keys, status=None, out=None, sync=True):
         d_off = torch.from_numpy(row_off.astype(np.int32)).cuda()
-        d_keys = torch.from_numpy(keys.view(np.int64)).cuda()
+        if self.kind == accel.KACC_KIND_PROC:  # PIDs are u32 keys
+            d_keys = torch.from_numpy(keys.astype(np.uint32).view(np.int32)).cuda()
+        else:
+            d_keys = torch.from_numpy(keys.view(np.int64)).cuda()
         d_st = None if status is None else torch.from_numpy(status.astype(np.int32)).cuda()
         n_rows = int(row_off[-1])
         if out is None:
             out = torch.zeros(max(n_rows, 1), dtype=torch.int32, device="cuda")
         s = current_stream_handle()
         self.m.join(n_rows, d_off.data_ptr(), d_keys.data_ptr(), 0 if d_st is None else d_st.data_ptr(),
-                    out.data_ptr(), self.tk.data_ptr(), self.ts.data_ptr(), self.cnt.data_ptr(), self.cap, s)
+                    out.data_ptr(), self.tk.data_ptr(), self.ts.data_ptr(), self.cnt.data_ptr(), s)
         if not sync:
             return out
         self.acc.sync(s)
-        n = min(int(self.cnt.item()), self.cap)
         got = out[:n_rows].cpu().numpy().view(np.uint32)
-        term = sorted(zip(self.tk[:n].cpu().numpy().view(np.uint64).tolist(),
-                          self.ts[:n].cpu().numpy().view(np.uint32).tolist()))
+        tk = self.tk.cpu().numpy().view(np.uint64)
+        ts = self.ts.cpu().numpy().view(np.uint32)
+        term = []  # node segments, ascending by slot
+        for n, c in enumerate(self.cnt.cpu().numpy()[: len(self.slot_off) - 1].tolist()):
+            if status is not None and status[n]:
+                continue
+            s0 = int(self.slot_off[n])
+            term += list(zip(tk[s0:s0 + c].tolist(), ts[s0:s0 + c].tolist()))
         return got, term
 
 
@@ -84,14 +93,15 @@ def test_join_bit_exact(name, sizes, churn, kind):
         status = None
         if it >= 2:
             status = np.where(rng.random(len(sizes)) < 0.2, accel.KACC_NODE_READ_ERROR, 0).astype(np.uint32)
-        rc, want, tk, ts = ora.join(row_off, keys, status)
+        rc, want, tk, ts, cnt = ora.join(row_off, keys, status)
         assert rc == 0
+        want_term = ora.terminated(tk, ts, cnt)
         got, term = gpu.join(row_off, keys, status)
         if status is not None:  # rows of skipped nodes are not produced by either side
             keep = np.repeat(status == 0, np.diff(row_off.astype(np.int64)))
             got, want = got[keep], want[keep]
         np.testing.assert_array_equal(got, want, err_msg=f"interval {it}")
-        assert term == sorted(zip(tk.tolist(), ts.tolist())), f"interval {it}"
+        assert term == want_term, f"interval {it}"
 
 
 def test_join_errors_raise_erange():
@@ -103,8 +113,11 @@ def test_join_errors_raise_erange():
         gpu.join(row_off, np.array([5, 5, 6, 1, 2, 3], dtype=np.uint64))
     assert ei.value.code == accel.KACC_ERANGE
     gpu.m.reset()
-    with pytest.raises(accel.AccelError):
-        gpu.join(row_off, np.array([1, accel.KACC_KEY_EMPTY, 2, 1, 2, 3], dtype=np.uint64))
+    with pytest.raises(accel.AccelError):  # reserved PID 0xffffffff
+        gpu.join(row_off, np.array([1, 0xFFFFFFFF, 2, 1, 2, 3], dtype=np.uint64))
+    gpu.m.reset()
+    with pytest.raises(accel.AccelError):  # a new ID given twice
+        gpu.join(np.array([0, 3, 3], dtype=np.uint32), np.array([9, 4, 9], dtype=np.uint64))
     gpu.m.reset()  # and a valid batch afterwards
     got, term = gpu.join(np.array([0, 3, 5], dtype=np.uint32), np.array([1, 2, 3, 7, 8], dtype=np.uint64))
     np.testing.assert_array_equal(got & 0x7FFFFFFF, [0, 1, 2, 8, 9])
@@ -130,7 +143,7 @@ def test_join_feeds_interval_bit_exact():
         a = sim.next_interval()
         keys = keys_sim.next_keys()
         # CPU deltas restart for new IDs (informer.go:518: prevTotal 0 for a new PID)
-        _, want_slots, _, _ = ojoin.join(layout.proc_off, keys, a["node_status"])
+        _, want_slots, _, _, _ = ojoin.join(layout.proc_off, keys, a["node_status"])
         a_ora = dict(a)
         a_ora["proc_slot"] = want_slots
         t = to_device(a)

@@ -44,9 +44,10 @@ class PySlotMap:
                     s = free.pop(0)
                     cur[k] = s
                     out[r] = (s0 + s) | KACC_SLOT_NEW
-            term += [(k, s0 + s) for k, s in prev.items() if k not in cur]  # informer.go:206-212
+            # informer.go:206-212; the node's segment ascending by slot
+            term += sorted(((k, s0 + s) for k, s in prev.items() if k not in cur), key=lambda x: x[1])
             self.live[n] = cur
-        return out, sorted(term)
+        return out, term
 
 
 def ranges(sizes, slack=1.25):
@@ -66,11 +67,12 @@ def test_oracle_join_matches_go_maps(kind):
     for it in range(6):
         keys = sim.next_keys()
         status = np.where(rng.random(len(sizes)) < 0.15, KACC_NODE_READ_ERROR, 0).astype(np.uint32) if it else None
-        rc, out, tk, ts = ora.join(row_off, keys, status)
+        rc, out, tk, ts, cnt = ora.join(row_off, keys, status)
         assert rc == 0
         want, want_term = py.join(row_off, keys, status)
         np.testing.assert_array_equal(out, want)
-        assert sorted(zip(tk.tolist(), ts.tolist())) == want_term
+        assert ora.terminated(tk, ts, cnt) == want_term
+        ts = np.array([s for _, s in want_term], dtype=np.uint32)
         # properties: slots in range and unique per node; a live key keeps its slot
         for n in range(len(sizes)):
             if status is not None and status[n]:
@@ -90,8 +92,8 @@ def test_oracle_join_matches_go_maps(kind):
 
 def test_oracle_join_first_interval_consecutive():
     row_off, slot_off = ranges([5, 3])
-    rc, out, tk, _ = OracleSlotMap(slot_off).join(row_off, np.arange(8, dtype=np.uint64))
-    assert rc == 0 and tk.size == 0
+    rc, out, _, _, cnt = OracleSlotMap(slot_off).join(row_off, np.arange(8, dtype=np.uint64))
+    assert rc == 0 and cnt.sum() == 0
     np.testing.assert_array_equal(out & 0x7FFFFFFF, [0, 1, 2, 3, 4, slot_off[1], slot_off[1] + 1, slot_off[1] + 2])
     assert np.all(out & KACC_SLOT_NEW)
 
@@ -99,17 +101,17 @@ def test_oracle_join_first_interval_consecutive():
 def test_oracle_join_errors():
     row_off = np.array([0, 3], dtype=np.uint32)
     # duplicate ID inside a node, reserved key
-    rc, out, _, _ = OracleSlotMap(np.array([0, 8], dtype=np.uint32)).join(row_off, np.array([5, 5, 6], dtype=np.uint64))
+    rc, out, _, _, _ = OracleSlotMap(np.array([0, 8], dtype=np.uint32)).join(row_off, np.array([5, 5, 6], dtype=np.uint64))
     assert rc == KACC_ERANGE and out[1] == 0xFFFFFFFF
-    rc, out, _, _ = OracleSlotMap(np.array([0, 8], dtype=np.uint32)).join(
+    rc, out, _, _, _ = OracleSlotMap(np.array([0, 8], dtype=np.uint32)).join(
         row_off, np.array([1, KACC_KEY_EMPTY, 2], dtype=np.uint64))
     assert rc == KACC_ERANGE and out[1] == 0xFFFFFFFF
     # range overflow: 3 live IDs, 2 slots
-    rc, out, _, _ = OracleSlotMap(np.array([0, 2], dtype=np.uint32)).join(row_off, np.array([1, 2, 3], dtype=np.uint64))
+    rc, out, _, _, _ = OracleSlotMap(np.array([0, 2], dtype=np.uint32)).join(row_off, np.array([1, 2, 3], dtype=np.uint64))
     assert rc == KACC_ERANGE and out[2] == 0xFFFFFFFF
     # terminated slots stay held for one interval: 2 slots, full turnover -> overflow now, fine next time
     m = OracleSlotMap(np.array([0, 2], dtype=np.uint32))
     two = np.array([0, 2], dtype=np.uint32)
     assert m.join(two, np.array([1, 2], dtype=np.uint64))[0] == 0
-    rc, out, tk, _ = m.join(two, np.array([3, 4], dtype=np.uint64))
-    assert rc == KACC_ERANGE and sorted(tk.tolist()) == [1, 2]
+    rc, out, tk, ts, cnt = m.join(two, np.array([3, 4], dtype=np.uint64))
+    assert rc == KACC_ERANGE and m.terminated(tk, ts, cnt) == [(1, 0), (2, 1)]
