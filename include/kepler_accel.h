@@ -126,6 +126,12 @@ typedef struct kacc_interval {
   const uint32_t *node_status;    /* KACC_NODE_* bits, may be NULL                    */
   const double *node_cpu_delta;   /* ProcessTotalCPUTimeDelta override (flags)        */
   const uint32_t *node_order;     /* optional launch order (heaviest first), NULL=id  */
+  const uint32_t *node_proc_span; /* optional [2*n_nodes]: {min, max} process slot of
+                                     each node's rows (kacc_slot_join's out_span).
+                                     When max - min < KACC_FAST_MAX_PROCS the node's
+                                     rows are moved in slot order (1 KiB-contiguous
+                                     wave accesses however fragmented the slots are);
+                                     a row outside its node's span raises ERANGE.   */
   /* zones [n_nodes * Z], node-major */
   const uint64_t *zone_energy;    /* EnergyZone.Energy()   (cpu_power_meter.go:22) */
   const uint64_t *zone_max;       /* EnergyZone.MaxEnergy() (cpu_power_meter.go:26) */
@@ -277,7 +283,8 @@ typedef struct kacc_slotmap kacc_slotmap;
  * slot capacity in kacc_config, each range <= 131072 slots.  Starts empty.   */
 int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const uint32_t *slot_off,
                         kacc_slotmap **out);
-void kacc_slotmap_destroy(kacc_slotmap *m);
+void kacc_slotmap_destroy(kacc_slotmap *m); /* safe before or after kacc_destroy(ctx); other
+                                               calls need the context alive */
 int kacc_slotmap_reset(kacc_slotmap *m); /* forget every ID (PowerMonitor restart) */
 /* Device pointers, asynchronous on `stream` (NULL = the context's stream).
  * n_rows = row_off[n_nodes] (the batch's n_procs / n_ctrs / n_vms / n_pods);
@@ -287,10 +294,12 @@ int kacc_slotmap_reset(kacc_slotmap *m); /* forget every ID (PowerMonitor restar
  * Terminated IDs, per node: term_count[n] of them, at positions
  * [slot_off[n], slot_off[n] + term_count[n]) of term_key (uint64_t) and
  * term_slot (both sized slot_off[n_nodes]), ascending by slot.  term_count of
- * a skipped node is set to 0.                                                */
+ * a skipped node is set to 0.  out_span (optional, [2*n_nodes]): {min, max}
+ * slot word & KACC_SLOT_MASK over the node's rows ({1, 0} for a node without
+ * rows; untouched for a skipped node) — kacc_interval.node_proc_span.        */
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                   uint32_t *term_slot, uint32_t *term_count, void *stream);
+                   uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream);
 
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */

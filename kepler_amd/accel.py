@@ -118,6 +118,7 @@ INTERVAL_ARRAYS = [
     "node_status",
     "node_cpu_delta",
     "node_order",
+    "node_proc_span",
     "zone_energy",
     "zone_max",
     "proc_off",
@@ -134,13 +135,14 @@ INTERVAL_ARRAYS = [
     "pod_slot",
 ]
 # the optional ones may be NULL
-OPTIONAL_ARRAYS = {"node_status", "node_cpu_delta", "node_order"}
+OPTIONAL_ARRAYS = {"node_status", "node_cpu_delta", "node_order", "node_proc_span"}
 ARRAY_DTYPES = {
     "node_ts_ns": np.int64,
     "node_usage_ratio": np.float64,
     "node_status": np.uint32,
     "node_cpu_delta": np.float64,
     "node_order": np.uint32,
+    "node_proc_span": np.uint32,
     "zone_energy": np.uint64,
     "zone_max": np.uint64,
     "proc_off": np.uint32,
@@ -223,7 +225,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_slotmap_destroy.restype = None
     lib.kacc_slotmap_reset.argtypes = [c_void_p]
     lib.kacc_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
-                                   c_void_p, c_void_p, c_void_p, c_void_p]
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     if lib.kacc_abi_version() != KACC_ABI_VERSION:
         raise ImportError("libkepler_accel ABI version mismatch")
     _lib = lib
@@ -372,12 +374,15 @@ class SlotMap:
         self.accel._check(self.lib.kacc_slotmap_reset(self.handle))
 
     def join(self, n_rows: int, row_off_ptr: int, keys_ptr: int, node_status_ptr: int, out_slot_ptr: int,
-             term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, stream: int = 0) -> None:
-        """term_key / term_slot: [slot_off[-1]], term_count: [n_nodes] (per-node segments)."""
+             term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, stream: int = 0,
+             out_span_ptr: int = 0) -> None:
+        """term_key / term_slot: [slot_off[-1]], term_count: [n_nodes] (per-node segments);
+        out_span: optional [2*n_nodes] {min, max} slot per node (kacc_interval.node_proc_span)."""
         self.accel._check(self.lib.kacc_slot_join(
             self.handle, n_rows, c_void_p(row_off_ptr), c_void_p(keys_ptr or None),
             c_void_p(node_status_ptr or None), c_void_p(out_slot_ptr), c_void_p(term_key_ptr),
-            c_void_p(term_slot_ptr), c_void_p(term_count_ptr), c_void_p(stream or None)))
+            c_void_p(term_slot_ptr), c_void_p(term_count_ptr), c_void_p(out_span_ptr or None),
+            c_void_p(stream or None)))
 
     def close(self) -> None:
         if self.handle:

@@ -51,6 +51,7 @@ constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
 constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
 constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
+constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row order only)
 constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
 constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
 constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk kernel idles)
@@ -255,31 +256,48 @@ __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, 
   store_row<Z, NT, double>(power, s, P);
 }
 
-// A 64-row group whose slots are consecutive (slot(row g+l) = s0 + l) is
-// moved with 1 KiB-contiguous wave instructions: its Z/2 × 64 16-B pieces of
-// the energy (and power) table are spread over the lanes, piece p = l + 64j
-// holding zones 2(p mod Z/2) and 2(p mod Z/2)+1 of row p div (Z/2).  Same
-// arithmetic as attribute_row, only the lane <-> (row, zone) mapping differs.
-template <int Z>
-__device__ __forceinline__ void load_group(const uint64_t *__restrict__ base, uint64_t s0,
-                                           uint64_t (&out)[Z]) {
+// Slot sweep: a node whose rows' slots span at most kRowsLds slots (the slot
+// join keeps each node in its own slot range) is attributed in SLOT order:
+// 64-slot groups [smin + pos0, +64) moved with 1 KiB-contiguous wave
+// instructions, each slot's row found through the LDS inverse map s_inv
+// (0xffff = no row: a free slot, skipped).  The same two functions move a
+// 64-row group whose slots are consecutive (row = row0 + index, no map).
+// Piece p = lane + 64j of a group holds zones 2(p mod Z/2), +1 of the group's
+// slot p div (Z/2); pieces past len or the table end are masked.
+// Loads are unconditional (a masked piece reads slot `safe`, a valid slot,
+// and is zeroed): no exec-mask branches, so every group's loads stay in flight.
+template <int Z, bool kMasked>
+__device__ __forceinline__ void load_group_masked(const uint64_t *__restrict__ base, uint64_t s0,
+                                                  uint32_t len, uint64_t safe, uint64_t (&out)[Z]) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
-  const u64x2 *p = reinterpret_cast<const u64x2 *>(base + s0 * Z);
+  constexpr int kHalf = Z / 2;
   const uint32_t lane = threadIdx.x & 63u;
+  const u64x2 *p = reinterpret_cast<const u64x2 *>(base + s0 * Z);
+  const u64x2 *q = reinterpret_cast<const u64x2 *>(base + safe * Z);
 #pragma unroll
-  for (int j = 0; j < Z / 2; ++j) {
-    const u64x2 x = p[lane + 64 * j];
-    out[2 * j] = x.x;
-    out[2 * j + 1] = x.y;
+  for (int j = 0; j < kHalf; ++j) {
+    const uint32_t piece = lane + 64u * j;
+    if constexpr (!kMasked) {  // a full group of consecutive slots
+      const u64x2 x = p[piece];
+      out[2 * j] = x.x;
+      out[2 * j + 1] = x.y;
+      continue;
+    }
+    const bool ok = piece / kHalf < len;
+    const u64x2 x = *(ok ? p + piece : q);
+    out[2 * j] = ok ? x.x : 0ull;
+    out[2 * j + 1] = ok ? x.y : 0ull;
   }
 }
 
-template <int Z, bool NT>
-__device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShared &sh,
-                                                const double *s_d_group, const uint32_t *s_w_group,
-                                                uint64_t s0, const uint64_t (&prev)[Z],
-                                                uint64_t *__restrict__ energy,
-                                                double *__restrict__ power) {
+template <int Z, bool NT, bool kInv>
+__device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const NodeShared &sh,
+                                                       const double *s_d, const uint32_t *s_w,
+                                                       const uint16_t *s_inv,
+                                                       uint32_t row0, uint64_t s0, uint32_t len,
+                                                       const uint64_t (&prev)[Z],
+                                                       uint64_t *__restrict__ energy,
+                                                       double *__restrict__ power) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
   using f64x2 = __attribute__((ext_vector_type(2))) double;
   constexpr int kHalf = Z / 2;
@@ -289,11 +307,17 @@ __device__ __forceinline__ void attribute_group(const Attr<Z> &a, const NodeShar
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) {
     const uint32_t piece = lane + 64u * j;
-    const uint32_t row = piece / kHalf;
+    const uint32_t idx = piece / kHalf;
     const uint32_t zp = piece % kHalf;
-    const uint32_t wr = s_w_group[row];
+    uint32_t row = row0 + idx;
+    if constexpr (kInv) {
+      if (idx >= len) continue;
+      row = s_inv[row];
+      if (row == 0xffffu) continue;  // free slot of the node's range
+    }
+    const uint32_t wr = s_w[row];
     const bool is_new = (wr & KACC_SLOT_NEW) != 0;
-    const double ratio = s_d_group[row] / a.nd;  // the row's own IEEE division
+    const double ratio = s_d[row] / a.nd;  // the row's own IEEE division
     uint64_t E[2];
     double P[2];
 #pragma unroll
@@ -410,6 +434,7 @@ void interval_kernel(const kacc_interval b, const DevState st) {
   __shared__ double s_ct[kThreads];  // container running CPU total
   __shared__ double red[kTree];
   __shared__ NodeShared sh;
+  __shared__ uint16_t s_inv[kRowsLds];  // slot sweep: slot - smin -> row (0xffff: none)
 
   const int tid = threadIdx.x;
   // the previous interval's pod_kernel has drained the deferred list; this
@@ -505,28 +530,60 @@ void interval_kernel(const kacc_interval b, const DevState st) {
     return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
   };
   // second-level gathers (depend on the slot words).  A 64-row group with
-  // consecutive slots is loaded 1 KiB-contiguous per wave instruction.
+  // consecutive slots is loaded 1 KiB-contiguous per wave instruction; a node
+  // whose slots are not consecutive but span <= kRowsLds slots is swept in
+  // slot order instead (see load_span_group).
   uint64_t prev[kRowsPerThread][Z];
   uint32_t contig = 0;  // bit k: group k of this wave is transposed (wave-uniform)
-  if constexpr ((V & kVarSkipProcs) == 0) {
+  constexpr bool kSweepable =
+      kTransposed<Z> && (V & (kVarNoTranspose | kVarNoSweep | kVarSkipProcs)) == 0;
+  // slot sweep when the caller gives the node's slot span (kacc_slot_join's
+  // out_span) and it fits the LDS inverse map; node-uniform -> SGPRs
+  uint32_t smin = 0, span = 0;
+  bool sweep = false;
+  if constexpr (kSweepable) {
+    if (b.node_proc_span) {
+      const uint32_t lo = uniform_u32(b.node_proc_span[2 * n]);
+      const uint32_t hi = uniform_u32(b.node_proc_span[2 * n + 1]);
+      sweep = rows > 0 && hi >= lo && hi - lo < static_cast<uint32_t>(kRowsLds) && hi < st.proc_slots;
+      smin = lo;
+      span = hi - lo + 1;
+      if (sweep) {
 #pragma unroll
-    for (int k = 0; k < kRowsPerThread; ++k) {
-      const uint64_t sl = w[k] & KACC_SLOT_MASK;
-      if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
-        const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));  // lane 0's slot
-        const bool mine = (tid + k * kThreads) < rows && sl == s0 + (tid & 63) &&
-                          s0 + 64 <= st.proc_slots;
-        if (__all(mine)) {
-          contig |= 1u << k;
-          load_group<Z>(st.proc_energy, s0, prev[k]);
-          continue;
+        for (int k = 0; k < kRowsPerThread; ++k) s_inv[tid + k * kThreads] = 0xffffu;
+      }
+    }
+  }
+  const bool swept = kSweepable && sweep;
+  if constexpr ((V & kVarSkipProcs) == 0) {
+    if (swept) {  // prev totals of the span's 64-slot groups (free slots read too)
+      if constexpr (kSweepable) {
+#pragma unroll
+        for (int k = 0; k < kRowsPerThread; ++k) {
+          const uint32_t pos0 = static_cast<uint32_t>(tid & ~63) + k * kThreads;
+          const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
+          load_group_masked<Z, true>(st.proc_energy, static_cast<uint64_t>(smin) + pos0, len, smin,
+                                     prev[k]);
         }
       }
-      if (sl < st.proc_slots) {
-        load_row<Z>(st.proc_energy, sl, prev[k]);
-      } else {
+    } else {
 #pragma unroll
-        for (int z = 0; z < Z; ++z) prev[k][z] = 0;
+      for (int k = 0; k < kRowsPerThread; ++k) {
+        const uint64_t sl = w[k] & KACC_SLOT_MASK;
+        if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
+          const uint64_t g0 = uniform_u32(static_cast<uint32_t>(sl));  // lane 0's slot
+          if (__all((tid + k * kThreads) < rows && sl == g0 + (tid & 63) && g0 + 64 <= st.proc_slots)) {
+            contig |= 1u << k;
+            load_group_masked<Z, false>(st.proc_energy, g0, 64u, g0, prev[k]);
+            continue;
+          }
+        }
+        if (sl < st.proc_slots) {
+          load_row<Z>(st.proc_energy, sl, prev[k]);
+        } else {
+#pragma unroll
+          for (int z = 0; z < Z; ++z) prev[k][z] = 0;
+        }
       }
     }
   }
@@ -551,6 +608,18 @@ void interval_kernel(const kacc_interval b, const DevState st) {
     }
   }
   __syncthreads();
+  if (swept) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; ++k) {
+      const uint32_t r = tid + k * kThreads;
+      if (r >= rows) continue;
+      const uint32_t sl = s_w[r] & KACC_SLOT_MASK;
+      if (sl - smin < span && sl < st.proc_slots)
+        s_inv[sl - smin] = static_cast<uint16_t>(r);
+      else  // outside the node's span / the table: not attributed
+        raise_err(st.err, kErrSlot);
+    }
+  }
   if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
     if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
   } else {
@@ -638,15 +707,27 @@ void interval_kernel(const kacc_interval b, const DevState st) {
     store_row<Z, kNT, double>(a_power(), a_s, P);
   };
   if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
-  if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
+  if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
+    if constexpr (kSweepable) {
+#pragma unroll
+      for (int k = 0; k < kRowsPerThread; ++k) {
+        const uint32_t pos0 = static_cast<uint32_t>(tid & ~63) + k * kThreads;
+        const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
+        attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
+                                             static_cast<uint64_t>(smin) + pos0, len, prev[k],
+                                             st.proc_energy, st.proc_power);
+      }
+    }
+  } else if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint32_t r = tid + k * kThreads;
       if constexpr (kTransposed<Z> && (V & kVarNoTranspose) == 0) {
-        if (contig & (1u << k)) {
-          const uint64_t s0 = uniform_u32(s_w[r - (tid & 63)] & KACC_SLOT_MASK);
-          attribute_group<Z, kNT>(a, sh, s_d + (r - (tid & 63)), s_w + (r - (tid & 63)), s0, prev[k],
-                                  st.proc_energy, st.proc_power);
+        if (contig & (1u << k)) {  // rows pos0 + i hold slots s0 + i
+          const uint32_t pos0 = r - (tid & 63);
+          attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
+                                                uniform_u32(s_w[pos0] & KACC_SLOT_MASK), 64u, prev[k],
+                                                st.proc_energy, st.proc_power);
           continue;
         }
       }
@@ -938,7 +1019,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
                             s0 + 64 <= st.proc_slots;
           if (__all(mine)) {
             contig |= 1u << u;
-            load_group<Z>(st.proc_energy, s0, prev[u]);
+            load_group_masked<Z, false>(st.proc_energy, s0, 64u, s0, prev[u]);
             continue;
           }
         }
@@ -1096,8 +1177,9 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
         if constexpr (kT) {
           if (contig & (1u << u)) {
             const uint32_t g = r - (tid & 63);
-            attribute_group<Z, kNT>(a, sh, s_d + g, s_w + g, uniform_u32(s_w[g] & KACC_SLOT_MASK),
-                                    prev[u], st.proc_energy, st.proc_power);
+            attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, nullptr, g,
+                                           uniform_u32(s_w[g] & KACC_SLOT_MASK), 64u, prev[u],
+                                           st.proc_energy, st.proc_power);
             continue;
           }
         }
@@ -1420,6 +1502,7 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 512: launch_zv<4, 512>(b, s, st); return true;
     case 768: launch_zv<4, 768>(b, s, st); return true;
     case 1024: launch_zv<4, 1024>(b, s, st); return true;
+    case 2048: launch_zv<4, 2048>(b, s, st); return true;
     default: return false;
   }
 }
@@ -1605,6 +1688,7 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   if (rc != KACC_OK || b->n_nodes == 0) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
   launch(ctx->cfg.zones, *b, dev_state(ctx), st);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
@@ -1658,6 +1742,14 @@ int kacc_validate_host(const kacc_ctx *cctx, const kacc_interval *b) {
   if ((rc = check_slots(ctx, "ctr_slot", b->ctr_slot, b->n_ctrs, ctx->cfg.ctr_slots))) return rc;
   if ((rc = check_slots(ctx, "vm_slot", b->vm_slot, b->n_vms, ctx->cfg.vm_slots))) return rc;
   if ((rc = check_slots(ctx, "pod_slot", b->pod_slot, b->n_pods, ctx->cfg.pod_slots))) return rc;
+  if (b->node_proc_span) {
+    for (uint32_t n = 0; n < N; ++n)
+      for (uint32_t r = b->proc_off[n]; r < b->proc_off[n + 1]; ++r) {
+        const uint32_t sl = b->proc_slot[r] & KACC_SLOT_MASK;
+        if (sl < b->node_proc_span[2 * n] || sl > b->node_proc_span[2 * n + 1])
+          return fail(ctx, KACC_EINVAL, "proc_slot[%u] outside node %u's node_proc_span", r, n);
+      }
+  }
   if (b->node_order) {
     std::vector<uint8_t> seen(N, 0);
     for (uint32_t i = 0; i < N; ++i) {
@@ -1694,6 +1786,7 @@ int kacc_batch_alloc(kacc_ctx *ctx, uint32_t N, uint32_t P, uint32_t C, uint32_t
       {(const void **)&h.node_status, (const void **)&d.node_status, 4ull * N},
       {(const void **)&h.node_cpu_delta, (const void **)&d.node_cpu_delta, 8ull * N},
       {(const void **)&h.node_order, (const void **)&d.node_order, 4ull * N},
+      {(const void **)&h.node_proc_span, (const void **)&d.node_proc_span, 8ull * N},
       {(const void **)&h.zone_energy, (const void **)&d.zone_energy, 8ull * N * Z},
       {(const void **)&h.zone_max, (const void **)&d.zone_max, 8ull * N * Z},
       {(const void **)&h.proc_off, (const void **)&d.proc_off, 4ull * (N + 1)},
@@ -1741,12 +1834,14 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (!bt->host.node_status) dv.node_status = nullptr;
   if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;
   if (!bt->host.node_order) dv.node_order = nullptr;
+  if (!bt->host.node_proc_span) dv.node_proc_span = nullptr;
   for (size_t i = 0; i < bt->bufs.size(); ++i) {
     if (!bt->sizes[i]) continue;
     KACC_HIP(ctx, hipMemcpyAsync(bt->bufs[i].second, bt->bufs[i].first, bt->sizes[i],
                                  hipMemcpyHostToDevice, ctx->stream));
   }
   if ((rc = ensure_items(ctx, dv.n_nodes, dv.n_procs, dv.n_pods)) != KACC_OK) return rc;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
   launch(ctx->cfg.zones, dv, dev_state(ctx), ctx->stream);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
@@ -1815,6 +1910,7 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, con
   if (!off || !slots || !out_energy || !out_power) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
   switch (ctx->cfg.zones) {
     case 1: launch_ns<1>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
     case 2: launch_ns<2>(n_ns, off, slots, ctx, out_energy, out_power, st); break;
@@ -1849,6 +1945,7 @@ int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, 
   if (rc != KACC_OK || b->n_nodes == 0) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
   if (!launch_variant(ctx->cfg.zones, variant, *b, dev_state(ctx), st))
     return fail(ctx, KACC_EINVAL, "variant %d not built for Z=%u", variant, ctx->cfg.zones);
   KACC_HIP(ctx, hipGetLastError());

@@ -64,6 +64,7 @@ struct Args {
   uint64_t *term_key;
   uint32_t *term_slot;
   uint32_t *term_count;
+  uint32_t *out_span;        // optional [2N]: {min, max} slot of the node's rows
   const uint32_t *slot_off;  // [N+1]
   const uint64_t *hoff;      // [N+1] bucket offsets (each node a power of two)
   uint64_t *ent;             // u32 keys: packed (key << 32 | slot); u64 keys: the keys
@@ -217,6 +218,31 @@ __device__ __forceinline__ bool node_view(const Args &a, uint32_t n, NodeView &v
   return true;
 }
 
+// {min, max} over the block (lane values; no row = {1, 0}) -> out_span[2n..]
+__device__ __forceinline__ void span_out(const Args &a, uint32_t n, uint32_t lo, uint32_t hi,
+                                         uint32_t *s_lo, uint32_t *s_hi) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
+    hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_lo[threadIdx.x >> 6] = lo;
+    s_hi[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int w = 1; w < kThreads / 64; ++w) {
+      lo = min(lo, s_lo[w]);
+      hi = max(hi, s_hi[w]);
+    }
+    const bool none = lo > hi;
+    a.out_span[2 * n] = none ? 1u : lo;
+    a.out_span[2 * n + 1] = none ? 0u : hi;
+  }
+}
+
 // ============================ small nodes (LDS) ====================================
 // Table in LDS, rows' keys / slot words in registers (lane owns kRpl
 // consecutive rows), per-slot marks in LDS written with plain stores:
@@ -239,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   __shared__ K s_newkey[kNewCap];
   __shared__ uint8_t s_newbad[kNewCap];
   __shared__ uint32_t s_dirty[kLdsBuckets / 32];
-  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint32_t s_wave[kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
   __shared__ uint32_t s_occ;
 
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
@@ -490,9 +516,16 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     }
   }
   uint32_t *__restrict__ out = a.out_slot + v.r0;
+  uint32_t lo = 0xffffffffu, hi = 0u;
 #pragma unroll
-  for (int j = 0; j < kRpl; ++j)
+  for (int j = 0; j < kRpl; ++j) {
     if (tid * kRpl + j < R) out[tid * kRpl + j] = res[j];
+    if (res[j] != kInvalid) {
+      lo = min(lo, res[j] & KACC_SLOT_MASK);
+      hi = max(hi, res[j] & KACC_SLOT_MASK);
+    }
+  }
+  if (a.out_span) span_out(a, n, lo, hi, s_lo, s_hi);
 }
 
 // ============================ big nodes (global table) =============================
@@ -505,7 +538,7 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
   __shared__ uint32_t s_seen[kWords];  // slots of rows found
   __shared__ uint32_t s_wpre[kWords];  // free slots before word w
   __shared__ uint32_t s_tpre[kWords];  // terminated before word w
-  __shared__ uint32_t s_wave[kThreads / 64];
+  __shared__ uint32_t s_wave[kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
   __shared__ uint32_t s_occ;
 
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
@@ -667,6 +700,16 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
       if (w != kInvalid) pr.insert(keys[r], (w & KACC_SLOT_MASK) - s0);
     }
   }
+  if (a.out_span) {
+    uint32_t lo = 0xffffffffu, hi = 0u;
+    for (uint32_t r = r0 + tid; r < r1; r += kThreads) {
+      const uint32_t w = a.out_slot[r];
+      if (w == kInvalid) continue;
+      lo = min(lo, w & KACC_SLOT_MASK);
+      hi = max(hi, w & KACC_SLOT_MASK);
+    }
+    span_out(a, n, lo, hi, s_lo, s_hi);
+  }
 }
 
 }  // namespace join
@@ -676,7 +719,8 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
 // C ABI
 // =============================================================================
 struct kacc_slotmap {
-  kacc_ctx *ctx = nullptr;
+  kacc_ctx *ctx = nullptr;  // for errors and the default stream while the context lives
+  int device = 0;           // destroy must not touch ctx (it may be gone already)
   kacc_kind kind = KACC_KIND_PROC;
   uint32_t n_nodes = 0;
   uint64_t buckets = 0;
@@ -734,6 +778,7 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   auto *m = new kacc_slotmap;
   m->ctx = ctx;
+  m->device = ctx->device;
   m->kind = kind;
   m->n_nodes = n_nodes;
   m->buckets = hoff[n_nodes];
@@ -766,8 +811,8 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
 
 void kacc_slotmap_destroy(kacc_slotmap *m) {
   if (!m) return;
-  (void)hipSetDevice(m->ctx->device);
-  (void)hipStreamSynchronize(m->ctx->stream);
+  (void)hipSetDevice(m->device);
+  (void)hipDeviceSynchronize();  // no launch of this map may still be running
   (void)hipFree(m->d_slot_off);
   (void)hipFree(m->d_hoff);
   (void)hipFree(m->d_ent);
@@ -787,27 +832,29 @@ int kacc_slotmap_reset(kacc_slotmap *m) {
 
 static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                      const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                     uint32_t *term_slot, uint32_t *term_count, void *stream, uint32_t stop_after);
+                     uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream,
+                     uint32_t stop_after);
 
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                   uint32_t *term_slot, uint32_t *term_count, void *stream) {
+                   uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream) {
   return slot_join(m, n_rows, row_off, keys, node_status, out_slot, term_key, term_slot, term_count,
-                   stream, 0u);
+                   out_span, stream, 0u);
 }
 
 int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                             uint32_t *out_slot, uint64_t *term_key, uint32_t *term_slot,
                             uint32_t *term_count, void *stream, uint32_t stop_after) {
   return slot_join(m, n_rows, row_off, keys, nullptr, out_slot, term_key, term_slot, term_count,
-                   stream, stop_after);
+                   nullptr, stream, stop_after);
 }
 
 }  // extern "C"
 
 static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                      const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
-                     uint32_t *term_slot, uint32_t *term_count, void *stream, uint32_t stop_after) {
+                     uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream,
+                     uint32_t stop_after) {
   if (!m) return KACC_EINVAL;
   kacc_ctx *ctx = m->ctx;
   if (!m->n_nodes) return KACC_OK;
@@ -827,11 +874,13 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   a.term_key = term_key;
   a.term_slot = term_slot;
   a.term_count = term_count;
+  a.out_span = out_span;
   a.slot_off = m->d_slot_off;
   a.hoff = m->d_hoff;
   a.ent = m->d_ent;
   a.slots = m->d_slots;
   a.err = ctx->d_err;
+  (void)hipGetLastError();  // a stale error of an earlier call must not be blamed on this launch
   using namespace kacc::join;
   const dim3 grid(m->n_nodes), block(kThreads);
   if (m->kind == KACC_KIND_PROC) {

@@ -90,6 +90,18 @@ class FleetLayout:
             pod_slots=max(int(self.pod_slot.max(initial=0)) + 1, 1),
         )
 
+    def proc_span(self) -> np.ndarray:
+        """node_proc_span [2N]: {min, max} process slot per node ({1, 0} when empty)."""
+        out = np.zeros(2 * self.n_nodes, dtype=np.uint32)
+        rows = np.diff(self.proc_off.astype(np.int64))
+        nz = rows > 0
+        starts = self.proc_off[:-1][nz].astype(np.int64)
+        out[0::2][~nz], out[1::2][~nz] = 1, 0
+        if nz.any():
+            out[0::2][nz] = np.minimum.reduceat(self.proc_slot, starts)
+            out[1::2][nz] = np.maximum.reduceat(self.proc_slot, starts)
+        return out
+
     def fast_flag(self) -> int:
         """KACC_F_FAST_NODES when every node fits the fast path, else 0."""
         from .accel import KACC_F_FAST_NODES, KACC_FAST_MAX_AGGREGATES, KACC_FAST_MAX_PROCS
@@ -139,7 +151,13 @@ def _split(rng, totals: np.ndarray, parts: np.ndarray) -> np.ndarray:
 def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
                 ctr_frac: float = 0.79, procs_per_ctr: int = 8, vm_frac: float = 0.01,
                 procs_per_vm: int = 1, ctrs_per_pod: float = 2.5, pod_frac: float = 0.9,
-                n_namespaces: Optional[int] = None, shuffle_slots: bool = False) -> FleetLayout:
+                n_namespaces: Optional[int] = None, shuffle_slots: bool = False,
+                fragment_slots: float = 0.0) -> FleetLayout:
+    """Synthetic fleet.  Process slots: consecutive per node (default), a global
+    permutation (``shuffle_slots``), or, with ``fragment_slots`` = f > 0, each
+    node's processes on a random subset of its own slot range of (1 + f) x rows
+    in random order — the steady state the slot join reaches under churn.
+    """
     rng = np.random.default_rng(seed)
     P = np.broadcast_to(np.asarray(procs_per_node, dtype=np.int64), (n_nodes,)).copy()
     Vp = np.floor(P * vm_frac).astype(np.int64)  # VM processes
@@ -173,7 +191,14 @@ def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
     pod_ctr_end = ctr_off[node_of_pod] + (qsum - pod_base)
 
     n_procs, n_ctrs, n_vms, n_pods = int(proc_off[-1]), int(ctr_off[-1]), int(vm_off[-1]), int(pod_off[-1])
-    if shuffle_slots:
+    if fragment_slots > 0:
+        rng_f = np.random.default_rng(seed ^ 0xF4A6)
+        cap = (P * (1.0 + fragment_slots)).astype(np.int64) + 1
+        slot_base = np.concatenate([[0], np.cumsum(cap)[:-1]])
+        proc_slot = np.concatenate([slot_base[n] + rng_f.permutation(int(cap[n]))[: int(P[n])]
+                                    for n in range(n_nodes)]) if n_procs else np.zeros(0, np.int64)
+        ctr_slot, vm_slot, pod_slot = np.arange(n_ctrs), np.arange(n_vms), np.arange(n_pods)
+    elif shuffle_slots:
         proc_slot = rng.permutation(n_procs)
         ctr_slot = rng.permutation(n_ctrs)
         vm_slot = rng.permutation(n_vms)
@@ -230,15 +255,19 @@ def layout_from_sizes(zones: int, nodes, seed: int = SEED, shuffle_slots: bool =
     )
 
 
-def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None) -> FleetLayout:
-    """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed)."""
+def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
+                  fragment_slots: float = 0.0) -> FleetLayout:
+    """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed).
+
+    ``fragment_slots`` > 0 places each node's processes on a random subset of
+    its own slot range (the slot join's steady state under churn)."""
     if config == 1:  # single node, 500 procs -> 50 containers -> 20 pods, package+dram
         return make_layout(1, 500, 2, seed, ctr_frac=0.8, procs_per_ctr=8, ctrs_per_pod=2.5,
                            pod_frac=1.0, n_namespaces=4)
     if config == 2:
-        return make_layout(nodes or 1000, 1000, 2, seed)
+        return make_layout(nodes or 1000, 1000, 2, seed, fragment_slots=fragment_slots)
     if config in (3, 4):
-        return make_layout(nodes or 10000, 2000, 4, seed)
+        return make_layout(nodes or 10000, 2000, 4, seed, fragment_slots=fragment_slots)
     if config == 5:
         rng = np.random.default_rng(seed ^ 5)
         n = nodes or 1000

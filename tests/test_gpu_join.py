@@ -36,6 +36,7 @@ class GpuJoin:
         self.tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
         self.ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
         self.cnt = torch.zeros(max(len(slot_off) - 1, 1), dtype=torch.int32, device="cuda")
+        self.span = torch.zeros(2 * max(len(slot_off) - 1, 1), dtype=torch.int32, device="cuda")
 
     def join(self, row_off, keys, status=None, out=None, sync=True):
         d_off = torch.from_numpy(row_off.astype(np.int32)).cuda()
@@ -49,11 +50,19 @@ class GpuJoin:
             out = torch.zeros(max(n_rows, 1), dtype=torch.int32, device="cuda")
         s = current_stream_handle()
         self.m.join(n_rows, d_off.data_ptr(), d_keys.data_ptr(), 0 if d_st is None else d_st.data_ptr(),
-                    out.data_ptr(), self.tk.data_ptr(), self.ts.data_ptr(), self.cnt.data_ptr(), s)
+                    out.data_ptr(), self.tk.data_ptr(), self.ts.data_ptr(), self.cnt.data_ptr(), s,
+                    self.span.data_ptr())
         if not sync:
             return out
         self.acc.sync(s)
         got = out[:n_rows].cpu().numpy().view(np.uint32)
+        span = self.span.cpu().numpy().view(np.uint32)
+        for n in range(len(self.slot_off) - 1):  # {min, max} slot of the node's rows
+            if status is not None and status[n]:
+                continue
+            w = got[row_off[n]:row_off[n + 1]] & 0x7FFFFFFF
+            want = (int(w.min()), int(w.max())) if w.size else (1, 0)
+            assert (int(span[2 * n]), int(span[2 * n + 1])) == want, n
         tk = self.tk.cpu().numpy().view(np.uint64)
         ts = self.ts.cpu().numpy().view(np.uint32)
         term = []  # node segments, ascending by slot
@@ -149,6 +158,7 @@ def test_join_feeds_interval_bit_exact():
         t = to_device(a)
         out = t["proc_slot"]  # the join writes the batch's slot words in place
         gpu.join(layout.proc_off, keys, a["node_status"], out=out, sync=False)
+        t["node_proc_span"] = gpu.span  # rows swept in slot order
         acc.run_interval(interval_from_tensors(t, sizes, layout.fast_flag()), stream)
         acc.sync(stream)
         ora.interval(a_ora, sizes)

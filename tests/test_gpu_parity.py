@@ -79,7 +79,7 @@ def test_golden_fleet_bit_exact():
             np.testing.assert_array_equal(be.table(name), want, err_msg=f"interval {k} {name}")
 
 
-def run_both(layout, sim_kwargs, n_intervals, node_order=False, seed=1):
+def run_both(layout, sim_kwargs, n_intervals, node_order=False, seed=1, span=False):
     from oracle.oracle import KOR_SUM_LISTING, Oracle
 
     caps = layout.capacities()
@@ -91,6 +91,8 @@ def run_both(layout, sim_kwargs, n_intervals, node_order=False, seed=1):
         a = sim.next_interval()
         if node_order:
             a["node_order"] = layout.node_order_heaviest_first()
+        if span:  # the slot join's per-node spans: rows moved in slot order
+            a["node_proc_span"] = layout.proc_span()
         eng.interval(a, layout.sizes(), layout.fast_flag())  # skip empty big-node launches when possible
         ora.interval(a, layout.sizes())
         lst.interval(a, layout.sizes())
@@ -111,7 +113,14 @@ FLEETS = [
     ("z4-rows-boundary", dict(n_nodes=6, procs_per_node=[2047, 2048, 2049, 4096, 1, 0], zones=4)),
     ("z2-many-aggregates", dict(n_nodes=5, procs_per_node=[600, 700, 800, 2000, 300], zones=2,
                                 procs_per_ctr=1, ctrs_per_pod=1.0, vm_frac=0.05)),
+    # fragmented per-node slot ranges (the slot join's steady state), swept in slot order
+    ("z4-fragmented", dict(n_nodes=12, procs_per_node=[2000, 1999, 1500, 64, 1, 0, 2005, 700, 3, 2040, 100, 1024],
+                           zones=4, fragment_slots=0.02)),
+    ("z4-fragmented-wide", dict(n_nodes=6, procs_per_node=[1600, 1200, 500, 17, 2048, 1000], zones=4,
+                                fragment_slots=0.3)),
+    ("z8-fragmented", dict(n_nodes=5, procs_per_node=[511, 300, 64, 1, 200], zones=8, fragment_slots=0.5)),
 ]
+SPAN_FLEETS = {"z4-fragmented", "z4-fragmented-wide", "z8-fragmented", "z4-config3-like", "z3-odd"}
 
 
 def test_fast_flag_rejects_oversized_node():
@@ -127,10 +136,24 @@ def test_fast_flag_rejects_oversized_node():
     eng.interval(a, layout.sizes(), 0)
 
 
+def test_row_outside_span_is_reported():
+    """A row whose slot lies outside its node's node_proc_span raises KACC_ERANGE."""
+    layout = fleet.make_layout(2, [300, 200], 4, seed=3, fragment_slots=0.1)
+    eng = EngineBackend(layout.zones, layout.capacities())
+    a = fleet.FleetSim(layout, seed=3).next_interval()
+    span = layout.proc_span()
+    span[1] = span[0] + 10  # node 0's span too narrow
+    a["node_proc_span"] = span
+    with pytest.raises(accel.AccelError) as ei:
+        eng.interval(a, layout.sizes(), layout.fast_flag())
+    assert ei.value.code == accel.KACC_ERANGE
+
+
 @pytest.mark.parametrize("name,kw", FLEETS, ids=[f[0] for f in FLEETS])
 def test_random_fleet_bit_exact(name, kw):
     layout = fleet.make_layout(seed=11, **kw)
-    eng, ora, lst = run_both(layout, dict(churn=0.03, zero_ratio_frac=0.05, read_error_frac=0.05), 4)
+    eng, ora, lst = run_both(layout, dict(churn=0.03, zero_ratio_frac=0.05, read_error_frac=0.05), 4,
+                             span=name in SPAN_FLEETS)
     # listing-order (Go map order) oracle: <= 1e-12 relative on the node totals,
     # <= 1 µJ per workload energy
     nd_e, nd_l = eng.table("node_cpu_delta"), lst.state["node_cpu_delta"]

@@ -58,11 +58,13 @@ def main():
     tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
     ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(layout.n_nodes, dtype=torch.int32, device="cuda")
+    span = torch.zeros(2 * layout.n_nodes, dtype=torch.int32, device="cuda")
+    t["node_proc_span"] = span  # the join's per-node slot spans: rows swept in slot order
     P = sizes["n_procs"]
 
     def join(k):
         sm.join(P, off.data_ptr(), key_sets[k].data_ptr(), 0, t["proc_slot"].data_ptr(), tk.data_ptr(),
-                ts.data_ptr(), cnt.data_ptr(), stream)
+                ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
 
     flag = layout.fast_flag()
     join(n_sets)  # first interval: every ID new

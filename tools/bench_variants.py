@@ -32,7 +32,8 @@ def main():
     torch.cuda.set_device(0)
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
-    layout = fleet.config_layout(cfg)
+    frag = float(os.environ.get("FRAG", "0"))  # slot fragmentation (+ node_proc_span)
+    layout = fleet.config_layout(cfg, fragment_slots=frag)
     sim = fleet.FleetSim(layout)
     acc = accel.Accel(layout.zones, **layout.capacities())
     stream = current_stream_handle()
@@ -42,6 +43,10 @@ def main():
     # distinct input sets cycled like bench.py (no cache reuse between launches)
     n_distinct = int(os.environ.get("DISTINCT", "4"))
     dev = [to_device(sim.next_interval()) for _ in range(n_distinct)]
+    if frag > 0 and not os.environ.get("NO_SPAN"):
+        span = to_device({"s": layout.proc_span()})["s"]
+        for d in dev:
+            d["node_proc_span"] = span
     flag = 0 if os.environ.get("KACC_LIB") else layout.fast_flag()  # older builds reject the flag
     ivs = [interval_from_tensors(a, layout.sizes(), flag) for a in dev]
     it = ivs[0]
