@@ -301,6 +301,45 @@ int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, co
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                    uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream);
 
+/* ---- terminated-workload tracker ----------------------
+ * TerminatedResourceTracker (internal/monitor/terminated_resource_tracker.go)
+ * for one workload kind, on the device: the top max_size terminated workloads
+ * by their final energy in the target zone (the meter's primary zone,
+ * monitor.go:123-144): max_size 0 disables (:82), an ID already tracked is
+ * ignored (:90), energy below min_energy is dropped (:102), below capacity an
+ * item is pushed (:116), at capacity it must beat the minimum (:124);
+ * Clear() after an export (process.go:80-84).
+ *
+ * kacc_tracker_add() takes one interval's terminated workloads — the per-node
+ * segments of kacc_slot_join — and reads their final values from the kind's
+ * state tables (the slots are not reused before the next join).  A batch is
+ * added as Go's loop over procs.Terminated (process.go:89-99) would add it in
+ * the map order "descending target-zone energy, then node, then slot"; Go's
+ * map order is unspecified, and for any batch whose energies differ at the
+ * retention boundary the retained set is the same for every order.  Ties at
+ * the boundary keep items already tracked first (Go's heap requires a strictly
+ * higher energy to evict), then the batch order.  Tracked items are frozen
+ * copies (energy and power per zone), as Add(prev.Clone()) keeps.           */
+typedef struct kacc_tracker kacc_tracker;
+#define KACC_TRACKER_MAX_BOUNDED 8192u /* largest max_size > 0 supported */
+/* max_size: > 0 top-N (<= KACC_TRACKER_MAX_BOUNDED), 0 disabled, < 0 unlimited
+ * (at most `capacity` items, more raise ERANGE).  zone: target zone index in
+ * the kind's [slot*Z + z] tables.  min_energy: minEnergyThreshold in µJ.     */
+int kacc_tracker_create(kacc_ctx *ctx, kacc_kind kind, int64_t max_size, uint32_t capacity,
+                        uint32_t zone, uint64_t min_energy, kacc_tracker **out);
+void kacc_tracker_destroy(kacc_tracker *t); /* safe before or after kacc_destroy(ctx) */
+int kacc_tracker_clear(kacc_tracker *t, void *stream);
+/* m: the slot map whose kacc_slot_join produced term_key / term_slot /
+ * term_count (device pointers); asynchronous on `stream`.                    */
+int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *term_key,
+                     const uint32_t *term_slot, const uint32_t *term_count, void *stream);
+/* Items(): synchronous.  *count = tracked items; when the arrays are non-NULL
+ * (HOST, sized >= *count; energy/power [*count * Z]) they receive key, node,
+ * and the frozen per-zone energy (µJ) and power (µW); highest energy first
+ * (bounded trackers and unlimited ones holding <= 8192 items).              */
+int kacc_tracker_items(kacc_tracker *t, uint32_t *count, uint64_t *key, uint32_t *node,
+                       uint64_t *energy, double *power);
+
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

@@ -73,6 +73,11 @@ TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)
 EXPORTS = [
+    "kacc_tracker_create",
+    "kacc_tracker_destroy",
+    "kacc_tracker_clear",
+    "kacc_tracker_add",
+    "kacc_tracker_items",
     "kacc_slotmap_create",
     "kacc_slotmap_destroy",
     "kacc_slotmap_reset",
@@ -220,6 +225,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
+    lib.kacc_tracker_create.argtypes = [c_void_p, c_int, ctypes.c_int64, c_uint32, c_uint32, c_uint64,
+                                        POINTER(c_void_p)]
+    lib.kacc_tracker_destroy.argtypes = [c_void_p]
+    lib.kacc_tracker_destroy.restype = None
+    lib.kacc_tracker_clear.argtypes = [c_void_p, c_void_p]
+    lib.kacc_tracker_add.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kacc_tracker_items.argtypes = [c_void_p, POINTER(c_uint32), c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kacc_slotmap_create.argtypes = [c_void_p, c_int, c_uint32, c_void_p, POINTER(c_void_p)]
     lib.kacc_slotmap_destroy.argtypes = [c_void_p]
     lib.kacc_slotmap_destroy.restype = None
@@ -387,6 +399,53 @@ class SlotMap:
     def close(self) -> None:
         if self.handle:
             self.lib.kacc_slotmap_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Tracker:
+    """Device TerminatedResourceTracker of one kind (kacc_tracker_*)."""
+
+    def __init__(self, accel: Accel, kind: int, max_size: int, zone: int, min_energy: int, capacity: int = 0):
+        self.accel = accel
+        self.lib = accel.lib
+        self.zones = accel.zones
+        h = c_void_p()
+        accel._check(self.lib.kacc_tracker_create(accel.ctx, kind, max_size, capacity, zone, min_energy,
+                                                  ctypes.byref(h)))
+        self.handle = h
+
+    def clear(self, stream: int = 0) -> None:
+        self.accel._check(self.lib.kacc_tracker_clear(self.handle, c_void_p(stream or None)))
+
+    def add(self, slotmap: "SlotMap", term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int,
+            stream: int = 0) -> None:
+        self.accel._check(self.lib.kacc_tracker_add(self.handle, slotmap.handle, c_void_p(term_key_ptr),
+                                                    c_void_p(term_slot_ptr), c_void_p(term_count_ptr),
+                                                    c_void_p(stream or None)))
+
+    def items(self):
+        """(key u64[n], node u32[n], energy u64[n, Z], power f64[n, Z]), highest energy first."""
+        n = c_uint32()
+        self.accel._check(self.lib.kacc_tracker_items(self.handle, ctypes.byref(n), None, None, None, None))
+        k = np.zeros(max(n.value, 1), np.uint64)
+        nd = np.zeros(max(n.value, 1), np.uint32)
+        e = np.zeros((max(n.value, 1), self.zones), np.uint64)
+        p = np.zeros((max(n.value, 1), self.zones), np.float64)
+        m = c_uint32()
+        self.accel._check(self.lib.kacc_tracker_items(self.handle, ctypes.byref(m), k.ctypes.data, nd.ctypes.data,
+                                                      e.ctypes.data, p.ctypes.data))
+        c = m.value
+        return k[:c], nd[:c], e[:c], p[:c]
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.kacc_tracker_destroy(self.handle)
             self.handle = None
 
     def __del__(self):  # pragma: no cover

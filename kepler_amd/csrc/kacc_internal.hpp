@@ -37,6 +37,21 @@ struct kacc_batch {
   std::vector<size_t> sizes;
 };
 
+// Slot map of one workload kind (kacc_join.hip).
+struct kacc_slotmap {
+  kacc_ctx *ctx = nullptr;  // for errors and the default stream while the context lives
+  int device = 0;           // destroy must not touch ctx (it may be gone already)
+  kacc_kind kind = KACC_KIND_PROC;
+  uint32_t n_nodes = 0;
+  uint32_t total_slots = 0;  // slot_off[n_nodes]
+  uint64_t buckets = 0;
+  uint32_t *d_slot_off = nullptr;
+  uint64_t *d_hoff = nullptr;
+  bool has_big = false;         // some node's table exceeds the LDS size
+  uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
+  uint32_t *d_slots = nullptr;  // 64-bit IDs only
+};
+
 // Records the message on ctx (or the thread's create error when ctx is NULL)
 // and returns code.
 int kacc_fail(kacc_ctx *ctx, int code, const char *fmt, ...) __attribute__((format(printf, 3, 4)));

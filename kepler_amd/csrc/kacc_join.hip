@@ -718,18 +718,6 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
 // =============================================================================
 // C ABI
 // =============================================================================
-struct kacc_slotmap {
-  kacc_ctx *ctx = nullptr;  // for errors and the default stream while the context lives
-  int device = 0;           // destroy must not touch ctx (it may be gone already)
-  kacc_kind kind = KACC_KIND_PROC;
-  uint32_t n_nodes = 0;
-  uint64_t buckets = 0;
-  uint32_t *d_slot_off = nullptr;
-  uint64_t *d_hoff = nullptr;
-  bool has_big = false;         // some node's table exceeds the LDS size
-  uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
-  uint32_t *d_slots = nullptr;  // 64-bit IDs only
-};
 
 namespace {
 
@@ -781,6 +769,7 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
   m->device = ctx->device;
   m->kind = kind;
   m->n_nodes = n_nodes;
+  m->total_slots = n_nodes ? slot_off[n_nodes] : 0;
   m->buckets = hoff[n_nodes];
   m->has_big = has_big;
   auto bail = [&](hipError_t e) {

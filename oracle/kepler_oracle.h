@@ -93,6 +93,19 @@ int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, cons
                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                   uint32_t *term_slot, uint32_t *term_count);
 
+/* TerminatedResourceTracker restatement (kor_tracker.cpp), Go's heap exactly.
+ * add_one = one Add(); add_batch = a batch in kacc_tracker_add's order.     */
+typedef struct kor_tracker kor_tracker;
+kor_tracker *kor_tracker_create(int64_t max_size, uint64_t min_energy, uint32_t zones, uint32_t zone);
+void kor_tracker_destroy(kor_tracker *t);
+void kor_tracker_clear(kor_tracker *t);
+void kor_tracker_add_one(kor_tracker *t, uint32_t node, uint64_t key, const uint64_t *energy,
+                         const double *power);
+void kor_tracker_add_batch(kor_tracker *t, uint32_t n, const uint32_t *node, const uint64_t *key,
+                           const uint32_t *slot, const uint64_t *tab_e, const double *tab_p);
+uint32_t kor_tracker_items(const kor_tracker *t, uint64_t *key, uint32_t *node, uint64_t *energy,
+                           double *power);
+
 #ifdef __cplusplus
 }
 #endif

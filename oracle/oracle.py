@@ -62,6 +62,18 @@ def load():
     lib.kor_slotmap_destroy.restype = None
     lib.kor_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p]
+    lib.kor_tracker_create.argtypes = [ctypes.c_int64, c_uint64, c_uint32, c_uint32]
+    lib.kor_tracker_create.restype = c_void_p
+    lib.kor_tracker_destroy.argtypes = [c_void_p]
+    lib.kor_tracker_destroy.restype = None
+    lib.kor_tracker_clear.argtypes = [c_void_p]
+    lib.kor_tracker_clear.restype = None
+    lib.kor_tracker_add_one.argtypes = [c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]
+    lib.kor_tracker_add_one.restype = None
+    lib.kor_tracker_add_batch.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kor_tracker_add_batch.restype = None
+    lib.kor_tracker_items.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.kor_tracker_items.restype = c_uint32
     lib.kor_gf_create.argtypes = [c_uint32]
     lib.kor_gf_create.restype = c_void_p
     lib.kor_gf_destroy.argtypes = [c_void_p]
@@ -207,5 +219,48 @@ class OracleSlotMap:
     def __del__(self):  # pragma: no cover
         try:
             self.lib.kor_slotmap_destroy(self.h)
+        except Exception:
+            pass
+
+
+class OracleTracker:
+    """TerminatedResourceTracker with Go's container/heap (oracle/kor_tracker.cpp)."""
+
+    def __init__(self, max_size: int, min_energy: int, zones: int, zone: int = 0):
+        self.lib = load()
+        self.zones = zones
+        self.h = self.lib.kor_tracker_create(max_size, min_energy, zones, zone)
+
+    def clear(self):
+        self.lib.kor_tracker_clear(self.h)
+
+    def add_one(self, node: int, key: int, energy, power=None):
+        e = np.ascontiguousarray(energy, dtype=np.uint64)
+        p = np.zeros(self.zones) if power is None else np.ascontiguousarray(power, dtype=np.float64)
+        self.lib.kor_tracker_add_one(self.h, node, key, e.ctypes.data, p.ctypes.data)
+
+    def add_batch(self, node, key, slot, tab_e, tab_p):
+        node = np.ascontiguousarray(node, dtype=np.uint32)
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        slot = np.ascontiguousarray(slot, dtype=np.uint32)
+        tab_e = np.ascontiguousarray(tab_e, dtype=np.uint64)
+        tab_p = np.ascontiguousarray(tab_p, dtype=np.float64)
+        if node.size:
+            self.lib.kor_tracker_add_batch(self.h, node.size, node.ctypes.data, key.ctypes.data, slot.ctypes.data,
+                                           tab_e.ctypes.data, tab_p.ctypes.data)
+
+    def items(self):
+        """(key, node, energy [n, Z], power [n, Z]) sorted by (node, key)."""
+        n = self.lib.kor_tracker_items(self.h, None, None, None, None)
+        k = np.zeros(max(n, 1), np.uint64)
+        nd = np.zeros(max(n, 1), np.uint32)
+        e = np.zeros((max(n, 1), self.zones), np.uint64)
+        p = np.zeros((max(n, 1), self.zones), np.float64)
+        self.lib.kor_tracker_items(self.h, k.ctypes.data, nd.ctypes.data, e.ctypes.data, p.ctypes.data)
+        return k[:n], nd[:n], e[:n], p[:n]
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.lib.kor_tracker_destroy(self.h)
         except Exception:
             pass
