@@ -340,6 +340,25 @@ int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *ter
 int kacc_tracker_items(kacc_tracker *t, uint32_t *count, uint64_t *key, uint32_t *node,
                        uint64_t *energy, double *power);
 
+/* ---- multi-socket aggregated zones ---------------------
+ * device.AggregatedZone (internal/device/energy_zone.go:47-148) for every
+ * (node, zone) of the fleet, each made of `sockets` sub-zones (package-0,
+ * package-1, ... of a multi-socket node).  sub_max: HOST [n_nodes*Z*sockets]
+ * MaxEnergy() of each sub-zone, summed (saturating) at creation as
+ * NewAggregatedZone caches it (:55-67).                                      */
+typedef struct kacc_zone_agg kacc_zone_agg;
+int kacc_zone_agg_create(kacc_ctx *ctx, uint32_t n_nodes, uint32_t sockets, const uint64_t *sub_max,
+                         kacc_zone_agg **out);
+void kacc_zone_agg_destroy(kacc_zone_agg *z); /* safe before or after kacc_destroy(ctx) */
+/* One Energy() per aggregated zone (device pointers, async on `stream`):
+ * readings [n_nodes*Z*sockets] sub-zone counters, [node][zone][socket];
+ * sub_status (optional, same shape) nonzero = that sub-zone's read failed:
+ * the zone's Energy() returns the error there (:104-108), the node's interval
+ * fails: KACC_NODE_READ_ERROR is ORed into node_status [n_nodes].  Outputs
+ * out_energy / out_max [n_nodes*Z] = the batch's zone_energy / zone_max.      */
+int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_t *sub_status,
+                       uint64_t *out_energy, uint64_t *out_max, uint32_t *node_status, void *stream);
+
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

@@ -73,6 +73,9 @@ TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)
 EXPORTS = [
+    "kacc_zone_agg_create",
+    "kacc_zone_agg_destroy",
+    "kacc_zone_agg_read",
     "kacc_tracker_create",
     "kacc_tracker_destroy",
     "kacc_tracker_clear",
@@ -225,6 +228,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
+    lib.kacc_zone_agg_create.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, POINTER(c_void_p)]
+    lib.kacc_zone_agg_destroy.argtypes = [c_void_p]
+    lib.kacc_zone_agg_destroy.restype = None
+    lib.kacc_zone_agg_read.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kacc_tracker_create.argtypes = [c_void_p, c_int, ctypes.c_int64, c_uint32, c_uint32, c_uint64,
                                         POINTER(c_void_p)]
     lib.kacc_tracker_destroy.argtypes = [c_void_p]
@@ -399,6 +406,35 @@ class SlotMap:
     def close(self) -> None:
         if self.handle:
             self.lib.kacc_slotmap_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ZoneAgg:
+    """Device AggregatedZone for every (node, zone) of a fleet (kacc_zone_agg_*)."""
+
+    def __init__(self, accel: Accel, n_nodes: int, sockets: int, sub_max: np.ndarray):
+        self.accel = accel
+        self.lib = accel.lib
+        m = np.ascontiguousarray(sub_max, dtype=np.uint64)
+        h = c_void_p()
+        accel._check(self.lib.kacc_zone_agg_create(accel.ctx, n_nodes, sockets, m.ctypes.data, ctypes.byref(h)))
+        self.handle = h
+
+    def read(self, readings_ptr: int, sub_status_ptr: int, out_energy_ptr: int, out_max_ptr: int,
+             node_status_ptr: int, stream: int = 0) -> None:
+        self.accel._check(self.lib.kacc_zone_agg_read(
+            self.handle, c_void_p(readings_ptr), c_void_p(sub_status_ptr or None), c_void_p(out_energy_ptr),
+            c_void_p(out_max_ptr), c_void_p(node_status_ptr), c_void_p(stream or None)))
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.kacc_zone_agg_destroy(self.handle)
             self.handle = None
 
     def __del__(self):  # pragma: no cover

@@ -342,6 +342,36 @@ uint64_t kor_aggregated_energy(uint32_t n, const uint64_t *reading, const uint64
   return *current;
 }
 
+// The same with per-sub-zone read errors: Energy() returns the error at the
+// first failing sub-zone (energy_zone.go:104-108) after updating the last
+// readings of the sub-zones before it; the aggregate is not updated.
+int kor_aggregated_energy_st(uint32_t n, const uint64_t *reading, const uint32_t *status,
+                             const uint64_t *sub_max, uint64_t *last, uint8_t *seen, uint64_t *current,
+                             uint64_t agg_max, uint64_t *out) {
+  uint64_t total_delta = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (status && status[i]) return KACC_ERANGE;
+    if (seen[i]) {
+      uint64_t delta;
+      if (reading[i] >= last[i])
+        delta = reading[i] - last[i];
+      else if (sub_max[i] > 0)
+        delta = (sub_max[i] - last[i]) + reading[i];
+      else
+        delta = reading[i] - last[i];
+      total_delta += delta;
+    } else {
+      total_delta += reading[i];
+    }
+    last[i] = reading[i];
+    seen[i] = 1;
+  }
+  *current += total_delta;
+  if (agg_max > 0) *current %= agg_max;
+  *out = *current;
+  return KACC_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -71,6 +71,11 @@ uint64_t kor_aggregated_max(uint32_t n, const uint64_t *sub_max);
 uint64_t kor_aggregated_energy(uint32_t n, const uint64_t *reading, const uint64_t *sub_max,
                                uint64_t *last, uint8_t *seen, uint64_t *current,
                                uint64_t agg_max);
+/* With per-sub-zone read errors (status nonzero): returns KACC_ERANGE at the
+ * first failing sub-zone, as Energy() returns its error; else 0 and *out.   */
+int kor_aggregated_energy_st(uint32_t n, const uint64_t *reading, const uint32_t *status,
+                             const uint64_t *sub_max, uint64_t *last, uint8_t *seen, uint64_t *current,
+                             uint64_t agg_max, uint64_t *out);
 
 /* Go-faithful CPU baseline: the same interval computed with the reference's
  * data structures (string-keyed maps of heap objects with per-object zone

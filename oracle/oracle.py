@@ -74,6 +74,8 @@ def load():
     lib.kor_tracker_add_batch.restype = None
     lib.kor_tracker_items.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kor_tracker_items.restype = c_uint32
+    lib.kor_aggregated_energy_st.argtypes = [c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_uint64, c_void_p]
     lib.kor_gf_create.argtypes = [c_uint32]
     lib.kor_gf_create.restype = c_void_p
     lib.kor_gf_destroy.argtypes = [c_void_p]
@@ -181,6 +183,37 @@ class AggregatedZone:
         return int(self.lib.kor_aggregated_energy(self.n, r.ctypes.data, self.sub_max.ctypes.data,
                                                   self.last.ctypes.data, self.seen.ctypes.data,
                                                   self.current.ctypes.data, self.max))
+
+
+class OracleZoneAgg:
+    """AggregatedZone for every (node, zone) of a fleet: sub-zones [N*Z*S] (oracle)."""
+
+    def __init__(self, n_nodes: int, zones: int, sockets: int, sub_max):
+        self.nz, self.S = n_nodes * zones, sockets
+        self.Z = zones
+        m = np.ascontiguousarray(sub_max, dtype=np.uint64).reshape(self.nz, sockets)
+        self.zones = [AggregatedZone(m[i]) for i in range(self.nz)]
+
+    def read(self, readings, sub_status=None):
+        """Returns (energy [N*Z], max [N*Z], node_status [N] with read errors)."""
+        lib = load()
+        r = np.ascontiguousarray(readings, dtype=np.uint64).reshape(self.nz, self.S)
+        st = None if sub_status is None else np.ascontiguousarray(sub_status, dtype=np.uint32).reshape(self.nz, self.S)
+        e = np.zeros(self.nz, np.uint64)
+        mx = np.array([z.max for z in self.zones], dtype=np.uint64)
+        ns = np.zeros(self.nz // self.Z, np.uint32)
+        for i, z in enumerate(self.zones):
+            out = np.zeros(1, np.uint64)
+            ri = np.ascontiguousarray(r[i])
+            si = None if st is None else np.ascontiguousarray(st[i])
+            rc = lib.kor_aggregated_energy_st(self.S, ri.ctypes.data, None if si is None else si.ctypes.data,
+                                              z.sub_max.ctypes.data, z.last.ctypes.data, z.seen.ctypes.data,
+                                              z.current.ctypes.data, z.max, out.ctypes.data)
+            if rc != 0:
+                ns[i // self.Z] |= 1
+            else:
+                e[i] = out[0]
+        return e, mx, ns
 
 
 class OracleSlotMap:

@@ -92,3 +92,21 @@ def test_golden_fleet_reproduces(oracle_lib):
         o.interval(ins, sizes)
         for name, want in outs.items():
             np.testing.assert_array_equal(o.state[name], want, err_msg=f"interval {k} {name}")
+
+
+def test_aggregated_zone_read_error_keeps_earlier_subzones(oracle_lib):
+    """energy_zone.go:104-108: Energy() returns at the first failing sub-zone;
+    the sub-zones before it have their last reading updated, the aggregate not."""
+    from oracle.oracle import OracleZoneAgg
+
+    z = OracleZoneAgg(1, 1, 2, [1000, 1000])
+    e, mx, ns = z.read([100, 200])
+    assert e[0] == 300 and mx[0] == 2000 and ns[0] == 0
+    e, _, ns = z.read([150, 999], sub_status=[0, 1])  # sub-zone 1 fails
+    assert ns[0] == 1
+    e, _, ns = z.read([170, 260])  # sub-zone 0: 150 -> 170 (+20); sub-zone 1: 200 -> 260 (+60)
+    assert ns[0] == 0 and e[0] == 380
+    e, _, ns = z.read([180, 999], sub_status=[1, 0])  # sub-zone 0 fails first: nothing updated
+    assert ns[0] == 1
+    e, _, _ = z.read([190, 270])  # 170 -> 190 (+20), 260 -> 270 (+10)
+    assert e[0] == 410

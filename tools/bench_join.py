@@ -66,24 +66,34 @@ def main():
         sm.join(P, off.data_ptr(), key_sets[k].data_ptr(), 0, t["proc_slot"].data_ptr(), tk.data_ptr(),
                 ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
 
+    tr = accel.Tracker(acc, accel.KACC_KIND_PROC, 500, zone=0, min_energy=10 * 10**6)  # config.go:210-211
+
+    def track():
+        tr.add(sm, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), stream)
+
     flag = layout.fast_flag()
     join(n_sets)  # first interval: every ID new
     acc.run_interval(interval_from_tensors(t, sizes, flag), stream)
     acc.sync(stream)
-    tj, tall = [], []
+    tj, tall, ttr = [], [], []
     for s in range(steps):
         k = s % n_sets
         t.update(t_next[k])
         it = interval_from_tensors(t, sizes, flag)
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
         e0.record()
         join(k)
         e1.record()
         acc.run_interval(it, stream)
         e2.record()
-        e2.synchronize()
+        if s % 2:  # an export every other interval: Clear() first (process.go:80-84)
+            tr.clear(stream)
+        track()
+        e3.record()
+        e3.synchronize()
         tj.append(e0.elapsed_time(e1))
         tall.append(e0.elapsed_time(e2))
+        ttr.append(e2.elapsed_time(e3))
     acc.sync(stream)
     n_term = int(cnt.sum().item())
     # phase ablation (kacc_debug_join_variant): each variant timed from the same state
@@ -128,7 +138,8 @@ def main():
     cpu_rate = reps * int(sub_off[-1]) / (time.time() - t0)
     print(json.dumps({
         "config": cfg, "n_procs": P, "n_nodes": layout.n_nodes, "buckets": H,
-        "join_ms": jm, "join_plus_interval_ms": am,
+        "join_ms": jm, "join_plus_interval_ms": am, "tracker_ms": float(np.median(ttr)),
+        "tracker_items": int(tr.items()[0].size),
         "join_rows_per_s": P / (jm * 1e-3), "join_plus_interval_proc_attr_per_s": P / (am * 1e-3),
         "join_bytes": join_bytes, "join_GBps": join_bytes / (jm * 1e-3) / 1e9,
         "terminated_last": n_term, "phase_ms": phases,
