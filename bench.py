@@ -258,7 +258,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
-            "kernel": "kacc::interval_kernel<4> (+ generic_kernel<4>, empty at config 3)",
+            "kernel": "kacc::interval_kernel<4,0> (one launch per step: every config-3 node fits the fast path, KACC_F_FAST_NODES)",
             "same_box_copy_GBps": copy_gbps,
             "frac_of_copy": achieved / copy_gbps,
         },
