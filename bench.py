@@ -151,8 +151,12 @@ def main():
     ns_off, ns_slot = layout.namespace_csr()
     ns_t = to_device({"off": ns_off, "slot": ns_slot})
     n_ns = len(ns_off) - 1
-    ns_e = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
-    ns_p = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
+    # namespace totals double-buffered: step k's RCCL all-reduce (async, on the
+    # process group's stream) overlaps step k+1's interval kernel; buffer k % 2
+    # is rewritten only after the all-reduce of step k-2 has been waited for.
+    ns_e = [torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+    ns_p = [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+    pending = [None, None]
 
     def step(k, ev=None):
         if ev is not None:
@@ -160,14 +164,26 @@ def main():
         acc.run_interval(step_ivs[k], stream)
         if ev is not None:
             ev[1].record()
-        acc.namespace_totals(n_ns, ns_t["off"].data_ptr(), ns_t["slot"].data_ptr(), ns_e.data_ptr(),
-                             ns_p.data_ptr(), stream)
+        b = k % 2
+        if pending[b] is not None:  # stream-level wait (no host sync)
+            for w in pending[b]:
+                w.wait()
+            pending[b] = None
+        acc.namespace_totals(n_ns, ns_t["off"].data_ptr(), ns_t["slot"].data_ptr(), ns_e[b].data_ptr(),
+                             ns_p[b].data_ptr(), stream)
         if world > 1:  # cluster-wide namespace totals over xGMI (RCCL): u64 sum is exact
-            dist.all_reduce(ns_e)
-            dist.all_reduce(ns_p)
+            pending[b] = [dist.all_reduce(ns_e[b], async_op=True), dist.all_reduce(ns_p[b], async_op=True)]
+
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                for w in pending[b]:
+                    w.wait()
+                pending[b] = None
 
     for k in range(args.warmup):
         step(k)
+    drain()
     acc.sync(stream)
     torch.cuda.synchronize()
     log(rank, f"[bench] warmup done, setup {time.time() - t_setup:.1f}s")
@@ -180,6 +196,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, events[i])
+    drain()  # every all-reduce of the timed steps is inside the timed region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

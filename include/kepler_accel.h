@@ -359,6 +359,19 @@ void kacc_zone_agg_destroy(kacc_zone_agg *z); /* safe before or after kacc_destr
 int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_t *sub_status,
                        uint64_t *out_energy, uint64_t *out_max, uint32_t *node_status, void *stream);
 
+/* ---- exposition values ---------------------------------
+ * The numbers of the Prometheus exposition (power_collector.go:306-436):
+ * every element of an energy table as Energy.Joules() (device/energy.go:30-32)
+ * or of a power table as Power.Watts() (:57-59), written as the text format
+ * writes floats (expfmt writeFloat, prometheus/common v0.62.0: 1/0/-1/NaN/
+ * +Inf/-Inf spelled out, else Go strconv.AppendFloat(f, 'g', -1, 64)).
+ * out: device [count * KACC_FMT_WIDTH] bytes, element i's text left-aligned in
+ * its field (zero-padded); len: device [count] text lengths.  Labels are the
+ * Go side's strings; it joins them with these fields into sample lines.       */
+#define KACC_FMT_WIDTH 24
+int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, char *out,
+                       uint8_t *len, void *stream);
+
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

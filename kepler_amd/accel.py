@@ -35,6 +35,7 @@ KACC_NODE_OK = 0
 KACC_NODE_FIRST_READ = 1
 KACC_NODE_SKIPPED = 2
 KACC_F_NODE_CPU_DELTA_GIVEN = 0x1
+KACC_FMT_WIDTH = 24
 KACC_KIND_PROC, KACC_KIND_CTR, KACC_KIND_VM, KACC_KIND_POD = 0, 1, 2, 3
 KACC_KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
 KACC_F_FAST_NODES = 0x2
@@ -73,6 +74,7 @@ TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)
 EXPORTS = [
+    "kacc_format_values",
     "kacc_zone_agg_create",
     "kacc_zone_agg_destroy",
     "kacc_zone_agg_read",
@@ -228,6 +230,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
+    lib.kacc_format_values.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]
     lib.kacc_zone_agg_create.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, POINTER(c_void_p)]
     lib.kacc_zone_agg_destroy.argtypes = [c_void_p]
     lib.kacc_zone_agg_destroy.restype = None
@@ -365,6 +368,11 @@ class Accel:
 
     def state(self) -> dict:
         return {name: self.download(name) for name, _ in TABLES}
+
+    def format_values(self, name: str, first: int, count: int, out_ptr: int, len_ptr: int, stream: int = 0) -> None:
+        """kacc_format_values: exposition text of table elements (KACC_FMT_WIDTH-byte fields)."""
+        self._check(self.lib.kacc_format_values(self.ctx, TABLE_INDEX[name], first, count, c_void_p(out_ptr),
+                                                c_void_p(len_ptr), c_void_p(stream or None)))
 
     def namespace_totals(self, n_ns: int, ns_pod_off_ptr: int, ns_pod_slot_ptr: int,
                          out_energy_ptr: int, out_power_ptr: int, stream: int = 0) -> None:

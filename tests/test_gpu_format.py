@@ -1,0 +1,95 @@
+"""Device exposition formatting (kacc_format_values) against oracle/gofmt.py — MI355X only.
+
+Text is compared byte for byte: energy tables as Joules(), power tables as
+Watts(), over edge values (0, 1 J, exact powers of ten, u64 extremes, NaN,
+±Inf, -0, subnormals, DBL_MAX, halfway-looking decimals) and 1M random bit
+patterns / realistic attribution values.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from kepler_amd import accel
+from oracle.gofmt import joules, watts, write_float
+
+pytestmark = pytest.mark.gpu
+W = accel.KACC_FMT_WIDTH
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_ready():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    accel.load()
+    torch.cuda.set_stream(torch.cuda.Stream())
+
+
+def device_text(acc, table, n):
+    from kepler_amd.torch_batch import current_stream_handle
+
+    out = torch.zeros(n * W, dtype=torch.uint8, device="cuda")
+    ln = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    s = current_stream_handle()
+    acc.format_values(table, 0, n, out.data_ptr(), ln.data_ptr(), s)
+    acc.sync(s)
+    buf = out.cpu().numpy().reshape(n, W)
+    lens = ln.cpu().numpy()
+    return [bytes(buf[i, : lens[i]]).decode() for i in range(n)]
+
+
+def edge_energies():
+    v = [0, 1, 2, 5, 999_999, 10**6, 10**6 + 1, 1_500_000, 10**12, 10**15, 123_456_789_012, 2**53, 2**53 + 1,
+         2**63, 2**64 - 1, 2**64 - 1024, 10**19, 7 * 10**18 + 3]
+    v += [10**k for k in range(20)] + [10**k - 1 for k in range(1, 20)]
+    return np.array(v, dtype=np.uint64)
+
+
+def edge_powers():
+    v = [0.0, -0.0, 1e6, -1e6, 1.0, -1.0, float("nan"), float("inf"), float("-inf"), 5e-324, 2.2250738585072014e-308,
+         1.7976931348623157e308, -1.7976931348623157e308, 0.5, 1.5e6, 123456.0, 9.999999e12, 1e-10, 2.5e-5,
+         3.0e5 / 7, 1e23, 9007199254740993.0, 0.1, 0.2, 0.30000000000000004]
+    v += [10.0 ** k for k in range(-30, 30)] + [5.0 * 10.0 ** k for k in range(-20, 20)]
+    return np.array(v, dtype=np.float64)
+
+
+def test_format_edges():
+    e, p = edge_energies(), edge_powers()
+    n = max(e.size, p.size)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=1)
+    acc.upload("proc_energy", np.resize(e, n))
+    acc.upload("proc_power", np.resize(p, n))
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "proc_power", n)
+    for i in range(n):
+        ev, pv = int(np.resize(e, n)[i]), float(np.resize(p, n)[i])
+        assert got_e[i] == write_float(joules(ev)), (ev, got_e[i])
+        want_p = write_float(watts(pv))
+        assert got_p[i] == want_p, (pv, got_p[i], want_p)
+
+
+@pytest.mark.parametrize("kind", ["bits", "realistic"])
+def test_format_random(kind):
+    rng = np.random.default_rng(17 if kind == "bits" else 18)
+    n = 1 << 20
+    if kind == "bits":  # any double; energies over the whole u64 range
+        p = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64).view(np.float64)
+        e = rng.integers(0, 2**64 - 1, size=n, dtype=np.uint64, endpoint=True)
+    else:  # attribution-like: µJ totals and µW powers
+        e = (rng.lognormal(18, 4, size=n)).astype(np.uint64)
+        p = rng.lognormal(12, 3, size=n) * rng.choice([1.0, 1.0, 1.0, 0.0], size=n)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=1)
+    acc.upload("proc_energy", e)
+    acc.upload("proc_power", p)
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "proc_power", n)
+    bad = []
+    for i in range(n):
+        we = write_float(joules(int(e[i])))
+        if got_e[i] != we:
+            bad.append(("E", int(e[i]), got_e[i], we))
+        wp = write_float(watts(float(p[i])))
+        if got_p[i] != wp and not (math.isnan(p[i]) and got_p[i] == "NaN"):
+            bad.append(("P", float(p[i]), got_p[i], wp))
+        if len(bad) > 10:
+            break
+    assert not bad, bad[:10]
