@@ -37,10 +37,17 @@ __device__ __forceinline__ uint32_t log10_pow2(int32_t e) {  // floor(e log10 2)
 __device__ __forceinline__ uint32_t log10_pow5(int32_t e) {  // floor(e log10 5)
   return (static_cast<uint32_t>(e) * 732923u) >> 20;
 }
+// Exact u64 division by 5 / 10 / 100 via multiply-high (no software divide).
+__device__ __forceinline__ uint64_t div5(uint64_t x) { return __umul64hi(x, 0xCCCCCCCCCCCCCCCDull) >> 2; }
+__device__ __forceinline__ uint64_t div10(uint64_t x) { return __umul64hi(x, 0xCCCCCCCCCCCCCCCDull) >> 3; }
+__device__ __forceinline__ uint64_t div100(uint64_t x) { return __umul64hi(x >> 2, 0x28F5C28F5C28F5C3ull) >> 2; }
+
 __device__ __forceinline__ uint32_t pow5_factor(uint64_t v) {
   uint32_t c = 0;
-  while (v % 5 == 0) {
-    v /= 5;
+  for (;;) {
+    const uint64_t q = div5(v);
+    if (v - 5 * q != 0) break;
+    v = q;
     ++c;
   }
   return c;
@@ -88,7 +95,7 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
     vp = mul_shift(mv + 2, kPow5Inv[q], i);
     vm = mul_shift(mv - 1 - mm_shift, kPow5Inv[q], i);
     if (q <= 21) {
-      if (mv % 5 == 0)
+      if (mv - 5 * div5(mv) == 0)
         vr_tz = multiple_of_pow5(mv, q);
       else if (even)
         vm_tz = multiple_of_pow5(mv - 1 - mm_shift, q);
@@ -119,10 +126,10 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
   uint64_t out;
   if (vm_tz || vr_tz) {  // rare: exact trailing zeros matter
     for (;;) {
-      const uint64_t vp10 = vp / 10, vm10 = vm / 10;
+      const uint64_t vp10 = div10(vp), vm10 = div10(vm);
       if (vp10 <= vm10) break;
       const uint32_t vm_mod = static_cast<uint32_t>(vm - 10 * vm10);
-      const uint64_t vr10 = vr / 10;
+      const uint64_t vr10 = div10(vr);
       const uint32_t vr_mod = static_cast<uint32_t>(vr - 10 * vr10);
       vm_tz &= vm_mod == 0;
       vr_tz &= last == 0;
@@ -134,9 +141,9 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
     }
     if (vm_tz) {
       for (;;) {
-        const uint64_t vm10 = vm / 10;
+        const uint64_t vm10 = div10(vm);
         if (vm - 10 * vm10 != 0) break;
-        const uint64_t vp10 = vp / 10, vr10 = vr / 10;
+        const uint64_t vp10 = div10(vp), vr10 = div10(vr);
         const uint32_t vr_mod = static_cast<uint32_t>(vr - 10 * vr10);
         vr_tz &= last == 0;
         last = vr_mod;
@@ -150,9 +157,9 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
     out = vr + (((vr == vm && (!even || !vm_tz)) || last >= 5) ? 1 : 0);
   } else {
     bool up = false;
-    const uint64_t vp100 = vp / 100, vm100 = vm / 100;
+    const uint64_t vp100 = div100(vp), vm100 = div100(vm);
     if (vp100 > vm100) {
-      const uint64_t vr100 = vr / 100;
+      const uint64_t vr100 = div100(vr);
       up = vr - 100 * vr100 >= 50;
       vr = vr100;
       vp = vp100;
@@ -160,9 +167,9 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
       removed += 2;
     }
     for (;;) {
-      const uint64_t vp10 = vp / 10, vm10 = vm / 10;
+      const uint64_t vp10 = div10(vp), vm10 = div10(vm);
       if (vp10 <= vm10) break;
-      const uint64_t vr10 = vr / 10;
+      const uint64_t vr10 = div10(vr);
       up = vr - 10 * vr10 >= 5;
       vr = vr10;
       vp = vp10;
@@ -199,7 +206,11 @@ __device__ void write_float(double f, Field &o) {
   // digits of d.m, most significant first
   char dig[20];
   int nd = 0;
-  for (uint64_t m = d.m; m; m /= 10) dig[nd++] = static_cast<char>('0' + m % 10);
+  for (uint64_t m = d.m; m;) {
+    const uint64_t q = div10(m);
+    dig[nd++] = static_cast<char>('0' + (m - 10 * q));
+    m = q;
+  }
   for (int i = 0; i < nd / 2; ++i) {
     const char t = dig[i];
     dig[i] = dig[nd - 1 - i];

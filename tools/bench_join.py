@@ -96,6 +96,21 @@ def main():
         ttr.append(e2.elapsed_time(e3))
     acc.sync(stream)
     n_term = int(cnt.sum().item())
+    # exposition values of every process row x zone (kacc_format_values), energy and power
+    nval = int(slot_off[-1]) * layout.zones
+    fout = torch.empty(nval * accel.KACC_FMT_WIDTH, dtype=torch.uint8, device="cuda")
+    flen = torch.empty(nval, dtype=torch.uint8, device="cuda")
+    tf = []
+    for rep in range(6):
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record()
+        acc.format_values("proc_energy" if rep % 2 == 0 else "proc_power", 0, nval, fout.data_ptr(),
+                          flen.data_ptr(), stream)
+        f1.record()
+        f1.synchronize()
+        tf.append(f0.elapsed_time(f1))
+    fmt_ms = float(np.median(tf[2:]))
+    del fout, flen
     # phase ablation (kacc_debug_join_variant): each variant timed from the same state
     import ctypes
     lib = accel.load()
@@ -143,6 +158,7 @@ def main():
         "join_rows_per_s": P / (jm * 1e-3), "join_plus_interval_proc_attr_per_s": P / (am * 1e-3),
         "join_bytes": join_bytes, "join_GBps": join_bytes / (jm * 1e-3) / 1e9,
         "terminated_last": n_term, "phase_ms": phases,
+        "format_values": nval, "format_ms": fmt_ms, "format_values_per_s": nval / (fmt_ms * 1e-3),
         "cpu_oracle_join_rows_per_s": cpu_rate, "cpu_sample": f"{nn} nodes, {reps} intervals, 1 thread",
     }, indent=1))
 
