@@ -81,6 +81,12 @@ extern "C" {
                                    are skipped.  A node that does not fit is not
                                    computed and raises KACC_ERANGE (bit 32).
                                    kacc_batch_submit sets it by itself.       */
+#define KACC_F_TRUSTED_LAYOUT 0x4u /* kacc_batch_submit skips the host layout
+                                       check (kacc_validate_host): for packers
+                                       whose slots come from kacc_slot_join.  The
+                                       device still clamps every index and raises
+                                       KACC_ERANGE; only duplicate slots go
+                                       unchecked (they would race, not fault). */
 #define KACC_FAST_MAX_PROCS 2048u
 #define KACC_FAST_MAX_AGGREGATES 512u
 
@@ -215,9 +221,12 @@ typedef struct kacc_batch kacc_batch;
  * and set the optional node_status / node_cpu_delta / node_order to NULL.   */
 int kacc_batch_alloc(kacc_ctx *ctx, uint32_t n_nodes, uint32_t n_procs, uint32_t n_ctrs,
                      uint32_t n_vms, uint32_t n_pods, kacc_batch **out, kacc_interval **view);
-/* Validate, copy H2D and launch on the context stream (asynchronous). */
+/* Validate (host, multi-threaded), copy H2D on the context's copy stream and
+ * launch on the context stream (asynchronous).  With two batches the copies
+ * of one overlap the kernel of the other (fill B, submit B, wait A, ...).   */
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *batch);
-/* Wait for the batch; afterwards the batch may be refilled and resubmitted. */
+/* Wait for this batch's interval; afterwards it may be refilled and
+ * resubmitted.  Reports device range errors raised up to this interval.    */
 int kacc_batch_wait(kacc_ctx *ctx, kacc_batch *batch);
 void kacc_batch_free(kacc_ctx *ctx, kacc_batch *batch);
 

@@ -39,6 +39,7 @@ KACC_FMT_WIDTH = 24
 KACC_KIND_PROC, KACC_KIND_CTR, KACC_KIND_VM, KACC_KIND_POD = 0, 1, 2, 3
 KACC_KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
 KACC_F_FAST_NODES = 0x2
+KACC_F_TRUSTED_LAYOUT = 0x4
 KACC_FAST_MAX_PROCS = 2048
 KACC_FAST_MAX_AGGREGATES = 512
 

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -1561,7 +1562,7 @@ int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
     return fail(ctx, KACC_EINVAL, "required row array is NULL");
   if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
     return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
-  if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES))
+  if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES | KACC_F_TRUSTED_LAYOUT))
     return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
   return KACC_OK;
 }
@@ -1574,14 +1575,96 @@ int check_offsets(kacc_ctx *ctx, const char *name, const uint32_t *off, uint32_t
   return KACC_OK;
 }
 
+// Host checks of big batches run on up to kHostThreads threads (the Go caller
+// blocks in cgo meanwhile; a 20M-row batch is ~10 ms on one core).
+constexpr uint32_t kHostThreads = 16;
+constexpr uint64_t kHostGrain = 1u << 18;  // rows per thread at least
+
+// Runs fn(begin, end) over [0, n) in contiguous pieces; returns the smallest
+// index any piece reported (fn returns n when its piece is clean).
+template <typename F>
+uint64_t par_first(uint64_t n, F fn) {
+  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint64_t t = std::min<uint64_t>({kHostThreads, hw, (n + kHostGrain - 1) / kHostGrain});
+  if (t <= 1) return fn(0, n);
+  std::vector<uint64_t> first(t, n);
+  std::vector<std::thread> pool;
+  const uint64_t piece = (n + t - 1) / t;
+  for (uint64_t i = 0; i < t; ++i)
+    pool.emplace_back([&, i] { first[i] = fn(std::min(n, i * piece), std::min(n, (i + 1) * piece)); });
+  for (auto &th : pool) th.join();
+  return *std::min_element(first.begin(), first.end());
+}
+
+// Range and duplicate check of a slot column.  Each thread takes a contiguous
+// piece of rows and marks a private bitset over the piece's own slot range
+// (slots are allocated per node, so pieces rarely overlap); overlapping word
+// ranges of different pieces are then ANDed.  No atomics, no cap-sized clear.
 int check_slots(kacc_ctx *ctx, const char *name, const uint32_t *w, uint32_t n, uint64_t cap) {
-  std::vector<uint8_t> seen(cap, 0);
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint64_t s = w[i] & KACC_SLOT_MASK;
-    if (s >= cap) return fail(ctx, KACC_EINVAL, "%s[%u]=%llu >= capacity", name, i, (unsigned long long)s);
-    if (seen[s]) return fail(ctx, KACC_EINVAL, "%s: slot %llu used twice", name, (unsigned long long)s);
-    seen[s] = 1;
+  if (n == 0) return KACC_OK;
+  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint64_t T = std::max<uint64_t>(1, std::min<uint64_t>({kHostThreads, hw, (n + kHostGrain - 1) / kHostGrain}));
+  const uint64_t piece = (n + T - 1) / T;
+  struct Piece {
+    uint64_t b, e, lo, hi, bad = ~0ull, dup = ~0ull;  // rows [b, e); words [lo, hi]
+    std::vector<uint64_t> bits;
+  };
+  std::vector<Piece> pc(T);
+  auto mark = [&](uint64_t i) {
+    Piece &p = pc[i];
+    p.b = std::min<uint64_t>(n, i * piece);
+    p.e = std::min<uint64_t>(n, (i + 1) * piece);
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint64_t r = p.b; r < p.e; ++r) {
+      const uint64_t s = w[r] & KACC_SLOT_MASK;
+      if (s >= cap) {
+        p.bad = r;
+        return;
+      }
+      lo = std::min(lo, s);
+      hi = std::max(hi, s);
+    }
+    if (p.b == p.e) return;
+    p.lo = lo >> 6;
+    p.hi = hi >> 6;
+    p.bits.assign(p.hi - p.lo + 1, 0);
+    for (uint64_t r = p.b; r < p.e; ++r) {
+      const uint64_t s = w[r] & KACC_SLOT_MASK;
+      uint64_t &word = p.bits[(s >> 6) - p.lo];
+      const uint64_t bit = 1ull << (s & 63);
+      if (word & bit) {
+        p.dup = s;
+        return;
+      }
+      word |= bit;
+    }
+  };
+  if (T == 1) {
+    mark(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (uint64_t i = 0; i < T; ++i) pool.emplace_back(mark, i);
+    for (auto &th : pool) th.join();
   }
+  for (const Piece &p : pc) {  // first bad row in row order
+    if (p.bad != ~0ull)
+      return fail(ctx, KACC_EINVAL, "%s[%llu]=%llu >= capacity", name, (unsigned long long)p.bad,
+                  (unsigned long long)(w[p.bad] & KACC_SLOT_MASK));
+    if (p.dup != ~0ull) return fail(ctx, KACC_EINVAL, "%s: slot %llu used twice", name, (unsigned long long)p.dup);
+  }
+  // pieces whose word ranges overlap: a bit set in two of them is a duplicate
+  for (uint64_t i = 0; i < T; ++i)
+    for (uint64_t j = i + 1; j < T; ++j) {
+      const Piece &a = pc[i], &c = pc[j];
+      if (a.bits.empty() || c.bits.empty()) continue;
+      const uint64_t lo = std::max(a.lo, c.lo), hi = std::min(a.hi, c.hi);
+      for (uint64_t x = lo; x <= hi && lo <= hi; ++x) {
+        const uint64_t both = a.bits[x - a.lo] & c.bits[x - c.lo];
+        if (both)
+          return fail(ctx, KACC_EINVAL, "%s: slot %llu used twice", name,
+                      (unsigned long long)(x * 64 + __builtin_ctzll(both)));
+      }
+    }
   return KACC_OK;
 }
 
@@ -1625,7 +1708,8 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
     kacc_destroy(ctx);
     return code;
   };
-  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) {
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking)) != hipSuccess) {
     fail(ctx, KACC_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
     return bail(KACC_EHIP);
   }
@@ -1659,6 +1743,10 @@ void kacc_destroy(kacc_ctx *ctx) {
   if (ctx->d_items) (void)hipFree(ctx->d_items);
   if (ctx->d_defer) (void)hipFree(ctx->d_defer);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->copy_stream) {
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipStreamDestroy(ctx->copy_stream);
+  }
   delete ctx;
 }
 
@@ -1718,37 +1806,62 @@ int kacc_validate_host(const kacc_ctx *cctx, const kacc_interval *b) {
   if ((rc = check_offsets(ctx, "ctr_off", b->ctr_off, N, b->n_ctrs))) return rc;
   if ((rc = check_offsets(ctx, "vm_off", b->vm_off, N, b->n_vms))) return rc;
   if ((rc = check_offsets(ctx, "pod_off", b->pod_off, N, b->n_pods))) return rc;
-  for (uint32_t n = 0; n < N; ++n) {
-    const uint32_t p0 = b->proc_off[n], p1 = b->proc_off[n + 1];
-    uint32_t prev = p0;
-    for (uint32_t c = b->ctr_off[n]; c < b->ctr_off[n + 1]; ++c) {
-      if (b->ctr_proc_end[c] < prev || b->ctr_proc_end[c] > p1)
-        return fail(ctx, KACC_EINVAL, "ctr_proc_end[%u] outside node %u rows", c, n);
-      prev = b->ctr_proc_end[c];
+  // membership per node: containers then VMs tile the node's rows in order,
+  // pods tile the node's containers (first bad node reported)
+  enum { kOkNode, kBadCtr, kBadVm, kBadPod };
+  std::vector<uint8_t> why(N, kOkNode);
+  std::vector<uint32_t> where(N, 0);
+  const uint64_t bad_node = par_first(N, [&](uint64_t nb, uint64_t ne) -> uint64_t {
+    for (uint64_t n = nb; n < ne; ++n) {
+      const uint32_t p0 = b->proc_off[n], p1 = b->proc_off[n + 1];
+      uint32_t prev = p0;
+      for (uint32_t c = b->ctr_off[n]; c < b->ctr_off[n + 1]; ++c) {
+        if (b->ctr_proc_end[c] < prev || b->ctr_proc_end[c] > p1) {
+          why[n] = kBadCtr, where[n] = c;
+          return n;
+        }
+        prev = b->ctr_proc_end[c];
+      }
+      for (uint32_t v = b->vm_off[n]; v < b->vm_off[n + 1]; ++v) {
+        if (b->vm_proc_end[v] < prev || b->vm_proc_end[v] > p1) {
+          why[n] = kBadVm, where[n] = v;
+          return n;
+        }
+        prev = b->vm_proc_end[v];
+      }
+      uint32_t cprev = b->ctr_off[n];
+      for (uint32_t q = b->pod_off[n]; q < b->pod_off[n + 1]; ++q) {
+        if (b->pod_ctr_end[q] < cprev || b->pod_ctr_end[q] > b->ctr_off[n + 1]) {
+          why[n] = kBadPod, where[n] = q;
+          return n;
+        }
+        cprev = b->pod_ctr_end[q];
+      }
     }
-    for (uint32_t v = b->vm_off[n]; v < b->vm_off[n + 1]; ++v) {
-      if (b->vm_proc_end[v] < prev || b->vm_proc_end[v] > p1)
-        return fail(ctx, KACC_EINVAL, "vm_proc_end[%u] outside node %u rows", v, n);
-      prev = b->vm_proc_end[v];
-    }
-    uint32_t cprev = b->ctr_off[n];
-    for (uint32_t q = b->pod_off[n]; q < b->pod_off[n + 1]; ++q) {
-      if (b->pod_ctr_end[q] < cprev || b->pod_ctr_end[q] > b->ctr_off[n + 1])
-        return fail(ctx, KACC_EINVAL, "pod_ctr_end[%u] outside node %u containers", q, n);
-      cprev = b->pod_ctr_end[q];
-    }
+    return N;
+  });
+  if (bad_node < N) {
+    const unsigned i = where[bad_node], n = static_cast<unsigned>(bad_node);
+    if (why[bad_node] == kBadCtr) return fail(ctx, KACC_EINVAL, "ctr_proc_end[%u] outside node %u rows", i, n);
+    if (why[bad_node] == kBadVm) return fail(ctx, KACC_EINVAL, "vm_proc_end[%u] outside node %u rows", i, n);
+    return fail(ctx, KACC_EINVAL, "pod_ctr_end[%u] outside node %u containers", i, n);
   }
   if ((rc = check_slots(ctx, "proc_slot", b->proc_slot, b->n_procs, ctx->cfg.proc_slots))) return rc;
   if ((rc = check_slots(ctx, "ctr_slot", b->ctr_slot, b->n_ctrs, ctx->cfg.ctr_slots))) return rc;
   if ((rc = check_slots(ctx, "vm_slot", b->vm_slot, b->n_vms, ctx->cfg.vm_slots))) return rc;
   if ((rc = check_slots(ctx, "pod_slot", b->pod_slot, b->n_pods, ctx->cfg.pod_slots))) return rc;
   if (b->node_proc_span) {
-    for (uint32_t n = 0; n < N; ++n)
-      for (uint32_t r = b->proc_off[n]; r < b->proc_off[n + 1]; ++r) {
-        const uint32_t sl = b->proc_slot[r] & KACC_SLOT_MASK;
-        if (sl < b->node_proc_span[2 * n] || sl > b->node_proc_span[2 * n + 1])
-          return fail(ctx, KACC_EINVAL, "proc_slot[%u] outside node %u's node_proc_span", r, n);
-      }
+    const uint64_t bad = par_first(N, [&](uint64_t nb, uint64_t ne) -> uint64_t {
+      for (uint64_t n = nb; n < ne; ++n)
+        for (uint32_t r = b->proc_off[n]; r < b->proc_off[n + 1]; ++r) {
+          const uint32_t sl = b->proc_slot[r] & KACC_SLOT_MASK;
+          if (sl < b->node_proc_span[2 * n] || sl > b->node_proc_span[2 * n + 1]) return n;
+        }
+      return N;
+    });
+    if (bad < N)
+      return fail(ctx, KACC_EINVAL, "a proc_slot of node %u lies outside its node_proc_span",
+                  static_cast<unsigned>(bad));
   }
   if (b->node_order) {
     std::vector<uint8_t> seen(N, 0);
@@ -1802,6 +1915,14 @@ int kacc_batch_alloc(kacc_ctx *ctx, uint32_t N, uint32_t P, uint32_t C, uint32_t
       {(const void **)&h.pod_ctr_end, (const void **)&d.pod_ctr_end, 4ull * Q},
       {(const void **)&h.pod_slot, (const void **)&d.pod_slot, 4ull * Q},
   };
+  hipError_t ee = hipEventCreateWithFlags(&bt->copied, hipEventDisableTiming);
+  if (ee == hipSuccess) ee = hipEventCreateWithFlags(&bt->done, hipEventDisableTiming);
+  if (ee == hipSuccess) ee = hipHostMalloc(reinterpret_cast<void **>(&bt->h_err), sizeof(uint32_t), hipHostMallocDefault);
+  if (ee != hipSuccess) {
+    kacc_batch_free(ctx, bt);
+    return fail(ctx, KACC_EHIP, "batch events: %s", hipGetErrorString(ee));
+  }
+  *bt->h_err = 0;
   for (const F &f : fields) {
     const size_t bytes = std::max<size_t>(f.bytes, 8);
     void *hp = nullptr, *dp = nullptr;
@@ -1817,48 +1938,75 @@ int kacc_batch_alloc(kacc_ctx *ctx, uint32_t N, uint32_t P, uint32_t C, uint32_t
     *f.d = dp;
     bt->bufs.emplace_back(hp, dp);
     bt->sizes.push_back(f.bytes);
+    bt->fields.push_back(f.h);
   }
   *out = bt;
   *view = &bt->host;
   return KACC_OK;
 }
 
+// Two (or more) batches pipeline: the H2D copies of a batch run on the copy
+// stream while the previous batch's interval kernel runs on the context
+// stream; the kernel waits for its own copies (event), and a batch's device
+// buffers are not overwritten before its previous kernel has read them.
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (!ctx || !bt) return KACC_EINVAL;
-  int rc = kacc_validate_host(ctx, &bt->host);
-  if (rc != KACC_OK) return rc;
+  int rc = (bt->host.flags & KACC_F_TRUSTED_LAYOUT) ? check_shape(ctx, &bt->host)
+                                                    : kacc_validate_host(ctx, &bt->host);
+  if (rc != KACC_OK || bt->host.n_nodes == 0) return rc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   kacc_interval dv = bt->dev;
-  dv.flags = bt->host.flags | (all_nodes_fast(bt->host) ? KACC_F_FAST_NODES : 0u);
+  dv.flags = (bt->host.flags & ~KACC_F_TRUSTED_LAYOUT) |
+             (all_nodes_fast(bt->host) ? KACC_F_FAST_NODES : 0u);
   // honour optional arrays the caller switched off
   if (!bt->host.node_status) dv.node_status = nullptr;
   if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;
   if (!bt->host.node_order) dv.node_order = nullptr;
   if (!bt->host.node_proc_span) dv.node_proc_span = nullptr;
+  if (bt->submitted) KACC_HIP(ctx, hipStreamWaitEvent(ctx->copy_stream, bt->done, 0));
   for (size_t i = 0; i < bt->bufs.size(); ++i) {
-    if (!bt->sizes[i]) continue;
+    if (!bt->sizes[i] || !*bt->fields[i]) continue;  // empty, or an optional array switched off
     KACC_HIP(ctx, hipMemcpyAsync(bt->bufs[i].second, bt->bufs[i].first, bt->sizes[i],
-                                 hipMemcpyHostToDevice, ctx->stream));
+                                 hipMemcpyHostToDevice, ctx->copy_stream));
   }
+  KACC_HIP(ctx, hipEventRecord(bt->copied, ctx->copy_stream));
   if ((rc = ensure_items(ctx, dv.n_nodes, dv.n_procs, dv.n_pods)) != KACC_OK) return rc;
+  KACC_HIP(ctx, hipStreamWaitEvent(ctx->stream, bt->copied, 0));
   (void)hipGetLastError();  // clear a stale error of an earlier call
   launch(ctx->cfg.zones, dv, dev_state(ctx), ctx->stream);
   KACC_HIP(ctx, hipGetLastError());
+  KACC_HIP(ctx, hipMemcpyAsync(bt->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  KACC_HIP(ctx, hipEventRecord(bt->done, ctx->stream));
+  bt->submitted = true;
   return KACC_OK;
 }
 
+// Waits for this batch only (earlier work on the context stream is done too;
+// later submits may still run).  The device error word is per context, so an
+// error reported here may come from any interval up to this batch's.
 int kacc_batch_wait(kacc_ctx *ctx, kacc_batch *bt) {
   if (!ctx || !bt) return KACC_EINVAL;
-  return kacc_sync(ctx, nullptr);
+  if (!bt->submitted) return KACC_OK;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  KACC_HIP(ctx, hipEventSynchronize(bt->done));
+  if (*bt->h_err) {
+    *bt->h_err = 0;
+    return kacc_sync(ctx, nullptr);  // drains the stream, reports and clears the word
+  }
+  return KACC_OK;
 }
 
 void kacc_batch_free(kacc_ctx *ctx, kacc_batch *bt) {
   if (!bt) return;
   if (ctx) (void)hipSetDevice(ctx->device);
+  if (bt->done && bt->submitted) (void)hipEventSynchronize(bt->done);
   for (auto &b : bt->bufs) {
     if (b.first) (void)hipHostFree(b.first);
     if (b.second) (void)hipFree(b.second);
   }
+  if (bt->copied) (void)hipEventDestroy(bt->copied);
+  if (bt->done) (void)hipEventDestroy(bt->done);
+  if (bt->h_err) (void)hipHostFree(bt->h_err);
   delete bt;
 }
 

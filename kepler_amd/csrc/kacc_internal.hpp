@@ -19,6 +19,7 @@ struct kacc_ctx {
   int device = 0;
   kacc_config cfg{};
   hipStream_t stream = nullptr;
+  hipStream_t copy_stream = nullptr;  // pinned-batch H2D (overlaps the previous interval's kernel)
   void *tables[KACC_T_COUNT] = {};
   uint64_t counts[KACC_T_COUNT] = {};
   uint32_t *d_err = nullptr;
@@ -35,6 +36,11 @@ struct kacc_batch {
   kacc_interval dev{};
   std::vector<std::pair<void *, void *>> bufs;  // {pinned host, device}
   std::vector<size_t> sizes;
+  std::vector<const void *const *> fields;  // the view's pointer of each buffer (NULL = switched off)
+  hipEvent_t copied = nullptr;  // H2D of the last submit done (copy stream)
+  hipEvent_t done = nullptr;    // the last submit's kernels + error word copy done
+  uint32_t *h_err = nullptr;    // pinned: device error word after the last submit
+  bool submitted = false;
 };
 
 // Slot map of one workload kind (kacc_join.hip).

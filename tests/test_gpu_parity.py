@@ -295,3 +295,64 @@ def test_config3_full_size_properties_and_sampled_parity():
     nd = eng.table("node_cpu_delta")
     ok = (nd != 0)[:, None] & (ap != 0)
     assert np.all(np.abs(sums - ap)[ok] <= 1e-9 * np.abs(ap)[ok])
+
+
+def test_host_batch_pipelined_bit_exact():
+    """Two pinned batches in flight (submit B, wait A): copies overlap the previous
+    kernel, intervals still apply in submission order, bit-exact vs the oracle."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(24, [2000, 700, 1, 0, 1500, 2048] * 4, 4, seed=77, shuffle_slots=True)
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=77, churn=0.05, read_error_frac=0.05)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    bs = [accel.HostBatch.alloc(acc, **sizes) for _ in range(2)]
+    try:
+        ivs = [sim.next_interval() for _ in range(6)]
+        bs[0].fill(ivs[0])
+        bs[0].submit()
+        for k in range(1, len(ivs)):
+            # the other batch is still in flight; odd intervals skip the host check
+            bs[k % 2].fill(ivs[k], accel.KACC_F_TRUSTED_LAYOUT if k % 2 else 0)
+            bs[k % 2].submit()
+            bs[(k - 1) % 2].wait()
+        bs[(len(ivs) - 1) % 2].wait()
+        for a in ivs:
+            ora.interval(a, sizes)
+        for name, _ in accel.TABLES:
+            np.testing.assert_array_equal(acc.download(name), ora.state[name], err_msg=name)
+    finally:
+        for b in bs:
+            b.free()
+        acc.close()
+
+
+def test_host_batch_rejects_bad_layout():
+    """kacc_batch_submit validates on the host (multi-threaded for big batches):
+    a duplicate slot, an out-of-range slot and a container past its node's rows
+    are KACC_EINVAL before anything is copied or launched."""
+    layout = fleet.make_layout(64, 5000, 2, seed=9)  # 320k rows: the threaded checks run
+    sizes = layout.sizes()
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    b = accel.HostBatch.alloc(acc, **sizes)
+    try:
+        good = fleet.FleetSim(layout, seed=9).next_interval()
+        for mutate, msg in (
+            (lambda a: a["proc_slot"].__setitem__(300001, a["proc_slot"][7]), "used twice"),
+            (lambda a: a["proc_slot"].__setitem__(250000, layout.capacities()["proc_slots"]), ">= capacity"),
+            (lambda a: a["ctr_proc_end"].__setitem__(len(a["ctr_proc_end"]) - 1, sizes["n_procs"] + 1),
+             "outside node"),
+        ):
+            a = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in good.items()}
+            mutate(a)
+            b.fill(a)
+            with pytest.raises(accel.AccelError) as ei:
+                b.submit()
+            assert ei.value.code == accel.KACC_EINVAL and msg in str(ei.value), str(ei.value)
+        b.fill(good)  # the context is usable afterwards
+        b.submit()
+        b.wait()
+    finally:
+        b.free()
+        acc.close()

@@ -179,6 +179,89 @@ __global__ void mix_rows4(const double *__restrict__ d, const unsigned *__restri
   }
 }
 
+// 1 KiB-contiguous shape with 4 groups per wave in flight; NT: nontemporal
+// stores (and loads of the streamed inputs) for the tables that are not re-read
+template <bool NT>
+__global__ void mix_lin4(const double *__restrict__ d, const unsigned *__restrict__ slot,
+                         u64x2 *__restrict__ energy, f64x2 *__restrict__ power, size_t rows) {
+  const size_t lane = threadIdx.x & 63;
+  const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+  const size_t waves = ((size_t)gridDim.x * blockDim.x) >> 6;
+  const size_t groups = (rows + 63) / 64;
+  for (size_t g0 = wave; g0 < groups; g0 += 4 * waves) {
+    double x[4];
+    unsigned s[4];
+    u64x2 e[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t g = g0 + k * waves;
+      const size_t r = g * 64 + lane;
+      const bool ok = g < groups && r < rows;
+      x[k] = ok ? (NT ? __builtin_nontemporal_load(d + r) : d[r]) : 0.0;
+      s[k] = ok ? (NT ? __builtin_nontemporal_load(slot + r) : slot[r]) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t g = min(g0 + k * waves, groups - 1);
+      e[k][0] = energy[g * 128 + lane];
+      e[k][1] = energy[g * 128 + 64 + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const size_t g = g0 + k * waves;
+      if (g >= groups) continue;
+      e[k][0].x += (unsigned long long)x[k] + s[k];
+      e[k][1].y += 1;
+      f64x2 p0, p1;
+      p0.x = x[k];
+      p0.y = x[k] * 2;
+      p1.x = x[k] * 3;
+      p1.y = x[k] * 4;
+      if (NT) {
+        __builtin_nontemporal_store(e[k][0], energy + g * 128 + lane);
+        __builtin_nontemporal_store(e[k][1], energy + g * 128 + 64 + lane);
+        __builtin_nontemporal_store(p0, power + g * 128 + lane);
+        __builtin_nontemporal_store(p1, power + g * 128 + 64 + lane);
+      } else {
+        energy[g * 128 + lane] = e[k][0];
+        energy[g * 128 + 64 + lane] = e[k][1];
+        power[g * 128 + lane] = p0;
+        power[g * 128 + 64 + lane] = p1;
+      }
+    }
+  }
+}
+
+__global__ void copy16x4_nt(const u64x2 *__restrict__ a, u64x2 *__restrict__ b, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+    u64x2 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i + k * stride < n ? __builtin_nontemporal_load(a + i + k * stride) : u64x2{};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + k * stride < n) __builtin_nontemporal_store(v[k], b + i + k * stride);
+  }
+}
+
+__global__ void fill16x4(float4 *__restrict__ b, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) b[i] = float4{1.f, 2.f, 3.f, (float)i};
+}
+
+__global__ void read16x4(const float4 *__restrict__ a, float *__restrict__ out, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  float acc = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = i + k * stride < n ? a[i + k * stride] : float4{};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc += v[k].x + v[k].w;
+  }
+  if (acc == 12345.f) out[0] = acc;
+}
+
 int main(int argc, char **argv) {
   const size_t rows = argc > 1 ? strtoull(argv[1], nullptr, 10) : 20000000ull;
   const int reps = 20;
@@ -198,9 +281,9 @@ int main(int argc, char **argv) {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const double mix_bytes = rows * (8.0 + 4 + 32 + 64);
-  const int grids[] = {512, 1024, 2048, 4096, 16384};
+  const int grids[] = {1024, 2048, 4096, 16384};
   for (int g : grids) {
-    for (int k = 0; k < 7; ++k) {
+    for (int k = 0; k < 12; ++k) {
       float best = 1e30f;
       for (int rep = 0; rep < reps; ++rep) {
         CHECK(hipEventRecord(e0, 0));
@@ -217,14 +300,21 @@ int main(int argc, char **argv) {
           hipLaunchKernelGGL(mix_zmaj4, dim3(g), dim3(256), 0, 0, d, slot, (unsigned long long *)energy,
                              (double *)power, rows);
         if (k == 6) hipLaunchKernelGGL(mix_rows4, dim3(g), dim3(256), 0, 0, d, slot, (u64x2 *)energy, (f64x2 *)power, rows);
+        if (k == 7) hipLaunchKernelGGL(mix_lin4<false>, dim3(g), dim3(256), 0, 0, d, slot, (u64x2 *)energy, (f64x2 *)power, rows);
+        if (k == 8) hipLaunchKernelGGL(mix_lin4<true>, dim3(g), dim3(256), 0, 0, d, slot, (u64x2 *)energy, (f64x2 *)power, rows);
+        if (k == 9)
+          hipLaunchKernelGGL(copy16x4_nt, dim3(g), dim3(256), 0, 0, (const u64x2 *)energy, (u64x2 *)power, rows * 2);
+        if (k == 10) hipLaunchKernelGGL(fill16x4, dim3(g), dim3(256), 0, 0, (float4 *)power, rows * 2);
+        if (k == 11) hipLaunchKernelGGL(read16x4, dim3(g), dim3(256), 0, 0, (const float4 *)energy, (float *)d, rows * 2);
         CHECK(hipEventRecord(e1, 0));
         CHECK(hipEventSynchronize(e1));
         float ms;
         CHECK(hipEventElapsedTime(&ms, e0, e1));
         if (rep > 2 && ms < best) best = ms;
       }
-      const char *name[] = {"copy16", "mix_rows", "mix_lin", "mix_zmaj", "copy16x4", "mix_zmaj4", "mix_rows4"};
-      const double bytes = (k == 0 || k == 4) ? rows * 64.0 : mix_bytes;
+      const char *name[] = {"copy16",    "mix_rows",  "mix_lin",     "mix_zmaj",  "copy16x4", "mix_zmaj4",
+                            "mix_rows4", "mix_lin4", "mix_lin4_nt", "copy16x4_nt", "fill16",  "read16x4"};
+      const double bytes = (k == 0 || k == 4 || k == 9) ? rows * 64.0 : (k == 10 || k == 11) ? rows * 32.0 : mix_bytes;
       printf("{\"kernel\":\"%s\",\"grid\":%d,\"ms\":%.4f,\"GBps\":%.1f}\n", name[k], g, best, bytes / (best * 1e-3) / 1e9);
     }
   }
