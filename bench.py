@@ -98,12 +98,19 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
+    # rehearsal of the N > 1 logic on a one-GPU box (never the driver's runs):
+    # KACC_BENCH_BACKEND=gloo KACC_BENCH_DEVICE=0 puts every rank on one device
+    backend = os.environ.get("KACC_BENCH_BACKEND", "nccl")
+    dev = int(os.environ.get("KACC_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     # an explicit stream: the engine launches on it and the HIP events below
     # time exactly that stream (a NULL handle would mean the context's stream)
     torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
@@ -123,7 +130,7 @@ def main():
     node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_steps)]
     log(rank, f"[bench] inputs generated in {time.time() - t_setup:.1f}s")
 
-    acc = accel.Accel(Z, **layout.capacities(), device=local)
+    acc = accel.Accel(Z, **layout.capacities(), device=dev)
     stream = current_stream_handle()
     assert stream != 0
     statics = to_device(layout.static_arrays())
@@ -263,7 +270,8 @@ def main():
             "pods_per_gpu": sizes["n_pods"],
             "zones": Z,
             "namespaces": n_ns,
-            "parallelism": f"node-sharded x{world} (namespace totals all-reduced over RCCL)",
+            "parallelism": f"node-sharded x{world} (namespace totals all-reduced over "
+                           f"{'RCCL' if backend == 'nccl' else backend})",
         },
         "node_snapshots_per_s": total_nodes * args.steps / wall_max,
         "kernel_ms": k_avg_ms,
