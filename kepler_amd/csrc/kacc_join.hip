@@ -198,22 +198,26 @@ struct NodeView {
 };
 template <bool kSmall>
 __device__ __forceinline__ bool node_view(const Args &a, uint32_t n, NodeView &v) {
-  if (a.node_status && (a.node_status[n] & KACC_NODE_READ_ERROR)) {  // map unchanged
+  // every node word is loaded up front (independent loads, one round trip)
+  const uint32_t status = a.node_status ? a.node_status[n] : 0u;
+  v.hb = a.hoff[n];
+  const uint64_t he = a.hoff[n + 1];
+  v.r0 = a.row_off[n];
+  v.r1 = a.row_off[n + 1];
+  v.s0 = a.slot_off[n];
+  const uint32_t s1 = a.slot_off[n + 1];
+  if (status & KACC_NODE_READ_ERROR) {  // map unchanged
     if (kSmall && threadIdx.x == 0) a.term_count[n] = 0u;
     return false;
   }
-  v.hb = a.hoff[n];
-  v.H = static_cast<uint32_t>(a.hoff[n + 1] - v.hb);
-  v.r0 = a.row_off[n];
-  v.r1 = a.row_off[n + 1];
+  v.H = static_cast<uint32_t>(he - v.hb);
   if (v.r1 > a.n_rows || v.r0 > v.r1) {
     if (kSmall && threadIdx.x == 0) atomicOr(a.err, kErrOffsets);
     v.r1 = min(v.r1, a.n_rows);
     v.r0 = min(v.r0, v.r1);
   }
   if ((v.H <= kLdsBuckets && v.r1 - v.r0 <= kSmallRows) != kSmall) return false;
-  v.s0 = a.slot_off[n];
-  v.S = a.slot_off[n + 1] - v.s0;
+  v.S = s1 - v.s0;
   v.shift = 32u - static_cast<uint32_t>(__builtin_ctz(v.H));
   return true;
 }
@@ -245,10 +249,10 @@ __device__ __forceinline__ void span_out(const Args &a, uint32_t n, uint32_t lo,
 
 // ============================ small nodes (LDS) ====================================
 // Table in LDS, rows' keys / slot words in registers (lane owns kRpl
-// consecutive rows), per-slot marks in LDS written with plain stores:
-// s_used[s] (slot held at the start), s_seen[s] = 1 + the row that found s
-// (a second finder of the same ID sees another row there: duplicate).
-constexpr uint32_t kSmallSlots = kSmallWords * 32;
+// consecutive rows), per-slot mark bitmaps in LDS (LDS atomics): s_used
+// (slot held at the start), s_seen (a row found the slot; the second finder
+// of the same ID sees the bit already set: duplicate).  Bitmaps keep the
+// workgroup at <= 40 KiB of LDS, i.e. 4 workgroups (8 waves/SIMD) per CU.
 constexpr uint32_t kNewCap = 512;  // new rows handled as a compact list
 
 template <typename K>
@@ -257,8 +261,8 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   constexpr bool kWide = sizeof(K) == 8;
   __shared__ uint64_t s_ent[kLdsBuckets];              // entries (u32 keys) / keys (u64)
   __shared__ uint32_t s_slot[kWide ? kLdsBuckets : 1];  // slots (u64 keys)
-  __shared__ __attribute__((aligned(16))) uint8_t s_used[kSmallSlots];
-  __shared__ __attribute__((aligned(16))) uint16_t s_seen[kSmallSlots];
+  __shared__ uint32_t s_used[kSmallWords];  // bit s: slot s held by a live ID
+  __shared__ uint32_t s_seen[kSmallWords];  // bit s: a row found slot s
   __shared__ uint32_t s_fmask[kSmallWords], s_tmask[kSmallWords];  // free / terminated bits
   __shared__ uint32_t s_wpre[kSmallWords];                          // (free << 16 | term) before w
   __shared__ uint16_t s_free[kNewCap];                              // the first free slots
@@ -289,20 +293,9 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   const Probe<K> pr{L, v.shift, H - 1, H};
 
   // ---- 1: table -> LDS, keys -> registers, marks cleared ---------------------------
-  for (uint32_t b = tid; b < H; b += kThreads) {
-    if constexpr (kWide) {
-      s_ent[b] = G.k[b];
-      s_slot[b] = G.s[b];
-    } else {
-      s_ent[b] = G.e[b];
-    }
-  }
-  for (uint32_t i = tid; i < W * 32; i += kThreads) {
-    s_used[i] = 0;
-    s_seen[i] = 0;
-  }
-  for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
-  if (tid == 0) s_occ = 0u;
+  // All loads of the phase are issued before the first LDS store (register
+  // staging): the node pays one memory round trip, not one per bucket.
+  constexpr int kPer = kLdsBuckets / kThreads;
   K key[kRpl];
   uint32_t res[kRpl];
 #pragma unroll
@@ -310,14 +303,47 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     const uint32_t r = tid * kRpl + j;
     key[j] = r < R ? keys[r] : T::kEmpty;
   }
+  {
+    uint64_t ev[kPer];
+    uint32_t sv[kWide ? kPer : 1];
+    if (H) {  // node-uniform; clamped addresses keep the loads unconditional
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t b = tid + j * kThreads, bb = b < H ? b : 0u;
+        if constexpr (kWide) {
+          ev[j] = G.k[bb];
+          sv[j] = G.s[bb];
+        } else {
+          ev[j] = G.e[bb];
+        }
+      }
+    }
+    for (uint32_t i = tid; i < W; i += kThreads) {
+      s_used[i] = 0u;
+      s_seen[i] = 0u;
+    }
+    for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
+    if (tid == 0) s_occ = 0u;
+    if (H) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t b = tid + j * kThreads;
+        if (b >= H) break;
+        s_ent[b] = ev[j];
+        if constexpr (kWide) s_slot[b] = sv[j];
+      }
+    }
+  }
   __syncthreads();
+  if (a.stop_after == 1u) return;  // timing ablation
 
   // ---- 2: held slots; lookups --------------------------------------------------------
   for (uint32_t b = tid; b < H; b += kThreads) {
     if (!is_live<K>(L.raw(b))) continue;
     const uint32_t sl = lslot(b);
-    if (sl < S) s_used[sl] = 1;
+    if (sl < S) atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
   }
+  uint32_t mine = 0;  // new rows of this lane
 #pragma unroll
   for (int j = 0; j < kRpl; ++j) {
     const uint32_t r = tid * kRpl + j;
@@ -331,43 +357,25 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     const uint32_t b = pr.find(k);
     if (b == ~0u) {
       res[j] = kPending;
+      ++mine;
       continue;
     }
     const uint32_t sl = lslot(b);
     if (sl >= S) continue;
-    s_seen[sl] = static_cast<uint16_t>(r + 1);
+    const uint32_t bit = 1u << (sl & 31);
+    if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
+      atomicOr(a.err, kErrKey);
+      continue;
+    }
     res[j] = s0 + sl;
   }
   __syncthreads();
-  uint32_t mine = 0;  // new rows of this lane
-#pragma unroll
-  for (int j = 0; j < kRpl; ++j) {
-    const uint32_t r = tid * kRpl + j;
-    if (res[j] == kPending) {
-      ++mine;
-    } else if (res[j] != kInvalid && s_seen[res[j] - s0] != r + 1) {  // ID on two rows
-      atomicOr(a.err, kErrKey);
-      res[j] = kInvalid;
-    }
-  }
+  if (a.stop_after == 2u) return;  // timing ablation
 
   // ---- 3: per-word free / terminated bits and their prefixes -------------------------
   uint32_t packed = 0;
   if (tid < W) {
-    uint32_t used = 0, seen = 0;
-    const uint32_t *u4 = reinterpret_cast<const uint32_t *>(s_used + tid * 32);
-    const uint2 *s4 = reinterpret_cast<const uint2 *>(s_seen + tid * 32);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {  // slots 4q .. 4q+3 of the word
-      const uint32_t x = u4[q];
-      const uint2 y = s4[q];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) used |= ((x >> (8 * i)) & 1u) << (4 * q + i);
-      seen |= (((y.x & 0xffffu) != 0) ? 1u : 0u) << (4 * q);
-      seen |= (((y.x >> 16) != 0) ? 1u : 0u) << (4 * q + 1);
-      seen |= (((y.y & 0xffffu) != 0) ? 1u : 0u) << (4 * q + 2);
-      seen |= (((y.y >> 16) != 0) ? 1u : 0u) << (4 * q + 3);
-    }
+    const uint32_t used = s_used[tid], seen = s_seen[tid];
     const uint32_t valid = (tid + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
     const uint32_t fm = ~used & valid, tm = used & ~seen & valid;
     s_fmask[tid] = fm;
@@ -381,6 +389,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot;
   if (tid == 0) a.term_count[n] = n_term;
   __syncthreads();
+  if (a.stop_after == 3u) return;  // timing ablation
 
   // ---- 4: terminated list (slot order) + tombstones; the first free slots ------------
   if (n_term) {
@@ -405,6 +414,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
       s_free[p] = static_cast<uint16_t>(tid * 32 + __builtin_ctz(fm));
   }
   __syncthreads();
+  if (a.stop_after == 4u) return;  // timing ablation
 
   // ---- 5: new rows take slots in row order ------------------------------------------
   auto take_slow = [&](uint32_t q) -> uint32_t {  // q-th free slot, q >= kNewCap
@@ -438,6 +448,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     ++q;
   }
   __syncthreads();
+  if (a.stop_after == 5u) return;  // timing ablation
 
   // ---- 6: inserts (one lane per new row), then a re-probe flags an ID twice ---------
   const uint32_t n_ins = min(n_new, total_free);
