@@ -283,7 +283,10 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
-            "kernel": "kacc::interval_kernel<4,0> (one launch per step: every config-3 node fits the fast path, KACC_F_FAST_NODES)",
+            "kernel": (f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, "
+                       f"KACC_F_FAST_NODES)" if layout.fast_flag() else
+                       f"kacc::interval_kernel<{Z},0> + chunk_kernel<{Z},0> + pod_kernel<{Z},0> (big nodes "
+                       f"chunked; HIP events bracket all three launches of the step)"),
             "same_box_copy_GBps": copy_gbps,
             "frac_of_copy": achieved / copy_gbps,
         },
