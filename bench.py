@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
     ap.add_argument("--nodes", type=int, default=None, help="override nodes per GPU")
     ap.add_argument("--distinct", type=int, default=4, help="distinct process-input sets cycled")
+    ap.add_argument("--intervals", type=int, default=1,
+                    help="intervals per step, issued by one kacc_run_intervals call (config 5: 60)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-nodes", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -123,11 +125,13 @@ def main():
     sizes = layout.sizes()
     log(rank, f"[bench] layout {sizes} Z={Z} built in {time.time() - t_setup:.1f}s")
 
+    K = max(1, args.intervals)
     n_steps = args.warmup + args.steps
-    n_distinct = max(1, min(args.distinct, n_steps))
+    n_ivs = n_steps * K  # every interval has its own node counters / clocks
+    n_distinct = max(1, min(args.distinct, n_ivs))
     prime = sim.next_interval()  # first read (monitor.go:326-330), untimed
     full = [sim.next_interval() for _ in range(n_distinct)]
-    node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_steps)]
+    node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_ivs)]
     log(rank, f"[bench] inputs generated in {time.time() - t_setup:.1f}s")
 
     acc = accel.Accel(Z, **layout.capacities(), device=dev)
@@ -148,8 +152,8 @@ def main():
             t["node_order"] = order
         return t
 
-    step_tensors = [make(k) for k in range(n_steps)]
-    step_ivs = [interval_from_tensors(t, sizes, layout.fast_flag()) for t in step_tensors]
+    iv_tensors = [make(k) for k in range(n_ivs)]
+    ivs = [interval_from_tensors(t, sizes, layout.fast_flag()) for t in iv_tensors]
     prime_t = to_device(prime)
     acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
     acc.sync(stream)
@@ -168,7 +172,10 @@ def main():
     def step(k, ev=None):
         if ev is not None:
             ev[0].record()
-        acc.run_interval(step_ivs[k], stream)
+        if K == 1:
+            acc.run_interval(ivs[k], stream)
+        else:  # K consecutive intervals, back to back from C
+            acc.run_intervals(ivs[k * K:(k + 1) * K], stream)
         if ev is not None:
             ev[1].record()
         b = k % 2
@@ -209,7 +216,7 @@ def main():
         dist.barrier()
     wall = time.perf_counter() - t0
     acc.sync(stream)  # surfaces any device-detected range error
-    kernel_ms = [a.elapsed_time(b) for a, b in events]
+    kernel_ms = [a.elapsed_time(b) / K for a, b in events]  # per interval
 
     # same-box reference for the roofline: a 1.28 GB device-to-device copy
     src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
@@ -249,7 +256,7 @@ def main():
 
     result = {
         "metric": METRIC,
-        "value": total_procs * args.steps / wall_max,
+        "value": total_procs * K * args.steps / wall_max,
         "unit": "proc-attr/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -262,7 +269,9 @@ def main():
         "data": "synthetic (kepler_amd/fleet.py, seed 0x4B45504C; inputs resident in HBM)",
         "config": {
             "workload": f"config{args.config}: {sizes['n_nodes']} nodes x "
-                        f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs, Z={Z} per GPU",
+                        f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs, Z={Z} per GPU"
+                        + (f", {K} intervals per step (kacc_run_intervals)" if K > 1 else ""),
+            "intervals_per_step": K,
             "nodes_per_gpu": sizes["n_nodes"],
             "procs_per_gpu": sizes["n_procs"],
             "containers_per_gpu": sizes["n_ctrs"],
@@ -273,7 +282,7 @@ def main():
             "parallelism": f"node-sharded x{world} (namespace totals all-reduced over "
                            f"{'RCCL' if backend == 'nccl' else backend})",
         },
-        "node_snapshots_per_s": total_nodes * args.steps / wall_max,
+        "node_snapshots_per_s": total_nodes * K * args.steps / wall_max,
         "kernel_ms": k_avg_ms,
         "roofline": {
             "bound": "hbm",

@@ -208,6 +208,12 @@ int kacc_reset(kacc_ctx *ctx);
  * context's own stream).  Asynchronous: call kacc_sync() to wait and to
  * collect device-detected range errors.                                      */
 int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream);
+/* `count` consecutive intervals (host array of device-pointer descriptors) in
+ * order on `stream`: interval k+1 sees the state interval k wrote, exactly as
+ * `count` kacc_run_interval calls, but issued back to back from C (fleet
+ * replay; BASELINE config 5: 60 batched intervals with counter wraparound).
+ * Every descriptor's shape is checked before the first launch.               */
+int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t count, void *stream);
 int kacc_sync(kacc_ctx *ctx, void *stream);
 
 /* Host-side layout check of a batch held in host memory (O(N+C+V+Q+P)). */

@@ -95,6 +95,7 @@ EXPORTS = [
     "kacc_get_config",
     "kacc_reset",
     "kacc_run_interval",
+    "kacc_run_intervals",
     "kacc_sync",
     "kacc_validate_host",
     "kacc_batch_alloc",
@@ -211,6 +212,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_get_config.argtypes = [c_void_p, POINTER(KaccConfig)]
     lib.kacc_reset.argtypes = [c_void_p]
     lib.kacc_run_interval.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p]
+    lib.kacc_run_intervals.argtypes = [c_void_p, POINTER(KaccInterval), ctypes.c_uint32, c_void_p]
     lib.kacc_sync.argtypes = [c_void_p, c_void_p]
     lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
     lib.kacc_batch_alloc.argtypes = [
@@ -329,6 +331,11 @@ class Accel:
 
     def run_interval(self, dev_interval: KaccInterval, stream: int = 0) -> None:
         self._check(self.lib.kacc_run_interval(self.ctx, ctypes.byref(dev_interval), c_void_p(stream or None)))
+
+    def run_intervals(self, dev_intervals, stream: int = 0) -> None:
+        """kacc_run_intervals: consecutive intervals issued back to back from C."""
+        arr = (KaccInterval * len(dev_intervals))(*dev_intervals)
+        self._check(self.lib.kacc_run_intervals(self.ctx, arr, len(dev_intervals), c_void_p(stream or None)))
 
     def run_variant(self, dev_interval: KaccInterval, stream: int, variant: int) -> None:
         """Timing ablation (kacc_debug.h); variant != 0 is not the reference semantics."""

@@ -1782,6 +1782,33 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   return KACC_OK;
 }
 
+// K consecutive intervals in one call (fleet replay, BASELINE config 5's 60
+// batched intervals): interval k+1 reads the state interval k wrote, so the
+// launches are issued in order on one stream, back to back from C (no host
+// round trip between intervals).  Every shape is checked before any launch.
+int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t count, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (count && !dev_batches) return fail(ctx, KACC_EINVAL, "dev_batches is NULL");
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  uint64_t max_nodes = 0, max_procs = 0, max_pods = 0;
+  for (uint32_t k = 0; k < count; ++k) {
+    const int rc = check_shape(ctx, &dev_batches[k]);
+    if (rc != KACC_OK) return fail(ctx, rc, "interval %u: %s", k, std::string(ctx->err).c_str());
+    max_nodes = std::max<uint64_t>(max_nodes, dev_batches[k].n_nodes);
+    max_procs = std::max<uint64_t>(max_procs, dev_batches[k].n_procs);
+    max_pods = std::max<uint64_t>(max_pods, dev_batches[k].n_pods);
+  }
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  int rc = ensure_items(ctx, max_nodes, max_procs, max_pods);
+  if (rc != KACC_OK) return rc;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
+  const kacc::DevState ds = dev_state(ctx);
+  for (uint32_t k = 0; k < count; ++k)
+    if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
 int kacc_sync(kacc_ctx *ctx, void *stream) {
   if (!ctx) return KACC_EINVAL;
   KACC_HIP(ctx, hipSetDevice(ctx->device));

@@ -356,3 +356,32 @@ def test_host_batch_rejects_bad_layout():
     finally:
         b.free()
         acc.close()
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("z4-wrap", dict(n_nodes=16, procs_per_node=[2000, 300, 1, 0] * 4, zones=4)),
+    ("z4-skew-chunked", dict(n_nodes=5, procs_per_node=[10000, 50000, 12, 0, 2049], zones=4,
+                             procs_per_vm=2, vm_frac=0.02)),
+])
+def test_run_intervals_matches_sequential(name, kw):
+    """kacc_run_intervals over K intervals == K interval calls == the oracle (BASELINE
+    config 5's batched intervals with counter wraparound: fake-meter MaxEnergy 1e6)."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(seed=21, **kw)
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=21, churn=0.03, read_error_frac=0.05, max_energy=fleet.MAX_ENERGY_FAKE)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    ivs = [sim.next_interval() for _ in range(12)]
+    dev = [to_device(a) for a in ivs]
+    descs = [interval_from_tensors(t, sizes) for t in dev]
+    s = current_stream_handle()
+    acc.run_intervals(descs[:1], s)  # first read alone, then 11 in one call
+    acc.run_intervals(descs[1:], s)
+    acc.sync(s)
+    for a in ivs:
+        ora.interval(a, sizes)
+    for tname, _ in accel.TABLES:
+        np.testing.assert_array_equal(acc.download(tname), ora.state[tname], err_msg=tname)
+    acc.close()
