@@ -152,11 +152,12 @@ def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
                 ctr_frac: float = 0.79, procs_per_ctr: int = 8, vm_frac: float = 0.01,
                 procs_per_vm: int = 1, ctrs_per_pod: float = 2.5, pod_frac: float = 0.9,
                 n_namespaces: Optional[int] = None, shuffle_slots: bool = False,
-                fragment_slots: float = 0.0) -> FleetLayout:
+                fragment_slots: float = 0.0, fragment_sorted: bool = False) -> FleetLayout:
     """Synthetic fleet.  Process slots: consecutive per node (default), a global
     permutation (``shuffle_slots``), or, with ``fragment_slots`` = f > 0, each
     node's processes on a random subset of its own slot range of (1 + f) x rows
-    in random order — the steady state the slot join reaches under churn.
+    in random order — the steady state the slot join reaches under churn
+    (``fragment_sorted``: the same subsets in increasing slot order).
     """
     rng = np.random.default_rng(seed)
     P = np.broadcast_to(np.asarray(procs_per_node, dtype=np.int64), (n_nodes,)).copy()
@@ -195,7 +196,8 @@ def make_layout(n_nodes: int, procs_per_node, zones: int, seed: int = SEED,
         rng_f = np.random.default_rng(seed ^ 0xF4A6)
         cap = (P * (1.0 + fragment_slots)).astype(np.int64) + 1
         slot_base = np.concatenate([[0], np.cumsum(cap)[:-1]])
-        proc_slot = np.concatenate([slot_base[n] + rng_f.permutation(int(cap[n]))[: int(P[n])]
+        pick = (lambda x: np.sort(x)) if fragment_sorted else (lambda x: x)
+        proc_slot = np.concatenate([slot_base[n] + pick(rng_f.permutation(int(cap[n]))[: int(P[n])])
                                     for n in range(n_nodes)]) if n_procs else np.zeros(0, np.int64)
         ctr_slot, vm_slot, pod_slot = np.arange(n_ctrs), np.arange(n_vms), np.arange(n_pods)
     elif shuffle_slots:
@@ -256,7 +258,7 @@ def layout_from_sizes(zones: int, nodes, seed: int = SEED, shuffle_slots: bool =
 
 
 def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
-                  fragment_slots: float = 0.0) -> FleetLayout:
+                  fragment_slots: float = 0.0, fragment_sorted: bool = False) -> FleetLayout:
     """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed).
 
     ``fragment_slots`` > 0 places each node's processes on a random subset of
@@ -267,7 +269,8 @@ def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
     if config == 2:
         return make_layout(nodes or 1000, 1000, 2, seed, fragment_slots=fragment_slots)
     if config in (3, 4):
-        return make_layout(nodes or 10000, 2000, 4, seed, fragment_slots=fragment_slots)
+        return make_layout(nodes or 10000, 2000, 4, seed, fragment_slots=fragment_slots,
+                           fragment_sorted=fragment_sorted)
     if config == 5:
         rng = np.random.default_rng(seed ^ 5)
         n = nodes or 1000

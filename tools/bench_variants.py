@@ -33,7 +33,7 @@ def main():
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
     frag = float(os.environ.get("FRAG", "0"))  # slot fragmentation (+ node_proc_span)
-    layout = fleet.config_layout(cfg, fragment_slots=frag)
+    layout = fleet.config_layout(cfg, fragment_slots=frag, fragment_sorted=bool(os.environ.get("FRAG_SORTED")))
     sim = fleet.FleetSim(layout)
     acc = accel.Accel(layout.zones, **layout.capacities())
     stream = current_stream_handle()
@@ -43,7 +43,7 @@ def main():
     # distinct input sets cycled like bench.py (no cache reuse between launches)
     n_distinct = int(os.environ.get("DISTINCT", "4"))
     dev = [to_device(sim.next_interval()) for _ in range(n_distinct)]
-    if frag > 0 and not os.environ.get("NO_SPAN"):
+    if (frag > 0 or os.environ.get("SPAN")) and not os.environ.get("NO_SPAN"):
         span = to_device({"s": layout.proc_span()})["s"]
         for d in dev:
             d["node_proc_span"] = span
