@@ -69,8 +69,11 @@ FLEETS = [
 ]
 
 
+@pytest.mark.parametrize("concurrent", [False, True], ids=["one-stream", "tracker-beside-interval"])
 @pytest.mark.parametrize("name,sizes,Z,churn,max_size", FLEETS, ids=[f[0] for f in FLEETS])
-def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size):
+def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurrent):
+    """concurrent: the tracker runs on a second stream beside the interval kernel
+    (it reads only terminated slots, which the interval never writes)."""
     layout = fleet.make_layout(len(sizes), sizes, Z, seed=31)
     sizes_d = layout.sizes()
     rows = np.diff(layout.proc_off.astype(np.int64))
@@ -91,6 +94,8 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size):
     tc = torch.zeros(layout.n_nodes, dtype=torch.int32, device="cuda")
     span = torch.zeros(2 * layout.n_nodes, dtype=torch.int32, device="cuda")
     s = current_stream_handle()
+    s2 = torch.cuda.Stream()
+    ts2 = s2.cuda_stream if concurrent else s
     for it in range(6):
         a = sim.next_interval()
         keys = keys_sim.next_keys()
@@ -103,11 +108,17 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size):
         sm.join(layout.n_procs, t["proc_off"].data_ptr(), d_keys.data_ptr(), t["node_status"].data_ptr(),
                 t["proc_slot"].data_ptr(), tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), s, span.data_ptr())
         t["node_proc_span"] = span
+        if concurrent:  # the tracker waits for the join only
+            joined = torch.cuda.Event()
+            joined.record(torch.cuda.current_stream())
+            s2.wait_event(joined)
         acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         if it == 3:  # an export happened: Clear() before this interval's adds (process.go:80-84)
-            tr.clear(s)
+            tr.clear(ts2)
             otr.clear()
-        tr.add(sm, tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), s)
+        tr.add(sm, tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), ts2)
+        if concurrent:  # the next join rewrites the terminated lists the tracker reads
+            torch.cuda.current_stream().wait_stream(s2)
         acc.sync(s)
         ora.interval(a_ora, sizes_d)
         # oracle: the same terminated batch (per-node segments), values from the oracle tables

@@ -75,7 +75,7 @@ def main():
     join(n_sets)  # first interval: every ID new
     acc.run_interval(interval_from_tensors(t, sizes, flag), stream)
     acc.sync(stream)
-    tj, tall, ttr = [], [], []
+    tj, tall, ttr, tseq = [], [], [], []
     for s in range(steps):
         k = s % n_sets
         t.update(t_next[k])
@@ -94,6 +94,30 @@ def main():
         tj.append(e0.elapsed_time(e1))
         tall.append(e0.elapsed_time(e2))
         ttr.append(e2.elapsed_time(e3))
+        tseq.append(e0.elapsed_time(e3))
+    acc.sync(stream)
+    # the same pipeline with the tracker on a second stream beside the interval
+    # kernel (it reads only terminated slots, which the interval never writes)
+    s2 = torch.cuda.Stream()
+    tpipe = []
+    for s in range(steps):
+        k = s % n_sets
+        t.update(t_next[k])
+        it = interval_from_tensors(t, sizes, flag)
+        e0, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        joined = torch.cuda.Event()
+        e0.record()
+        join(k)
+        joined.record()
+        s2.wait_event(joined)
+        acc.run_interval(it, stream)
+        if s % 2:
+            tr.clear(s2.cuda_stream)
+        tr.add(sm, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), s2.cuda_stream)
+        torch.cuda.current_stream().wait_stream(s2)
+        e3.record()
+        e3.synchronize()
+        tpipe.append(e0.elapsed_time(e3))
     acc.sync(stream)
     n_term = int(cnt.sum().item())
     # exposition values of every process row x zone (kacc_format_values), energy and power
@@ -155,6 +179,7 @@ def main():
         "config": cfg, "n_procs": P, "n_nodes": layout.n_nodes, "buckets": H,
         "join_ms": jm, "join_plus_interval_ms": am, "tracker_ms": float(np.median(ttr)),
         "tracker_items": int(tr.items()[0].size),
+        "pipeline_ms": float(np.median(tseq)), "pipeline_tracker_beside_interval_ms": float(np.median(tpipe)),
         "join_rows_per_s": P / (jm * 1e-3), "join_plus_interval_proc_attr_per_s": P / (am * 1e-3),
         "join_bytes": join_bytes, "join_GBps": join_bytes / (jm * 1e-3) / 1e9,
         "terminated_last": n_term, "phase_ms": phases,
