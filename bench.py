@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 5])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
+                    help="BASELINE config; 4 = a 100k-node fleet split over the ranks")
     ap.add_argument("--nodes", type=int, default=None, help="override nodes per GPU")
     ap.add_argument("--distinct", type=int, default=4, help="distinct process-input sets cycled")
     ap.add_argument("--intervals", type=int, default=1,
@@ -118,7 +119,7 @@ def main():
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
     t_setup = time.time()
-    nodes = args.nodes or {2: 1000, 3: 10000, 5: 1000}[args.config]
+    nodes = args.nodes or {2: 1000, 3: 10000, 4: -(-100000 // world), 5: 1000}[args.config]
     layout = fleet.config_layout(args.config, seed=fleet.SEED + 7919 * rank, nodes=nodes)
     sim = fleet.FleetSim(layout, seed=fleet.SEED + 7919 * rank)
     Z = layout.zones
@@ -263,7 +264,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall_max * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == 4 else "weak",
         "vs_baseline": None,
         "dtype": "f64+u64",
         "data": "synthetic (kepler_amd/fleet.py, seed 0x4B45504C; inputs resident in HBM)",
