@@ -387,6 +387,28 @@ int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_
 int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, char *out,
                        uint8_t *len, void *stream);
 
+/* ---- exposition lines (the text around the values) -----
+ * The sample lines of one workload metric family, as Kepler's collector
+ * (power_collector.go:306-436: MustNewConstMetric, whose label pairs
+ * client_golang sorts by name) is written by expfmt's text format:
+ *     NAME{LABELS,zone="ZONE"} VALUE\n
+ * "zone" sorts after every other label name of Kepler's process / container /
+ * VM / pod metrics, so LABELS is the row's other label pairs, name-sorted and
+ * escaped by the caller (`comm="bash",container_id="",...`); VALUE is written
+ * as kacc_format_values writes it.  Lines are row-major: for i in [0, count)
+ * row first + (row_order ? row_order[i] : i), for j in [0, n_zones) the table
+ * zone zone_order ? zone_order[j] : j named zone_names[j].
+ *   name, zone_names, zone_order: HOST; labels, label_off [count + 1] (u64
+ *   offsets into labels, indexed by i's row - first), row_order [count]: DEVICE
+ *   line_off: DEVICE [count * n_zones + 1] byte offset of every line (+ total)
+ *   out: DEVICE buffer of out_cap bytes, or NULL to size only
+ *   *total: HOST, bytes of the whole text.
+ * Synchronous (the total is read back).  KACC_ERANGE when out_cap < *total.   */
+int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const char *name,
+                      const char *const *zone_names, const uint32_t *zone_order, uint32_t n_zones,
+                      const char *labels, const uint64_t *label_off, const uint32_t *row_order,
+                      uint64_t *line_off, char *out, uint64_t out_cap, uint64_t *total, void *stream);
+
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

@@ -76,6 +76,7 @@ TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 # exported symbols, in header order (checked by tests/test_abi.py)
 EXPORTS = [
     "kacc_format_values",
+    "kacc_format_lines",
     "kacc_zone_agg_create",
     "kacc_zone_agg_destroy",
     "kacc_zone_agg_read",
@@ -212,6 +213,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_get_config.argtypes = [c_void_p, POINTER(KaccConfig)]
     lib.kacc_reset.argtypes = [c_void_p]
     lib.kacc_run_interval.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p]
+    lib.kacc_format_lines.argtypes = [c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, c_char_p,
+                                      POINTER(c_char_p), POINTER(ctypes.c_uint32), ctypes.c_uint32,
+                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_uint64,
+                                      POINTER(ctypes.c_uint64), c_void_p]
     lib.kacc_run_intervals.argtypes = [c_void_p, POINTER(KaccInterval), ctypes.c_uint32, c_void_p]
     lib.kacc_sync.argtypes = [c_void_p, c_void_p]
     lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
@@ -381,6 +386,21 @@ class Accel:
         """kacc_format_values: exposition text of table elements (KACC_FMT_WIDTH-byte fields)."""
         self._check(self.lib.kacc_format_values(self.ctx, TABLE_INDEX[name], first, count, c_void_p(out_ptr),
                                                 c_void_p(len_ptr), c_void_p(stream or None)))
+
+    def format_lines(self, name: str, metric: str, first: int, count: int, zone_names, labels_ptr: int,
+                     label_off_ptr: int, line_off_ptr: int, out_ptr: int = 0, out_cap: int = 0,
+                     zone_order=None, row_order_ptr: int = 0, stream: int = 0) -> int:
+        """kacc_format_lines: sample lines of table `name` (device pointers); returns the text size."""
+        t = TABLE_INDEX[name]
+        zn = (c_char_p * len(zone_names))(*[z.encode() for z in zone_names])
+        zo = (ctypes.c_uint32 * len(zone_names))(*zone_order) if zone_order is not None else None
+        total = ctypes.c_uint64(0)
+        self._check(self.lib.kacc_format_lines(self.ctx, t, first, count, metric.encode(), zn, zo, len(zone_names),
+                                               c_void_p(labels_ptr or None), c_void_p(label_off_ptr or None),
+                                               c_void_p(row_order_ptr or None), c_void_p(line_off_ptr or None),
+                                               c_void_p(out_ptr or None), out_cap, ctypes.byref(total),
+                                               c_void_p(stream or None)))
+        return total.value
 
     def namespace_totals(self, n_ns: int, ns_pod_off_ptr: int, ns_pod_slot_ptr: int,
                          out_energy_ptr: int, out_power_ptr: int, stream: int = 0) -> None:

@@ -1818,7 +1818,7 @@ int kacc_sync(kacc_ctx *ctx, void *stream) {
   KACC_HIP(ctx, hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     KACC_HIP(ctx, hipMemset(ctx->d_err, 0, sizeof(uint32_t)));
-    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list 32=oversized node under KACC_F_FAST_NODES)", err);
+    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list 32=oversized node under KACC_F_FAST_NODES 64=join key 128=join range 256=format lines)", err);
   }
   return KACC_OK;
 }

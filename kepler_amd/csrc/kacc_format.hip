@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <string>
+#include <vector>
 
 #include "kacc_internal.hpp"
 #include "kacc_pow5_tables.h"
@@ -271,6 +273,197 @@ __global__ __launch_bounds__(kThreads) void format_kernel(const Args a) {
   a.len[i] = static_cast<uint8_t>(o.n);
 }
 
+// ---- sample lines: NAME{LABELS,zone="ZONE"} VALUE\n ------------------------------
+// Constants of one call, staged in LDS: the metric name, then the zone names.
+constexpr uint32_t kConstCap = 1024;
+constexpr int kLineWaves = 4;  // line_write_kernel: one wave per line in flight
+
+struct LineArgs {
+  const void *src;       // table base
+  uint32_t Z;            // table zones
+  uint32_t is_energy;
+  uint64_t first, count;  // rows (slots) [first, first + count)
+  uint32_t n_zones;
+  const uint32_t *row_order;  // device [count] or NULL
+  const char *labels;         // device
+  const uint64_t *label_off;  // device [count + 1]
+  const char *consts;         // device: name, then zone names
+  uint32_t name_len;
+  uint32_t zone_table[KACC_MAX_ZONES];  // table zone of line zone j
+  uint32_t zone_pos[KACC_MAX_ZONES + 1];  // zone name j = consts[zone_pos[j] .. zone_pos[j+1])
+  uint32_t const_len;
+  char *vals;        // temp [lines * KACC_FMT_WIDTH]
+  uint8_t *vlen;     // temp [lines]
+  uint64_t *len;     // temp [lines + 1]
+  uint64_t *line_off;  // [lines + 1]
+  char *out;
+  uint64_t out_cap;
+  uint32_t *err;       // context error word (a line past out_cap is not written)
+};
+
+__device__ __forceinline__ uint64_t line_row(const LineArgs &a, uint64_t r) {
+  // a row_order entry past the range is clamped: wrong text, never a fault
+  return a.row_order ? min(static_cast<uint64_t>(a.row_order[r]), a.count - 1) : r;
+}
+
+// Pass 1: the value field of every line and the line's length.
+__global__ __launch_bounds__(kThreads) void line_len_kernel(const LineArgs a) {
+  const uint64_t lines = a.count * a.n_zones;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < lines;
+       i += static_cast<uint64_t>(gridDim.x) * kThreads) {
+    const uint64_t ri = i / a.n_zones;
+    const uint32_t j = static_cast<uint32_t>(i - ri * a.n_zones);
+    const uint64_t r = line_row(a, ri);
+    const uint64_t e = (a.first + r) * a.Z + a.zone_table[j];
+    double f;
+    if (a.is_energy)
+      f = static_cast<double>(static_cast<const uint64_t *>(a.src)[e]) / 1e6;  // energy.go:30-32
+    else
+      f = static_cast<const double *>(a.src)[e] / 1e6;  // energy.go:57-59
+    Field o;
+    write_float(f, o);
+    uint64_t w[3] = {0, 0, 0};
+    for (uint32_t k = 0; k < o.n; ++k) w[k >> 3] |= static_cast<uint64_t>(static_cast<uint8_t>(o.c[k])) << (8 * (k & 7));
+    uint64_t *dst = reinterpret_cast<uint64_t *>(a.vals + i * KACC_FMT_WIDTH);
+    dst[0] = w[0];
+    dst[1] = w[1];
+    dst[2] = w[2];
+    a.vlen[i] = static_cast<uint8_t>(o.n);
+    const uint64_t ll = a.label_off[r + 1] - a.label_off[r];
+    const uint32_t zl = a.zone_pos[j + 1] - a.zone_pos[j];
+    // NAME { LABELS ,zone=" ZONE "}<sp> VALUE \n
+    a.len[i] = a.name_len + 1 + ll + 7 + zl + 3 + o.n + 1;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.len[lines] = 0;
+}
+
+// Pass 2: a wave takes 64 consecutive lines: lane l loads line (base + l)'s
+// offsets in one round trip, then the wave writes the 64 lines one after the
+// other, lane l writing bytes l, l + 64, ... of the line (64 contiguous bytes
+// per store instruction); each line's words are broadcast with readlane.
+__device__ __forceinline__ uint64_t bcast64(uint64_t x, int k) {
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(x), k);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(x >> 32), k);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineArgs a) {
+  __shared__ char s_c[kConstCap];
+  for (uint32_t k = threadIdx.x; k < a.const_len; k += 64 * kLineWaves) s_c[k] = a.consts[k];
+  __syncthreads();
+  const uint64_t lines = a.count * a.n_zones;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kLineWaves * 64;
+  for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kLineWaves + (threadIdx.x >> 6)) * 64; base < lines;
+       base += step) {
+    // ---- this lane's line: offsets and lengths (all loads in flight together)
+    const uint64_t i = min(base + lane, lines - 1);
+    const uint64_t ri = i / a.n_zones;
+    const uint32_t j = static_cast<uint32_t>(i - ri * a.n_zones);
+    const uint64_t r = line_row(a, ri);
+    const uint64_t l0 = a.label_off[r], l1 = a.label_off[r + 1];
+    const uint64_t o0 = a.line_off[i], o1 = a.line_off[i + 1];
+    const uint32_t vl = a.vlen[i];
+    const uint32_t zpair = (a.zone_pos[j] << 16) | (a.zone_pos[j + 1] - a.zone_pos[j]);  // z0 | zl
+    const uint32_t nl = static_cast<uint32_t>(min<uint64_t>(lines - base, 64));
+    for (uint32_t k = 0; k < nl; ++k) {
+      const uint64_t L0 = bcast64(l0, k), LL = bcast64(l1, k) - L0;
+      const uint64_t O0 = bcast64(o0, k), N = bcast64(o1, k) - O0;
+      const uint32_t VL = __builtin_amdgcn_readlane(vl, k), ZP = __builtin_amdgcn_readlane(zpair, k);
+      const uint32_t z0 = ZP >> 16, zl = ZP & 0xffffu;
+      if (O0 > a.out_cap || N > a.out_cap - O0) {  // cannot happen with a consistent scan
+        if (lane == 0) atomicOr(a.err, 1u << 8);
+        continue;
+      }
+      const char *val = a.vals + (base + k) * KACC_FMT_WIDTH;
+      const uint64_t cL = a.name_len + 1, cD = cL + LL, cE = cD + 7, cF = cE + zl, cG = cF + 3, cH = cG + VL;
+      for (uint64_t p = lane; p < N; p += 64) {
+        char c;
+        if (p < a.name_len) c = s_c[p];
+        else if (p < cL) c = '{';
+        else if (p < cD) c = a.labels[L0 + (p - cL)];
+        else if (p < cE) c = ",zone=\""[p - cD];
+        else if (p < cF) c = s_c[z0 + (p - cE)];
+        else if (p < cG) c = "\"} "[p - cF];
+        else if (p < cH) c = val[p - cG];
+        else c = '\n';
+        a.out[O0 + p] = c;
+      }
+    }
+  }
+}
+
+// Exclusive scan of the u64 line lengths (reduce-then-scan, three launches,
+// no inter-workgroup communication inside a launch): tiles of kTile lengths.
+constexpr int kScanThreads = 256;
+constexpr int kScanPer = 16;
+constexpr uint64_t kTile = static_cast<uint64_t>(kScanThreads) * kScanPer;
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t *s_w, uint64_t &total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_w[wave] = x;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    if (w < wave) base += s_w[w];
+    tot += s_w[w];
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_tile_sums(const uint64_t *in, uint64_t n, uint64_t *tile_sum) {
+  __shared__ uint64_t s_w[kScanThreads / 64];
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile + static_cast<uint64_t>(threadIdx.x) * kScanPer;
+  uint64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) x += t0 + k < n ? in[t0 + k] : 0;
+  uint64_t total;
+  (void)block_excl_scan(x, s_w, total);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = total;
+}
+
+// one workgroup: tile_sum -> exclusive prefixes, in place
+__global__ __launch_bounds__(kScanThreads) void scan_tile_prefix(uint64_t *tile_sum, uint64_t tiles) {
+  __shared__ uint64_t s_w[kScanThreads / 64];
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < tiles; b += kScanThreads) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t v = i < tiles ? tile_sum[i] : 0;
+    uint64_t total;
+    const uint64_t ex = block_excl_scan(v, s_w, total);
+    if (i < tiles) tile_sum[i] = carry + ex;
+    carry += total;
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_tiles(const uint64_t *in, uint64_t n, const uint64_t *tile_prefix,
+                                                            uint64_t *out) {
+  __shared__ uint64_t s_w[kScanThreads / 64];
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile + static_cast<uint64_t>(threadIdx.x) * kScanPer;
+  uint64_t v[kScanPer], x = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = t0 + k < n ? in[t0 + k] : 0;
+    x += v[k];
+  }
+  uint64_t total;
+  uint64_t run = tile_prefix[blockIdx.x] + block_excl_scan(x, s_w, total);
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (t0 + k < n) out[t0 + k] = run;
+    run += v[k];
+  }
+}
+
 }  // namespace fmt
 }  // namespace kacc
 
@@ -306,6 +499,101 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
                      st, a);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
+}
+
+int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const char *name,
+                      const char *const *zone_names, const uint32_t *zone_order, uint32_t n_zones,
+                      const char *labels, const uint64_t *label_off, const uint32_t *row_order,
+                      uint64_t *line_off, char *out, uint64_t out_cap, uint64_t *total, void *stream) {
+  if (!ctx || t < 0 || t >= KACC_T_COUNT || !total) return KACC_EINVAL;
+  *total = 0;
+  const uint32_t Z = ctx->cfg.zones;
+  const bool energy = t == KACC_T_PROC_ENERGY || t == KACC_T_CTR_ENERGY || t == KACC_T_VM_ENERGY ||
+                      t == KACC_T_POD_ENERGY;
+  const bool power = t == KACC_T_PROC_POWER || t == KACC_T_CTR_POWER || t == KACC_T_VM_POWER ||
+                     t == KACC_T_POD_POWER;
+  if (!energy && !power) return kacc_fail(ctx, KACC_EINVAL, "table %d is not a workload energy or power table", (int)t);
+  const uint64_t slots = ctx->counts[t] / Z;
+  if (first > slots || count > slots - first)
+    return kacc_fail(ctx, KACC_EINVAL, "format_lines: rows outside table %d", (int)t);
+  if (!name || !zone_names || n_zones == 0 || n_zones > Z)
+    return kacc_fail(ctx, KACC_EINVAL, "format_lines: name / zone names missing or n_zones > %u", Z);
+  if (count && (!labels || !label_off || !line_off))
+    return kacc_fail(ctx, KACC_EINVAL, "format_lines: NULL device array");
+  kacc::fmt::LineArgs a{};
+  std::string consts(name);
+  a.name_len = static_cast<uint32_t>(consts.size());
+  for (uint32_t j = 0; j < n_zones; ++j) {
+    const uint32_t z = zone_order ? zone_order[j] : j;
+    if (z >= Z || !zone_names[j]) return kacc_fail(ctx, KACC_EINVAL, "format_lines: bad zone %u", j);
+    a.zone_table[j] = z;
+    a.zone_pos[j] = static_cast<uint32_t>(consts.size());
+    consts += zone_names[j];
+  }
+  a.zone_pos[n_zones] = static_cast<uint32_t>(consts.size());
+  if (consts.size() > kacc::fmt::kConstCap)
+    return kacc_fail(ctx, KACC_EINVAL, "format_lines: name + zone names exceed %u bytes", kacc::fmt::kConstCap);
+  if (!count) return KACC_OK;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const uint64_t lines = count * n_zones;
+  a.src = ctx->tables[t];
+  a.Z = Z;
+  a.is_energy = energy ? 1u : 0u;
+  a.first = first;
+  a.count = count;
+  a.n_zones = n_zones;
+  a.row_order = row_order;
+  a.labels = labels;
+  a.label_off = label_off;
+  a.const_len = static_cast<uint32_t>(consts.size());
+  a.line_off = line_off;
+  a.out = out;
+  a.out_cap = out_cap;
+  a.err = ctx->d_err;
+  // temporaries, stream ordered: consts, value fields, lengths, tile sums
+  const uint64_t tiles = (lines + 1 + kacc::fmt::kTile - 1) / kacc::fmt::kTile;
+  if (tiles > 0x7fffffffull) return kacc_fail(ctx, KACC_EINVAL, "format_lines: too many lines");
+  const size_t scan_bytes = 8 * tiles;
+  char *tmp = nullptr;
+  // every sub-buffer 256-B aligned (the scan's look-back state needs aligned storage)
+  auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
+  const uint64_t off_vals = 1024, off_vlen = al(off_vals + lines * KACC_FMT_WIDTH),
+                 off_len = al(off_vlen + lines), off_scan = al(off_len + 8 * (lines + 1));
+  KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), off_scan + scan_bytes, st));
+  a.consts = tmp;
+  a.vals = tmp + off_vals;
+  a.vlen = reinterpret_cast<uint8_t *>(tmp + off_vlen);
+  a.len = reinterpret_cast<uint64_t *>(tmp + off_len);
+  int rc = KACC_OK;
+  auto done = [&](int code) {
+    (void)hipFreeAsync(tmp, st);
+    return code;
+  };
+  if (hipMemcpyAsync(tmp, consts.data(), consts.size(), hipMemcpyHostToDevice, st) != hipSuccess)
+    return done(kacc_fail(ctx, KACC_EHIP, "format_lines: constants upload"));
+  (void)hipGetLastError();
+  const uint64_t g1 = std::min<uint64_t>((lines + kacc::fmt::kThreads - 1) / kacc::fmt::kThreads, 1u << 20);
+  hipLaunchKernelGGL(kacc::fmt::line_len_kernel, dim3(static_cast<uint32_t>(g1)), dim3(kacc::fmt::kThreads), 0, st, a);
+  uint64_t *tile_sum = reinterpret_cast<uint64_t *>(tmp + off_scan);
+  const dim3 gt(static_cast<uint32_t>(tiles)), bt(kacc::fmt::kScanThreads);
+  hipLaunchKernelGGL(kacc::fmt::scan_tile_sums, gt, bt, 0, st, a.len, lines + 1, tile_sum);
+  hipLaunchKernelGGL(kacc::fmt::scan_tile_prefix, dim3(1), bt, 0, st, tile_sum, tiles);
+  hipLaunchKernelGGL(kacc::fmt::scan_tiles, gt, bt, 0, st, a.len, lines + 1, tile_sum, line_off);
+  if (hipGetLastError() != hipSuccess) return done(kacc_fail(ctx, KACC_EHIP, "format_lines: scan launch"));
+  if (hipMemcpyAsync(total, line_off + lines, sizeof(uint64_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return done(kacc_fail(ctx, KACC_EHIP, "format_lines: %s", hipGetErrorString(hipGetLastError())));
+  if (!out) return done(KACC_OK);  // sizing call
+  if (out_cap < *total)
+    return done(kacc_fail(ctx, KACC_ERANGE, "format_lines: %llu bytes of text, out_cap %llu",
+                          (unsigned long long)*total, (unsigned long long)out_cap));
+  const uint64_t g2 = std::min<uint64_t>((lines + 64 * kacc::fmt::kLineWaves - 1) / (64 * kacc::fmt::kLineWaves),
+                                         1u << 14);
+  hipLaunchKernelGGL(kacc::fmt::line_write_kernel, dim3(static_cast<uint32_t>(g2)), dim3(64 * kacc::fmt::kLineWaves),
+                     0, st, a);
+  if (hipGetLastError() != hipSuccess) rc = kacc_fail(ctx, KACC_EHIP, "format_lines: launch");
+  return done(rc);
 }
 
 }  // extern "C"

@@ -86,3 +86,19 @@ def joules(e: int) -> float:
 
 def watts(p: float) -> float:
     return p / 1e6
+
+
+def escape_label_value(v: str) -> str:
+    """expfmt text format label-value escaping: backslash, double quote, newline."""
+    return v.replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n")
+
+
+def label_pairs(pairs) -> str:
+    """`name="value",...` in label-name order (client_golang MakeLabelPairs sorts by name)."""
+    return ",".join(f'{k}="{escape_label_value(v)}"' for k, v in sorted(pairs))
+
+
+def sample_line(metric: str, labels: str, zone: str, value: float) -> str:
+    """One expfmt text line of a Kepler workload metric; "zone" sorts after every
+    other label of the process / container / VM / pod families."""
+    return f'{metric}{{{labels},zone="{escape_label_value(zone)}"}} {write_float(value)}\n'

@@ -93,3 +93,66 @@ def test_format_random(kind):
         if len(bad) > 10:
             break
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("table,metric", [
+    ("proc_energy", "kepler_process_cpu_joules_total"),
+    ("pod_power", "kepler_pod_cpu_watts"),
+])
+def test_format_lines_byte_exact(table, metric):
+    """kacc_format_lines: NAME{LABELS,zone="ZONE"} VALUE lines, byte for byte against
+    oracle/gofmt.sample_line, with escaped label values, a row permutation, a
+    zone subset in a caller-chosen order and a sizing call first."""
+    from kepler_amd.torch_batch import current_stream_handle
+    from oracle.gofmt import label_pairs, sample_line
+
+    rng = np.random.default_rng(17)
+    Z, slots, first, count = 4, 700, 37, 600
+    acc = accel.Accel(Z, nodes=1, proc_slots=slots, ctr_slots=1, vm_slots=1, pod_slots=slots)
+    if table.endswith("energy"):
+        vals = rng.integers(0, 2**40, size=slots * Z, dtype=np.uint64)
+        vals[:8] = [0, 10**6, 1, 2**64 - 1, 123, 10**12, 5 * 10**5, 10**19]
+    else:
+        vals = rng.random(slots * Z) * 10.0 ** rng.integers(-3, 9, size=slots * Z)
+        vals[:6] = [0.0, 1e6, -1e6, float("nan"), float("inf"), 1e-300]
+    acc.upload(table, vals)
+    alphabet = ['a', 'Z', '0', '/', '-', '"', '\\', '\n', 'é', ' ', '{', '=']
+    rows = []
+    for r in range(count):
+        comm = "".join(rng.choice(alphabet, size=int(rng.integers(0, 12))))
+        rows.append(label_pairs([("pid", str(1000 + r)), ("comm", comm), ("container_id", ""),
+                                 ("exe", "/usr/bin/" + comm), ("state", "running"), ("type", "regular"),
+                                 ("vm_id", "")]).encode())
+    label_off = np.r_[0, np.cumsum([len(x) for x in rows])].astype(np.uint64)
+    d_labels = torch.from_numpy(np.frombuffer(b"".join(rows), dtype=np.uint8).copy()).cuda()
+    d_loff = torch.from_numpy(label_off.view(np.int64)).cuda()
+    order = rng.permutation(count).astype(np.uint32)
+    d_order = torch.from_numpy(order.view(np.int32)).cuda()
+    zone_order, zone_names = [3, 0, 2], ["dram", "package", "uncore"]
+    n_lines = count * len(zone_order)
+    d_line_off = torch.zeros(n_lines + 1, dtype=torch.int64, device="cuda")
+    s = current_stream_handle()
+    args = (table, metric, first, count, zone_names, d_labels.data_ptr(), d_loff.data_ptr(), d_line_off.data_ptr())
+    total = acc.format_lines(*args, zone_order=zone_order, row_order_ptr=d_order.data_ptr(), stream=s)
+    with pytest.raises(accel.AccelError):  # too small a buffer: KACC_ERANGE, nothing written
+        small = torch.zeros(16, dtype=torch.uint8, device="cuda")
+        acc.format_lines(*args, out_ptr=small.data_ptr(), out_cap=16, zone_order=zone_order,
+                         row_order_ptr=d_order.data_ptr(), stream=s)
+    out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+    assert acc.format_lines(*args, out_ptr=out.data_ptr(), out_cap=total, zone_order=zone_order,
+                            row_order_ptr=d_order.data_ptr(), stream=s) == total
+    acc.sync(s)
+    conv = (lambda v: joules(int(v))) if table.endswith("energy") else (lambda v: watts(float(v)))
+    want = []
+    for i in range(count):
+        r = int(order[i])
+        labels = rows[r].decode()
+        for z, zn in zip(zone_order, zone_names):
+            want.append(sample_line(metric, labels, zn, conv(vals[(first + r) * Z + z])))
+    want = "".join(want).encode()
+    got = bytes(out.cpu().numpy())
+    assert len(got) == len(want)
+    assert got == want
+    offs = d_line_off.cpu().numpy()
+    assert offs[-1] == total and np.all(np.diff(offs) > 0)
+    acc.close()
