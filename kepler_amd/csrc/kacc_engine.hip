@@ -49,10 +49,11 @@ constexpr int kNsUnroll = 4;                 // pods in flight per namespace lan
 constexpr int kVarSkipAggregates = 1;  // skip containers / VMs / pods
 constexpr int kVarSkipProcs = 2;       // skip the process attribution pass
 constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
-constexpr int kVarNtStores = 8;        // non-temporal stores for the row outputs
+constexpr int kVarTemporalStores = 8;  // plain (temporal) stores for the row outputs
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
 constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
 constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row order only)
+constexpr int kVarTemporalLoads = 16384;  // plain loads of the streamed inputs and prev totals
 constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
 constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
 constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk kernel idles)
@@ -267,7 +268,7 @@ __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, 
 // slot p div (Z/2); pieces past len or the table end are masked.
 // Loads are unconditional (a masked piece reads slot `safe`, a valid slot,
 // and is zeroed): no exec-mask branches, so every group's loads stay in flight.
-template <int Z, bool kMasked>
+template <int Z, bool kMasked, bool kNtLoad = false>
 __device__ __forceinline__ void load_group_masked(const uint64_t *__restrict__ base, uint64_t s0,
                                                   uint32_t len, uint64_t safe, uint64_t (&out)[Z]) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
@@ -279,13 +280,14 @@ __device__ __forceinline__ void load_group_masked(const uint64_t *__restrict__ b
   for (int j = 0; j < kHalf; ++j) {
     const uint32_t piece = lane + 64u * j;
     if constexpr (!kMasked) {  // a full group of consecutive slots
-      const u64x2 x = p[piece];
+      const u64x2 x = kNtLoad ? __builtin_nontemporal_load(p + piece) : p[piece];
       out[2 * j] = x.x;
       out[2 * j + 1] = x.y;
       continue;
     }
     const bool ok = piece / kHalf < len;
-    const u64x2 x = *(ok ? p + piece : q);
+    const u64x2 *src = ok ? p + piece : q;
+    const u64x2 x = kNtLoad ? __builtin_nontemporal_load(src) : *src;
     out[2 * j] = ok ? x.x : 0ull;
     out[2 * j + 1] = ok ? x.y : 0ull;
   }
@@ -428,7 +430,11 @@ __global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : 6)
 void interval_kernel(const kacc_interval b, const DevState st) {
   constexpr int kThreads = kTpb<V>;
   constexpr int kRowsPerThread = kRpt<V>;
-  constexpr bool kNT = (V & kVarNtStores) != 0;
+  // non-temporal hints on the row streams (read once / written once per
+  // interval, 2.5 GB at config 3: nothing to keep in L2 or the Infinity
+  // Cache): loads + stores together measured 5 % faster (profiles/r01/ablations)
+  constexpr bool kNT = (V & kVarTemporalStores) == 0;
+  constexpr bool kNtLd = (V & kVarTemporalLoads) == 0;
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
   __shared__ uint32_t s_w[kRowsLds];  // and their slot words (frees VGPRs across barriers)
   __shared__ double s_cd[kThreads];  // container Δ of this interval
@@ -483,8 +489,13 @@ void interval_kernel(const kacc_interval b, const DevState st) {
   for (int k = 0; k < kRowsPerThread; ++k) {
     const uint32_t r = tid + k * kThreads;
     const bool in = r < rows;
-    d[k] = in ? dcpu[r] : 0.0;
-    w[k] = in ? pslot[r] : 0xffffffffu;
+    if constexpr (kNtLd) {
+      d[k] = in ? __builtin_nontemporal_load(dcpu + r) : 0.0;
+      w[k] = in ? __builtin_nontemporal_load(pslot + r) : 0xffffffffu;
+    } else {
+      d[k] = in ? dcpu[r] : 0.0;
+      w[k] = in ? pslot[r] : 0xffffffffu;
+    }
   }
   // aggregate role of this lane: 1 container, 2 VM, 3 pod
   // role/index/validity are recomputed from tid and the node's (SGPR) counts
@@ -563,7 +574,7 @@ void interval_kernel(const kacc_interval b, const DevState st) {
         for (int k = 0; k < kRowsPerThread; ++k) {
           const uint32_t pos0 = static_cast<uint32_t>(tid & ~63) + k * kThreads;
           const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
-          load_group_masked<Z, true>(st.proc_energy, static_cast<uint64_t>(smin) + pos0, len, smin,
+          load_group_masked<Z, true, kNtLd>(st.proc_energy, static_cast<uint64_t>(smin) + pos0, len, smin,
                                      prev[k]);
         }
       }
@@ -575,7 +586,7 @@ void interval_kernel(const kacc_interval b, const DevState st) {
           const uint64_t g0 = uniform_u32(static_cast<uint32_t>(sl));  // lane 0's slot
           if (__all((tid + k * kThreads) < rows && sl == g0 + (tid & 63) && g0 + 64 <= st.proc_slots)) {
             contig |= 1u << k;
-            load_group_masked<Z, false>(st.proc_energy, g0, 64u, g0, prev[k]);
+            load_group_masked<Z, false, kNtLd>(st.proc_energy, g0, 64u, g0, prev[k]);
             continue;
           }
         }
@@ -955,7 +966,11 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
                                                                            const DevState st) {
   constexpr int kThreads = kChunkThreads;
   constexpr int kR = kChunkRpt;
-  constexpr bool kNT = (V & kVarNtStores) != 0;
+  // non-temporal hints on the row streams (read once / written once per
+  // interval, 2.5 GB at config 3: nothing to keep in L2 or the Infinity
+  // Cache): loads + stores together measured 5 % faster (profiles/r01/ablations)
+  constexpr bool kNT = (V & kVarTemporalStores) == 0;
+  constexpr bool kNtLd = (V & kVarTemporalLoads) == 0;
   constexpr bool kT = kTransposed<Z> && (V & kVarNoTranspose) == 0;
   constexpr bool kAgg = (V & kVarSkipAggregates) == 0;
   __shared__ double s_d[kChunkRows];
@@ -1005,8 +1020,8 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
     for (int u = 0; u < kR; ++u) {
       const uint32_t r = utid + u * kThreads;
       const bool in = r < rows;
-      d[u] = in ? dcpu[r] : 0.0;
-      w[u] = in ? pslot[r] : 0xffffffffu;
+      d[u] = in ? (kNtLd ? __builtin_nontemporal_load(dcpu + r) : dcpu[r]) : 0.0;
+      w[u] = in ? (kNtLd ? __builtin_nontemporal_load(pslot + r) : pslot[r]) : 0xffffffffu;
     }
     uint64_t prev[kR][Z];
     uint32_t contig = 0;
@@ -1020,7 +1035,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
                             s0 + 64 <= st.proc_slots;
           if (__all(mine)) {
             contig |= 1u << u;
-            load_group_masked<Z, false>(st.proc_energy, s0, 64u, s0, prev[u]);
+            load_group_masked<Z, false, kNtLd>(st.proc_energy, s0, 64u, s0, prev[u]);
             continue;
           }
         }
@@ -1235,7 +1250,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
 // the deferred list itself is re-armed by the next interval_kernel.
 template <int Z, int V>
 __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, const DevState st) {
-  constexpr bool kNT = (V & kVarNtStores) != 0;
+  constexpr bool kNT = (V & kVarTemporalStores) == 0;  // as interval_kernel
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) {
     st.item_ctr[0] = 0u;
@@ -1504,6 +1519,8 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 768: launch_zv<4, 768>(b, s, st); return true;
     case 1024: launch_zv<4, 1024>(b, s, st); return true;
     case 2048: launch_zv<4, 2048>(b, s, st); return true;
+    case 16384: launch_zv<4, 16384>(b, s, st); return true;
+    case 16392: launch_zv<4, 16392>(b, s, st); return true;
     default: return false;
   }
 }
