@@ -393,8 +393,9 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
  * client_golang sorts by name) is written by expfmt's text format:
  *     NAME{LABELS,zone="ZONE"} VALUE\n
  * "zone" sorts after every other label name of Kepler's process / container /
- * VM / pod metrics, so LABELS is the row's other label pairs, name-sorted and
- * escaped by the caller (`comm="bash",container_id="",...`); VALUE is written
+ * VM / pod metrics (power_collector.go:128-139, and the node_name const label
+ * of :63-95), so LABELS is the row's other label pairs incl. node_name,
+ * name-sorted and escaped by the caller (`comm="bash",...`); VALUE is written
  * as kacc_format_values writes it.  Lines are row-major: for i in [0, count)
  * row first + (row_order ? row_order[i] : i), for j in [0, n_zones) the table
  * zone zone_order ? zone_order[j] : j named zone_names[j].

@@ -53,3 +53,25 @@ def test_round_trip_and_shortest():
         assert float(s) == x, (x, s)
         mant = s.split("e")[0].replace(".", "").replace("-", "").lstrip("0")
         assert len(mant) <= 17
+
+
+def test_sample_line_layout_and_escaping():
+    """expfmt text: label pairs sorted by name (client_golang MakeLabelPairs),
+    label values escaped (backslash, double quote, newline), zone last."""
+    from oracle.gofmt import escape_label_value, label_pairs, sample_line
+
+    assert escape_label_value('a"b\\c\nd') == 'a\\"b\\\\c\\nd'
+    # node_name is the descriptors' const label (power_collector.go:17, :63-95), merged and sorted
+    labels = label_pairs([("pid", "42"), ("comm", 'sh "x"'), ("vm_id", ""), ("container_id", "c1"),
+                          ("exe", "/bin/sh"), ("state", "running"), ("type", "container"), ("node_name", "n7")])
+    assert labels == ('comm="sh \\"x\\"",container_id="c1",exe="/bin/sh",node_name="n7",pid="42",'
+                      'state="running",type="container",vm_id=""')
+    assert sample_line("kepler_process_cpu_joules_total", labels, "package", joules(1_500_000)) == (
+        'kepler_process_cpu_joules_total{' + labels + ',zone="package"} 1.5\n')
+    assert sample_line("kepler_pod_cpu_watts", 'pod_id="p"', "dram", watts(0.0)).endswith('zone="dram"} 0\n')
+    # "zone" sorts after every other label name of the workload families
+    # (power_collector.go:128-139, plus the node_name const label)
+    for names in (["comm", "container_id", "exe", "pid", "state", "type", "vm_id"],
+                  ["container_id", "container_name", "pod_id", "runtime", "state"],
+                  ["hypervisor", "state", "vm_id", "vm_name"], ["pod_id", "pod_name", "pod_namespace", "state"]):
+        assert sorted(names + ["node_name", "zone"])[-1] == "zone"
