@@ -1,0 +1,52 @@
+"""The C++ oracle (kepler_oracle.cpp) against an independent pure-Python
+restatement written in Go's shape (oracle/pyref.py) — CPU.
+
+Every state table bit for bit, over multi-interval fleets with churn (new
+slots), counter wraparound (fake-meter MaxEnergy 1e6), zero usage ratios,
+read errors, empty and single-process nodes, VMs and pods; the C++ oracle in
+listing-order summation mode (the Go map order replaced by /proc order).
+"""
+
+import numpy as np
+import pytest
+
+from kepler_amd import accel, fleet
+from oracle.pyref import PyRef, duration_seconds, go_float64_to_uint64
+
+
+def test_go_conversions():
+    assert go_float64_to_uint64(1.9) == 1
+    assert go_float64_to_uint64(-0.5) == 0
+    assert go_float64_to_uint64(-1.5) == (1 << 64) - 1       # int64(-1) as uint64
+    assert go_float64_to_uint64(float("nan")) == 1 << 63     # CVTTSD2SQ indefinite
+    assert go_float64_to_uint64(2.0 ** 63) == 1 << 63
+    assert go_float64_to_uint64(2.0 ** 64) == 1 << 63        # out of range -> indefinite | 1<<63
+    assert duration_seconds(5_000_000_001) == 5.000000001
+    assert duration_seconds(-1_500_000_000) == -1.5
+
+
+FLEETS = [
+    ("z2-small", dict(n_nodes=6, procs_per_node=[40, 0, 1, 300, 7, 64], zones=2, vm_frac=0.05, procs_per_vm=2)),
+    ("z4-churn", dict(n_nodes=5, procs_per_node=[200, 150, 90, 3, 500], zones=4, shuffle_slots=True)),
+    ("z3-odd", dict(n_nodes=4, procs_per_node=[33, 257, 1, 80], zones=3, vm_frac=0.1, procs_per_vm=3)),
+]
+
+
+@pytest.mark.parametrize("max_energy", [fleet.MAX_ENERGY_RAPL, fleet.MAX_ENERGY_FAKE], ids=["rapl", "wrap"])
+@pytest.mark.parametrize("name,kw", FLEETS, ids=[f[0] for f in FLEETS])
+def test_cpp_oracle_matches_python_restatement(name, kw, max_energy, oracle_lib):
+    from oracle.oracle import KOR_SUM_LISTING, Oracle
+
+    layout = fleet.make_layout(seed=5, **kw)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=5, churn=0.1, read_error_frac=0.15, zero_ratio_frac=0.1,
+                         max_energy=max_energy)
+    ora = Oracle(layout.zones, **caps, sum_mode=KOR_SUM_LISTING)
+    ref = PyRef(layout.zones)
+    for k in range(5):
+        a = sim.next_interval()
+        ora.interval(a, layout.sizes())
+        ref.interval(a)
+        got = ref.tables(layout.n_nodes, caps)
+        for tname, _ in accel.TABLES:
+            np.testing.assert_array_equal(ora.state[tname], got[tname], err_msg=f"interval {k} {tname}")
