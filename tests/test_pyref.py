@@ -43,8 +43,13 @@ def test_cpp_oracle_matches_python_restatement(name, kw, max_energy, oracle_lib)
                          max_energy=max_energy)
     ora = Oracle(layout.zones, **caps, sum_mode=KOR_SUM_LISTING)
     ref = PyRef(layout.zones)
+    rng = np.random.default_rng(11)
     for k in range(5):
         a = sim.next_interval()
+        if k:  # containers / VMs / pods recreated in their slots (no previous entry)
+            for key in ("ctr_slot", "vm_slot", "pod_slot"):
+                a[key] = a[key] | np.where(rng.random(a[key].size) < 0.2, np.uint32(accel.KACC_SLOT_NEW),
+                                           np.uint32(0)).astype(np.uint32)
         ora.interval(a, layout.sizes())
         ref.interval(a)
         got = ref.tables(layout.n_nodes, caps)
