@@ -385,3 +385,25 @@ def test_run_intervals_matches_sequential(name, kw):
     for tname, _ in accel.TABLES:
         np.testing.assert_array_equal(acc.download(tname), ora.state[tname], err_msg=tname)
     acc.close()
+
+
+def test_recreated_aggregates_bit_exact():
+    """Containers / VMs / pods recreated in their slots (NEW on aggregate slot
+    words after the first interval): totals restart, CPU caches reset."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(12, [300, 2000, 1, 0, 700, 64] * 2, 4, seed=13, vm_frac=0.05, procs_per_vm=2)
+    sim = fleet.FleetSim(layout, seed=13, churn=0.05, read_error_frac=0.05)
+    eng = EngineBackend(layout.zones, layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    rng = np.random.default_rng(3)
+    for k in range(5):
+        a = sim.next_interval()
+        if k:
+            for key in ("ctr_slot", "vm_slot", "pod_slot"):
+                a[key] = a[key] | np.where(rng.random(a[key].size) < 0.2, np.uint32(accel.KACC_SLOT_NEW),
+                                           np.uint32(0)).astype(np.uint32)
+        eng.interval(a, layout.sizes(), layout.fast_flag())
+        ora.interval(a, layout.sizes())
+        for name, _ in accel.TABLES:
+            np.testing.assert_array_equal(eng.table(name), ora.state[name], err_msg=f"interval {k} {name}")
