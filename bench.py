@@ -89,6 +89,24 @@ def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds):
             done += sizes["n_procs"]
             k += 1
         out[name] = dict(value=done / t_run, intervals=k, seconds=t_run)
+    # the flat-array port on the host's cores (node ranges per thread), on a
+    # 10x larger node sample: the strongest CPU number this repo can produce
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    nodes_mt = np.arange(min(10 * n_nodes, layout.n_nodes))
+    subs_mt = [fleet.subset_interval(a, nodes_mt, layout.zones) for a in intervals[:3]]
+    _, sizes_mt, _ = subs_mt[0]
+    o = Oracle(layout.zones, nodes=sizes_mt["n_nodes"], proc_slots=sizes_mt["n_procs"],
+               ctr_slots=sizes_mt["n_ctrs"], vm_slots=sizes_mt["n_vms"], pod_slots=sizes_mt["n_pods"])
+    o.interval_mt(subs_mt[0][0], sizes_mt, threads)
+    done, t_run, k = 0, 0.0, 0
+    while t_run < 5.0:
+        a = subs_mt[1 + k % 2][0]
+        t0 = time.perf_counter()
+        o.interval_mt(a, sizes_mt, threads)
+        t_run += time.perf_counter() - t0
+        done += sizes_mt["n_procs"]
+        k += 1
+    out["soa_mt"] = dict(value=done / t_run, threads=threads, intervals=k, procs=sizes_mt["n_procs"])
     return out, sizes
 
 
@@ -315,6 +333,8 @@ def main():
                       f"maps, per-object zone maps), first {cs['n_nodes']} nodes of the same fleet "
                       f"({cs['n_procs']} procs, Z={Z}), {gf['intervals']} intervals in {gf['seconds']:.1f}s",
             "soa_port_1thread": res["soa"]["value"],
+            "soa_port_threads": {"value": res["soa_mt"]["value"], "threads": res["soa_mt"]["threads"],
+                                 "sample": f"{res['soa_mt']['procs']} procs, {res['soa_mt']['intervals']} intervals"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
 

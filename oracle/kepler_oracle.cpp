@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -123,6 +124,131 @@ void attribute(uint32_t Z, double cpu_delta, double node_delta, const NodeZ &nz,
 
 }  // namespace
 
+// One node of kor_interval (nodes are independent: disjoint state rows).
+static void node_interval(kor_state *st, const kacc_interval *b, uint32_t n, int sum_mode) {
+  const uint32_t Z = st->zones;
+  const uint32_t status = b->node_status ? b->node_status[n] : 0u;
+  if (status & KACC_NODE_READ_ERROR) {
+    // node.go:39-44 joins the read error; calculatePower returns it
+    // (monitor.go:401-403) and refreshSnapshot keeps the old snapshot
+    // (monitor.go:332-334) without calling Refresh.
+    st->node_status[n] = KACC_NODE_SKIPPED;
+    return;
+  }
+  const bool first_read = st->node_has_prev[n] == 0;  // monitor.go:326-330
+  const double ratio = b->node_usage_ratio[n];
+  const int64_t now = b->node_ts_ns[n];
+  NodeZ nz;
+
+  // ---- node zones: node.go:10-84 (calculateNodePower) / node.go:101-131 (firstNodeRead)
+  double time_diff = 0;
+  if (!first_read) time_diff = kor_go_duration_seconds(go_sub_mono(now, st->node_ts[n]));
+  for (uint32_t z = 0; z < Z; ++z) {
+    const uint64_t i = static_cast<uint64_t>(n) * Z + z;
+    const uint64_t abs_energy = b->zone_energy[i];
+    if (first_read) {
+      const uint64_t active = kor_go_f64_to_u64(u2f(abs_energy) * ratio);  // node.go:118
+      st->node_energy_total[i] = abs_energy;
+      st->node_active_total[i] = active;
+      st->node_idle_total[i] = abs_energy - active;  // node.go:119
+      st->node_active_energy[i] = active;
+      st->node_power[i] = 0;  // node.go:126: no power on the first read
+      st->node_active_power[i] = 0;
+      st->node_idle_power[i] = 0;
+    } else {
+      const uint64_t delta =
+          kor_calculate_energy_delta(abs_energy, st->node_energy_total[i], b->zone_max[i]);
+      const uint64_t active = kor_go_f64_to_u64(u2f(delta) * ratio);  // node.go:58
+      const uint64_t idle = delta - active;                           // node.go:59
+      st->node_active_total[i] += active;                             // node.go:61
+      st->node_idle_total[i] += idle;                                 // node.go:62
+      const double p = u2f(delta) / time_diff;                        // node.go:64
+      st->node_power[i] = p;
+      st->node_active_power[i] = p * ratio;  // node.go:66
+      st->node_idle_power[i] = st->node_power[i] - st->node_active_power[i];
+      st->node_energy_total[i] = abs_energy;
+      st->node_active_energy[i] = active;
+    }
+    nz.active_energy[z] = st->node_active_energy[i];
+    nz.power[z] = st->node_power[i];
+    nz.active_power[z] = st->node_active_power[i];
+  }
+  st->node_ts[n] = now;                             // node.go:16 / node.go:102
+  st->node_usage_ratio[n] = first_read ? 0 : ratio;  // node.go:26 (firstNodeRead leaves 0)
+  st->node_has_prev[n] = 1;
+  st->node_status[n] = first_read ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+
+  // ---- resources.Refresh(): informer.go:349-410
+  const Ranges r = node_ranges(b, n);
+  const double *d = b->proc_cpu_delta;
+  // refreshContainers + updateContainerCache (informer.go:223-249, 469-489)
+  for (uint32_t c = r.c0; c < r.c1; ++c) {
+    const uint32_t w = b->ctr_slot[c];
+    const uint32_t s = w & KACC_SLOT_MASK;
+    double delta = 0;  // resetCPUTime on the container's first process
+    double total = (w & KACC_SLOT_NEW) ? 0.0 : st->ctr_cpu_total[s];  // Clone() drops totals
+    for (uint32_t i = ctr_begin(b, r, c); i < b->ctr_proc_end[c]; ++i) {
+      delta += d[i];
+      total += d[i];
+    }
+    st->ctr_cpu_delta[s] = delta;
+    st->ctr_cpu_total[s] = total;
+  }
+  // refreshVMs + updateVMCache (informer.go:251-273, 433-449): last writer wins
+  for (uint32_t v = r.v0; v < r.v1; ++v) {
+    const uint32_t s = b->vm_slot[v] & KACC_SLOT_MASK;
+    double delta = 0;
+    for (uint32_t i = vm_begin(b, r, v); i < b->vm_proc_end[v]; ++i) delta = d[i];
+    st->vm_cpu_delta[s] = delta;
+  }
+  // refreshPods + updatePodCache (informer.go:275-326, 491-510)
+  for (uint32_t q = r.q0; q < r.q1; ++q) {
+    const uint32_t w = b->pod_slot[q];
+    const uint32_t s = w & KACC_SLOT_MASK;
+    double delta = 0;
+    double total = (w & KACC_SLOT_NEW) ? 0.0 : st->pod_cpu_total[s];
+    for (uint32_t c = pod_begin(b, r, q); c < b->pod_ctr_end[q]; ++c) {
+      const uint32_t cs = b->ctr_slot[c] & KACC_SLOT_MASK;
+      delta += st->ctr_cpu_delta[cs];
+      total += st->ctr_cpu_total[cs];  // quirk: adds the container's running total
+    }
+    st->pod_cpu_delta[s] = delta;
+    st->pod_cpu_total[s] = total;
+  }
+  // refreshNode (informer.go:328-345)
+  const double node_delta = (b->flags & KACC_F_NODE_CPU_DELTA_GIVEN)
+                                ? b->node_cpu_delta[n]
+                                : node_cpu_delta_sum(d, r.p0, r.p1, sum_mode);
+  st->node_cpu_delta[n] = node_delta;
+
+  // ---- workloads: process.go:79-161, container.go:71-153, vm.go:46-121, pod.go:46-131
+  for (uint32_t i = r.p0; i < r.p1; ++i) {
+    const uint32_t w = b->proc_slot[i];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    attribute(Z, d[i], node_delta, nz, false, first_read, (w & KACC_SLOT_NEW) != 0,
+              st->proc_energy + s * Z, st->proc_power + s * Z);
+  }
+  for (uint32_t c = r.c0; c < r.c1; ++c) {
+    const uint32_t w = b->ctr_slot[c];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    attribute(Z, st->ctr_cpu_delta[s], node_delta, nz, false, first_read,
+              (w & KACC_SLOT_NEW) != 0, st->ctr_energy + s * Z, st->ctr_power + s * Z);
+  }
+  for (uint32_t v = r.v0; v < r.v1; ++v) {
+    const uint32_t w = b->vm_slot[v];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    attribute(Z, st->vm_cpu_delta[s], node_delta, nz, false, first_read,
+              (w & KACC_SLOT_NEW) != 0, st->vm_energy + s * Z, st->vm_power + s * Z);
+  }
+  // pod.go:70-73 returns early when no pod is running: nothing to write.
+  for (uint32_t q = r.q0; q < r.q1; ++q) {
+    const uint32_t w = b->pod_slot[q];
+    const uint64_t s = w & KACC_SLOT_MASK;
+    attribute(Z, st->pod_cpu_delta[s], node_delta, nz, true, first_read,
+              (w & KACC_SLOT_NEW) != 0, st->pod_energy + s * Z, st->pod_power + s * Z);
+  }
+}
+
 extern "C" {
 
 // cmd/compile ssagen float64ToUint64 (amd64): x < 2^63 ? CVTTSD2SQ(x)
@@ -150,129 +276,25 @@ int kor_interval(kor_state *st, const kacc_interval *b, int sum_mode) {
   if (!st || !b) return KACC_EINVAL;
   const uint32_t Z = st->zones;
   if (Z == 0 || Z > KACC_MAX_ZONES || b->n_nodes > st->nodes) return KACC_EINVAL;
+  for (uint32_t n = 0; n < b->n_nodes; ++n) node_interval(st, b, n, sum_mode);
+  return KACC_OK;
+}
 
-  for (uint32_t n = 0; n < b->n_nodes; ++n) {
-    const uint32_t status = b->node_status ? b->node_status[n] : 0u;
-    if (status & KACC_NODE_READ_ERROR) {
-      // node.go:39-44 joins the read error; calculatePower returns it
-      // (monitor.go:401-403) and refreshSnapshot keeps the old snapshot
-      // (monitor.go:332-334) without calling Refresh.
-      st->node_status[n] = KACC_NODE_SKIPPED;
-      continue;
-    }
-    const bool first_read = st->node_has_prev[n] == 0;  // monitor.go:326-330
-    const double ratio = b->node_usage_ratio[n];
-    const int64_t now = b->node_ts_ns[n];
-    NodeZ nz;
-
-    // ---- node zones: node.go:10-84 (calculateNodePower) / node.go:101-131 (firstNodeRead)
-    double time_diff = 0;
-    if (!first_read) time_diff = kor_go_duration_seconds(go_sub_mono(now, st->node_ts[n]));
-    for (uint32_t z = 0; z < Z; ++z) {
-      const uint64_t i = static_cast<uint64_t>(n) * Z + z;
-      const uint64_t abs_energy = b->zone_energy[i];
-      if (first_read) {
-        const uint64_t active = kor_go_f64_to_u64(u2f(abs_energy) * ratio);  // node.go:118
-        st->node_energy_total[i] = abs_energy;
-        st->node_active_total[i] = active;
-        st->node_idle_total[i] = abs_energy - active;  // node.go:119
-        st->node_active_energy[i] = active;
-        st->node_power[i] = 0;  // node.go:126: no power on the first read
-        st->node_active_power[i] = 0;
-        st->node_idle_power[i] = 0;
-      } else {
-        const uint64_t delta =
-            kor_calculate_energy_delta(abs_energy, st->node_energy_total[i], b->zone_max[i]);
-        const uint64_t active = kor_go_f64_to_u64(u2f(delta) * ratio);  // node.go:58
-        const uint64_t idle = delta - active;                           // node.go:59
-        st->node_active_total[i] += active;                             // node.go:61
-        st->node_idle_total[i] += idle;                                 // node.go:62
-        const double p = u2f(delta) / time_diff;                        // node.go:64
-        st->node_power[i] = p;
-        st->node_active_power[i] = p * ratio;  // node.go:66
-        st->node_idle_power[i] = st->node_power[i] - st->node_active_power[i];
-        st->node_energy_total[i] = abs_energy;
-        st->node_active_energy[i] = active;
-      }
-      nz.active_energy[z] = st->node_active_energy[i];
-      nz.power[z] = st->node_power[i];
-      nz.active_power[z] = st->node_active_power[i];
-    }
-    st->node_ts[n] = now;                             // node.go:16 / node.go:102
-    st->node_usage_ratio[n] = first_read ? 0 : ratio;  // node.go:26 (firstNodeRead leaves 0)
-    st->node_has_prev[n] = 1;
-    st->node_status[n] = first_read ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
-
-    // ---- resources.Refresh(): informer.go:349-410
-    const Ranges r = node_ranges(b, n);
-    const double *d = b->proc_cpu_delta;
-    // refreshContainers + updateContainerCache (informer.go:223-249, 469-489)
-    for (uint32_t c = r.c0; c < r.c1; ++c) {
-      const uint32_t w = b->ctr_slot[c];
-      const uint32_t s = w & KACC_SLOT_MASK;
-      double delta = 0;  // resetCPUTime on the container's first process
-      double total = (w & KACC_SLOT_NEW) ? 0.0 : st->ctr_cpu_total[s];  // Clone() drops totals
-      for (uint32_t i = ctr_begin(b, r, c); i < b->ctr_proc_end[c]; ++i) {
-        delta += d[i];
-        total += d[i];
-      }
-      st->ctr_cpu_delta[s] = delta;
-      st->ctr_cpu_total[s] = total;
-    }
-    // refreshVMs + updateVMCache (informer.go:251-273, 433-449): last writer wins
-    for (uint32_t v = r.v0; v < r.v1; ++v) {
-      const uint32_t s = b->vm_slot[v] & KACC_SLOT_MASK;
-      double delta = 0;
-      for (uint32_t i = vm_begin(b, r, v); i < b->vm_proc_end[v]; ++i) delta = d[i];
-      st->vm_cpu_delta[s] = delta;
-    }
-    // refreshPods + updatePodCache (informer.go:275-326, 491-510)
-    for (uint32_t q = r.q0; q < r.q1; ++q) {
-      const uint32_t w = b->pod_slot[q];
-      const uint32_t s = w & KACC_SLOT_MASK;
-      double delta = 0;
-      double total = (w & KACC_SLOT_NEW) ? 0.0 : st->pod_cpu_total[s];
-      for (uint32_t c = pod_begin(b, r, q); c < b->pod_ctr_end[q]; ++c) {
-        const uint32_t cs = b->ctr_slot[c] & KACC_SLOT_MASK;
-        delta += st->ctr_cpu_delta[cs];
-        total += st->ctr_cpu_total[cs];  // quirk: adds the container's running total
-      }
-      st->pod_cpu_delta[s] = delta;
-      st->pod_cpu_total[s] = total;
-    }
-    // refreshNode (informer.go:328-345)
-    const double node_delta = (b->flags & KACC_F_NODE_CPU_DELTA_GIVEN)
-                                  ? b->node_cpu_delta[n]
-                                  : node_cpu_delta_sum(d, r.p0, r.p1, sum_mode);
-    st->node_cpu_delta[n] = node_delta;
-
-    // ---- workloads: process.go:79-161, container.go:71-153, vm.go:46-121, pod.go:46-131
-    for (uint32_t i = r.p0; i < r.p1; ++i) {
-      const uint32_t w = b->proc_slot[i];
-      const uint64_t s = w & KACC_SLOT_MASK;
-      attribute(Z, d[i], node_delta, nz, false, first_read, (w & KACC_SLOT_NEW) != 0,
-                st->proc_energy + s * Z, st->proc_power + s * Z);
-    }
-    for (uint32_t c = r.c0; c < r.c1; ++c) {
-      const uint32_t w = b->ctr_slot[c];
-      const uint64_t s = w & KACC_SLOT_MASK;
-      attribute(Z, st->ctr_cpu_delta[s], node_delta, nz, false, first_read,
-                (w & KACC_SLOT_NEW) != 0, st->ctr_energy + s * Z, st->ctr_power + s * Z);
-    }
-    for (uint32_t v = r.v0; v < r.v1; ++v) {
-      const uint32_t w = b->vm_slot[v];
-      const uint64_t s = w & KACC_SLOT_MASK;
-      attribute(Z, st->vm_cpu_delta[s], node_delta, nz, false, first_read,
-                (w & KACC_SLOT_NEW) != 0, st->vm_energy + s * Z, st->vm_power + s * Z);
-    }
-    // pod.go:70-73 returns early when no pod is running: nothing to write.
-    for (uint32_t q = r.q0; q < r.q1; ++q) {
-      const uint32_t w = b->pod_slot[q];
-      const uint64_t s = w & KACC_SLOT_MASK;
-      attribute(Z, st->pod_cpu_delta[s], node_delta, nz, true, first_read,
-                (w & KACC_SLOT_NEW) != 0, st->pod_energy + s * Z, st->pod_power + s * Z);
-    }
+// The same on `threads` host threads over contiguous node ranges (CPU
+// baseline only; results identical to kor_interval).
+int kor_interval_mt(kor_state *st, const kacc_interval *b, int sum_mode, int threads) {
+  if (!st || !b) return KACC_EINVAL;
+  const uint32_t Z = st->zones;
+  if (Z == 0 || Z > KACC_MAX_ZONES || b->n_nodes > st->nodes) return KACC_EINVAL;
+  const uint32_t N = b->n_nodes, T = threads < 1 ? 1u : static_cast<uint32_t>(threads);
+  std::vector<std::thread> pool;
+  for (uint32_t t = 0; t < T; ++t) {
+    const uint32_t n0 = static_cast<uint32_t>(uint64_t(N) * t / T), n1 = static_cast<uint32_t>(uint64_t(N) * (t + 1) / T);
+    pool.emplace_back([=] {
+      for (uint32_t n = n0; n < n1; ++n) node_interval(st, b, n, sum_mode);
+    });
   }
+  for (auto &th : pool) th.join();
   return KACC_OK;
 }
 

@@ -60,6 +60,8 @@ uint64_t kor_calculate_energy_delta(uint64_t current, uint64_t previous, uint64_
 
 /* One interval for every node of a host batch; returns 0 or KACC_E*. */
 int kor_interval(kor_state *st, const kacc_interval *b, int sum_mode);
+/* the same over `threads` host threads (node ranges): the CPU baseline */
+int kor_interval_mt(kor_state *st, const kacc_interval *b, int sum_mode, int threads);
 
 int kor_namespace_totals(const kor_state *st, uint32_t n_ns, const uint32_t *ns_pod_off,
                          const uint32_t *ns_pod_slot, uint64_t *out_energy, double *out_power);

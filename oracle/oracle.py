@@ -51,6 +51,7 @@ def load():
     lib.kor_calculate_energy_delta.argtypes = [c_uint64, c_uint64, c_uint64]
     lib.kor_calculate_energy_delta.restype = c_uint64
     lib.kor_interval.argtypes = [POINTER(KorState), POINTER(KaccInterval), c_int]
+    lib.kor_interval_mt.argtypes = [POINTER(KorState), POINTER(KaccInterval), c_int, c_int]
     lib.kor_namespace_totals.argtypes = [POINTER(KorState), c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kor_aggregated_max.argtypes = [c_uint32, c_void_p]
     lib.kor_aggregated_max.restype = c_uint64
@@ -131,6 +132,13 @@ class Oracle:
         rc = self.lib.kor_interval(ctypes.byref(self.state.c), ctypes.byref(it), self.sum_mode)
         if rc != 0:
             raise RuntimeError(f"kor_interval failed: {rc}")
+
+    def interval_mt(self, arrays: dict, sizes: dict, threads: int, flags: int = 0) -> None:
+        """kor_interval over `threads` host threads (the multi-core CPU baseline)."""
+        it = make_interval(arrays, sizes, flags)
+        rc = self.lib.kor_interval_mt(ctypes.byref(self.state.c), ctypes.byref(it), self.sum_mode, threads)
+        if rc != 0:
+            raise RuntimeError(f"kor_interval_mt failed: {rc}")
 
     def namespace_totals(self, ns_off: np.ndarray, ns_slot: np.ndarray):
         n_ns = len(ns_off) - 1

@@ -55,3 +55,19 @@ def test_cpp_oracle_matches_python_restatement(name, kw, max_energy, oracle_lib)
         got = ref.tables(layout.n_nodes, caps)
         for tname, _ in accel.TABLES:
             np.testing.assert_array_equal(ora.state[tname], got[tname], err_msg=f"interval {k} {tname}")
+
+
+def test_threaded_oracle_matches_serial(oracle_lib):
+    """kor_interval_mt (the multi-core CPU baseline) == kor_interval, every table."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(37, [300, 2000, 1, 0, 700, 64, 5000] * 5 + [9, 9], 4, seed=8, shuffle_slots=True)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=8, churn=0.05, read_error_frac=0.1)
+    a_ser, a_mt = Oracle(layout.zones, **caps), Oracle(layout.zones, **caps)
+    for _ in range(3):
+        a = sim.next_interval()
+        a_ser.interval(a, layout.sizes())
+        a_mt.interval_mt(a, layout.sizes(), threads=5)
+    for tname, _ in accel.TABLES:
+        np.testing.assert_array_equal(a_mt.state[tname], a_ser.state[tname], err_msg=tname)
