@@ -87,8 +87,18 @@ extern "C" {
                                        device still clamps every index and raises
                                        KACC_ERANGE; only duplicate slots go
                                        unchecked (they would race, not fault). */
+#define KACC_F_SMALL_NODES 0x8u /* caller guarantees every node has at most
+                                    KACC_SMALL_MAX_PROCS process rows and at most
+                                    KACC_SMALL_MAX_AGGREGATES containers+VMs+pods:
+                                    one wavefront per node (4 nodes per
+                                    workgroup), bit-identical results; implies
+                                    KACC_F_FAST_NODES.  A node that does not fit
+                                    is not computed and raises KACC_ERANGE (bit
+                                    32).  kacc_batch_submit sets it by itself. */
 #define KACC_FAST_MAX_PROCS 2048u
 #define KACC_FAST_MAX_AGGREGATES 512u
+#define KACC_SMALL_MAX_PROCS 512u
+#define KACC_SMALL_MAX_AGGREGATES 128u
 
 typedef struct kacc_ctx kacc_ctx;
 

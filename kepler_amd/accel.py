@@ -42,6 +42,9 @@ KACC_F_FAST_NODES = 0x2
 KACC_F_TRUSTED_LAYOUT = 0x4
 KACC_FAST_MAX_PROCS = 2048
 KACC_FAST_MAX_AGGREGATES = 512
+KACC_F_SMALL_NODES = 0x8
+KACC_SMALL_MAX_PROCS = 512
+KACC_SMALL_MAX_AGGREGATES = 128
 
 # kacc_table enum, in header order: (name, numpy dtype)
 TABLES = [

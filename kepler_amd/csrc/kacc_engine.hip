@@ -760,6 +760,360 @@ void interval_kernel(const kacc_interval b, const DevState st) {
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
 }
 
+// ======================= small nodes: one wavefront per node ======================
+// Real nodes run a few hundred processes (the reference's own single-node case
+// is 500 procs -> 50 containers -> 20 pods).  A 512-lane workgroup per such
+// node leaves most lanes idle and caps residency at 3 nodes per CU (measured:
+// 250 procs/node 1.7 TB/s, 500 procs/node 2.9 TB/s against 5.5 TB/s at 2000).
+// Under KACC_F_SMALL_NODES every node has <= kSmallRows rows and
+// <= kSmallAgg aggregates, and one WAVEFRONT owns a node: the same phases
+// A-E as interval_kernel with wave-level LDS ordering instead of workgroup
+// barriers, the canonical 256-lane CPU-total tree evaluated by 64 lanes (4
+// partial sums per lane, the same additions in the same order), two
+// aggregates per lane, and the rows moved as 64-row groups in two batches of
+// four (the first batch's previous totals are in flight with the Δ loads).
+// Results are bit-identical to interval_kernel's.
+constexpr int kSmallRows = 512;
+constexpr int kSmallAgg = 128;
+constexpr int kSmallWaves = 4;                   // nodes per workgroup
+constexpr int kSmallGroups = kSmallRows / 64;    // 64-row groups per node
+constexpr int kSmallBatch = 4;                   // groups whose prev totals are in flight together
+static_assert(kSmallRows == KACC_SMALL_MAX_PROCS && kSmallAgg == KACC_SMALL_MAX_AGGREGATES,
+              "KACC_SMALL_* must match the small-node kernel's capacity");
+static_assert(kSmallRows <= 2 * kTree && kSmallGroups == 2 * kSmallBatch && kSmallAgg == 128,
+              "small-node tree / batch / aggregate loops assume these sizes");
+
+// LDS writes of one lane made visible to the other lanes of the same wave.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int Z>
+__global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_interval b, const DevState st) {
+  constexpr bool kNT = true, kNtLd = true;  // as interval_kernel's production variant
+  __shared__ double s_d_all[kSmallWaves][kSmallRows];
+  __shared__ uint32_t s_w_all[kSmallWaves][kSmallRows];
+  __shared__ double s_cd_all[kSmallWaves][kSmallAgg];
+  __shared__ double s_ct_all[kSmallWaves][kSmallAgg];
+  __shared__ uint16_t s_inv_all[kSmallWaves][kSmallRows];
+  __shared__ NodeShared sh_all[kSmallWaves];
+
+  const uint32_t wv = uniform_u32(threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  double *s_d = s_d_all[wv];
+  uint32_t *s_w = s_w_all[wv];
+  double *s_cd = s_cd_all[wv];
+  double *s_ct = s_ct_all[wv];
+  uint16_t *s_inv = s_inv_all[wv];
+  NodeShared &sh = sh_all[wv];
+
+  if (blockIdx.x == 0 && threadIdx.x == 0) st.defer_ctr[0] = 0u;  // as interval_kernel
+  const uint32_t idx = blockIdx.x * kSmallWaves + wv;
+  if (idx >= b.n_nodes) return;  // wave-uniform: no workgroup barrier below
+  const uint32_t n = b.node_order ? uniform_u32(b.node_order[idx]) : idx;
+  if (n >= b.n_nodes) {
+    if (lane == 0) raise_err(st.err, kErrNode);
+    return;
+  }
+  const uint32_t status = b.node_status ? b.node_status[n] : 0u;
+  if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44
+    if (lane == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+    return;
+  }
+  const NodeRanges rg = node_ranges(b, st, n, static_cast<int>(lane));
+  const uint32_t p0 = rg.p0, p1 = rg.p1, c0 = rg.c0, c1 = rg.c1, q0 = rg.q0, q1 = rg.q1;
+  const uint32_t rows = p1 - p0, nc = c1 - c0, nv = rg.v1 - rg.v0, nq = q1 - q0;
+  if (rows > static_cast<uint32_t>(kSmallRows) || nc + nv + nq > static_cast<uint32_t>(kSmallAgg)) {
+    if (lane == 0) raise_err(st.err, kErrBigNode);  // the caller's promise was wrong
+    return;
+  }
+
+  // ---- A: node zones ---------------------------------------------------------------
+  if (lane < static_cast<uint32_t>(Z)) node_zone<Z>(b, st, n, static_cast<int>(lane), sh);
+
+  // ---- loads: Δ and slot words of every row, then the first batch's prev totals ----
+  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
+  const uint32_t *__restrict__ pslot = b.proc_slot + p0;
+  double d[kSmallGroups];
+  uint32_t w[kSmallGroups];
+#pragma unroll
+  for (int k = 0; k < kSmallGroups; ++k) {
+    const uint32_t r = lane + 64u * k;
+    const bool in = r < rows;
+    d[k] = in ? __builtin_nontemporal_load(dcpu + r) : 0.0;
+    w[k] = in ? __builtin_nontemporal_load(pslot + r) : 0xffffffffu;
+  }
+  constexpr bool kSweepable = kTransposed<Z>;
+  uint32_t smin = 0, span = 0;
+  bool swept = false;
+  if constexpr (kSweepable) {
+    if (b.node_proc_span) {
+      const uint32_t lo = uniform_u32(b.node_proc_span[2 * n]);
+      const uint32_t hi = uniform_u32(b.node_proc_span[2 * n + 1]);
+      swept = rows > 0 && hi >= lo && hi - lo < static_cast<uint32_t>(kSmallRows) && hi < st.proc_slots;
+      smin = lo;
+      span = hi - lo + 1;
+      if (swept) {
+#pragma unroll
+        for (int k = 0; k < kSmallGroups; ++k) s_inv[lane + 64u * k] = 0xffffu;
+      }
+    }
+  }
+  // batch kb (groups 4kb .. 4kb+3): previous totals into prev; bit g of contig:
+  // group 4kb+g is a full group of consecutive slots (wave-uniform)
+  uint64_t prev[kSmallBatch][Z];
+  uint32_t contig = 0;
+  auto load_batch = [&](int kb, bool from_regs) {
+    contig = 0;
+#pragma unroll
+    for (int g = 0; g < kSmallBatch; ++g) {
+      const int k = kb * kSmallBatch + g;
+      const uint32_t pos0 = 64u * k;
+      if constexpr (kSweepable) {
+        if (swept) {
+          const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
+          load_group_masked<Z, true, kNtLd>(st.proc_energy, static_cast<uint64_t>(smin) + pos0, len, smin,
+                                            prev[g]);
+          continue;
+        }
+      }
+      const uint32_t r = pos0 + lane;
+      const uint32_t wk = from_regs ? w[k] : (r < rows ? s_w[r] : 0xffffffffu);
+      const uint64_t sl = wk & KACC_SLOT_MASK;
+      if constexpr (kTransposed<Z>) {
+        const uint64_t g0 = uniform_u32(static_cast<uint32_t>(sl));
+        if (__all(r < rows && sl == g0 + lane && g0 + 64 <= st.proc_slots)) {
+          contig |= 1u << g;
+          load_group_masked<Z, false, kNtLd>(st.proc_energy, g0, 64u, g0, prev[g]);
+          continue;
+        }
+      }
+      if (r < rows && sl < st.proc_slots) {
+        load_row<Z>(st.proc_energy, sl, prev[g]);
+      } else {
+#pragma unroll
+        for (int z = 0; z < Z; ++z) prev[g][z] = 0;
+      }
+    }
+  };
+  load_batch(0, true);
+
+  // aggregates: lane handles aggregate i = lane + 64h (containers, VMs, pods)
+  auto role_of = [&](uint32_t i) -> uint32_t {
+    return i < nc ? 1u : i < nc + nv ? 2u : i < nc + nv + nq ? 3u : 0u;
+  };
+  auto index_of = [&](uint32_t i) -> uint32_t { return i < nc ? i : i < nc + nv ? i - nc : i - nc - nv; };
+  auto cap_of = [&](uint32_t role) -> uint64_t {
+    return role == 1 ? st.ctr_slots : role == 2 ? st.vm_slots : role == 3 ? st.pod_slots : 0;
+  };
+  auto energy_of = [&](uint32_t role) { return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy; };
+  auto power_of = [&](uint32_t role) { return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power; };
+  auto cpu_total_of = [&](uint32_t role) { return role == 1 ? st.ctr_cpu_total : st.pod_cpu_total; };
+  auto cpu_delta_of = [&](uint32_t role) {
+    return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
+  };
+  uint32_t a_beg[2], a_end[2], a_w[2];
+  uint64_t a_prev[2][Z];
+  double a_total[2], a_delta[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = lane + 64u * h, role = role_of(i), j = index_of(i);
+    a_beg[h] = a_end[h] = 0;
+    a_w[h] = 0xffffffffu;
+    if (role == 1) {
+      a_beg[h] = j == 0 ? p0 : b.ctr_proc_end[c0 + j - 1];
+      a_end[h] = b.ctr_proc_end[c0 + j];
+      a_w[h] = b.ctr_slot[c0 + j];
+    } else if (role == 2) {
+      a_beg[h] = j == 0 ? (nc ? b.ctr_proc_end[c1 - 1] : p0) : b.vm_proc_end[rg.v0 + j - 1];
+      a_end[h] = b.vm_proc_end[rg.v0 + j];
+      a_w[h] = b.vm_slot[rg.v0 + j];
+    } else if (role == 3) {
+      a_beg[h] = j == 0 ? c0 : b.pod_ctr_end[q0 + j - 1];
+      a_end[h] = b.pod_ctr_end[q0 + j];
+      a_w[h] = b.pod_slot[q0 + j];
+    }
+    const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
+    const bool a_ok = role != 0 && a_s < cap_of(role);
+    a_total[h] = 0.0;
+    a_delta[h] = 0.0;
+    if (a_ok) {
+      load_row<Z>(energy_of(role), a_s, a_prev[h]);
+      if (role != 2 && !(a_w[h] & KACC_SLOT_NEW)) a_total[h] = cpu_total_of(role)[a_s];
+    } else {
+#pragma unroll
+      for (int z = 0; z < Z; ++z) a_prev[h][z] = 0;
+    }
+    if (role != 0 && !a_ok) raise_err(st.err, kErrSlot);
+  }
+
+  // ---- B: stage Δ / slot words; ProcessTotalCPUTimeDelta (informer.go:330-333) ------
+#pragma unroll
+  for (int k = 0; k < kSmallGroups; ++k) {
+    const uint32_t r = lane + 64u * k;
+    if (r < rows) {
+      s_d[r] = d[k];
+      s_w[r] = w[k];
+    }
+  }
+  wave_sync();  // s_inv reset and the staged rows visible to every lane
+  if (swept) {
+#pragma unroll
+    for (int k = 0; k < kSmallGroups; ++k) {
+      const uint32_t r = lane + 64u * k;
+      if (r >= rows) continue;
+      const uint32_t sl = s_w[r] & KACC_SLOT_MASK;
+      if (sl - smin < span && sl < st.proc_slots)
+        s_inv[sl - smin] = static_cast<uint16_t>(r);
+      else
+        raise_err(st.err, kErrSlot);
+    }
+  }
+  if (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
+    if (lane == 0) sh.node_delta = b.node_cpu_delta[n];
+  } else {
+    // the 256 tree leaves of interval_kernel: leaf l sums rows l, l+256 in order;
+    // lane t holds leaves t, t+64, t+128, t+192; then red[l] + red[l+128],
+    // red[t] + red[t+64] and the shuffle tree, exactly as there
+    double leaf[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double s = 0.0;
+      for (uint32_t r = lane + 64u * q; r < rows; r += kTree) s = s + s_d[r];
+      leaf[q] = s;
+    }
+    const double t0 = leaf[0] + leaf[2];
+    const double t1 = leaf[1] + leaf[3];
+    double x = t0 + t1;
+#pragma unroll
+    for (int k = 32; k >= 1; k >>= 1) x = x + __shfl_down(x, k, 64);
+    if (lane == 0) sh.node_delta = x;
+  }
+
+  // ---- C: containers and VMs ---------------------------------------------------------
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = lane + 64u * h, role = role_of(i), j = index_of(i);
+    if (role != 1 && role != 2) continue;
+    const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
+    const bool a_ok = a_s < cap_of(role);
+    uint32_t beg = a_beg[h], end = a_end[h];
+    if (beg < p0 || end < beg || end > p1) {
+      raise_err(st.err, kErrOffsets);
+      beg = max(min(beg, p1), p0);
+      end = max(min(end, p1), beg);
+    }
+    double ad = 0.0;
+    if (role == 1) {  // informer.go:229-233, 481-486
+      double at = a_total[h];
+      for (uint32_t r = beg - p0; r < end - p0; ++r) {
+        const double dr = s_d[r];
+        ad = ad + dr;
+        at = at + dr;
+      }
+      a_total[h] = at;
+      s_cd[j] = a_ok ? ad : 0.0;
+      s_ct[j] = a_ok ? at : 0.0;
+    } else {  // informer.go:445: the last process in listing order wins
+      ad = end > beg ? s_d[end - 1 - p0] : 0.0;
+    }
+    a_delta[h] = ad;
+    if (a_ok) {
+      cpu_delta_of(role)[a_s] = ad;
+      if (role == 1) cpu_total_of(role)[a_s] = a_total[h];
+    }
+  }
+  wave_sync();
+
+  // ---- D: pods (informer.go:305-309, 502-507) ---------------------------------------
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t i = lane + 64u * h;
+    if (role_of(i) != 3) continue;
+    const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
+    uint32_t beg = a_beg[h], end = a_end[h];
+    if (beg < c0 || end < beg || end > c1) {
+      raise_err(st.err, kErrOffsets);
+      beg = max(min(beg, c1), c0);
+      end = max(min(end, c1), beg);
+    }
+    double ad = 0.0, at = a_total[h];
+    for (uint32_t c = beg - c0; c < end - c0; ++c) {
+      ad = ad + s_cd[c];
+      at = at + s_ct[c];  // quirk: the container's running total
+    }
+    a_delta[h] = ad;
+    a_total[h] = at;
+    if (a_s < st.pod_slots) {
+      st.pod_cpu_delta[a_s] = ad;
+      st.pod_cpu_total[a_s] = at;
+    }
+  }
+
+  // ---- E: attribution ------------------------------------------------------------------
+  const Attr<Z> a = make_attr<Z>(sh);
+  if (lane == 0) {
+    st.node_ts[n] = b.node_ts_ns[n];
+    st.node_has_prev[n] = 1u;
+    st.node_usage_ratio[n] = a.first ? 0.0 : b.node_usage_ratio[n];
+    st.node_cpu_delta[n] = a.nd;
+    st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+    const uint32_t role = role_of(lane + 64u * h);
+    const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
+    if (role == 0 || a_s >= cap_of(role)) continue;
+    uint64_t E[Z];
+    double P[Z];
+    attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h], (a_w[h] & KACC_SLOT_NEW) != 0,
+                     a_prev[h], E, P);
+    store_row<Z, kNT, uint64_t>(energy_of(role), a_s, E);
+    store_row<Z, kNT, double>(power_of(role), a_s, P);
+  }
+  auto attr_batch = [&](int kb) {  // process.go:118-148
+#pragma unroll
+    for (int g = 0; g < kSmallBatch; ++g) {
+      const uint32_t pos0 = 64u * (kb * kSmallBatch + g);
+      if constexpr (kSweepable) {
+        if (swept) {
+          const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
+          attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0, static_cast<uint64_t>(smin) + pos0,
+                                               len, prev[g], st.proc_energy, st.proc_power);
+          continue;
+        }
+        if (contig & (1u << g)) {
+          attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
+                                                uniform_u32(s_w[pos0] & KACC_SLOT_MASK), 64u, prev[g],
+                                                st.proc_energy, st.proc_power);
+          continue;
+        }
+      }
+      const uint32_t r = pos0 + lane;
+      if (r >= rows) continue;
+      const uint32_t wk = s_w[r];
+      const uint64_t sl = wk & KACC_SLOT_MASK;
+      if (sl >= st.proc_slots) {
+        raise_err(st.err, kErrSlot);
+        continue;
+      }
+      uint64_t E[Z];
+      double P[Z];
+      attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[g], E, P);
+      store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
+      store_row<Z, kNT, double>(st.proc_power, sl, P);
+    }
+  };
+  attr_batch(0);
+  const uint32_t extent = swept ? span : rows;  // wave-uniform
+  if (extent > 64u * kSmallBatch) {
+    load_batch(1, false);
+    attr_batch(1);
+  }
+}
+
 // ======================= big nodes: chunked row passes ==========================
 // A node that does not fit one fast workgroup (> kRowsLds rows or > kTpb
 // aggregates, e.g. BASELINE config 5's 10-50k-process nodes) is cut into
@@ -1477,11 +1831,18 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
 // their node phase there and are cut into chunk items), the chunk kernel and
 // the deferred-pod kernel (both exit at once when no node was oversized; not
 // launched at all under KACC_F_FAST_NODES).
+template <int Z>
+void launch_small(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
+  const uint32_t grid = (b.n_nodes + kacc::kSmallWaves - 1) / kacc::kSmallWaves;
+  hipLaunchKernelGGL((kacc::small_kernel<Z>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
+}
+
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
+  if (V == 0 && (b.flags & KACC_F_SMALL_NODES)) return launch_small<Z>(b, s, st);
   hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
                      s);
-  if (b.flags & KACC_F_FAST_NODES) return;
+  if (b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES)) return;
   const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
   hipLaunchKernelGGL((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
                      b, s);
@@ -1521,6 +1882,7 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 2048: launch_zv<4, 2048>(b, s, st); return true;
     case 16384: launch_zv<4, 16384>(b, s, st); return true;
     case 16392: launch_zv<4, 16392>(b, s, st); return true;
+    case 65536: launch_small<4>(b, s, st); return true;  // one wavefront per node
     default: return false;
   }
 }
@@ -1579,7 +1941,8 @@ int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
     return fail(ctx, KACC_EINVAL, "required row array is NULL");
   if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
     return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
-  if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES | KACC_F_TRUSTED_LAYOUT))
+  if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES | KACC_F_TRUSTED_LAYOUT |
+                   KACC_F_SMALL_NODES))
     return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
   return KACC_OK;
 }
@@ -1685,15 +2048,19 @@ int check_slots(kacc_ctx *ctx, const char *name, const uint32_t *w, uint32_t n, 
   return KACC_OK;
 }
 
-// Every node fits the fast path (host batch, offsets already validated).
-bool all_nodes_fast(const kacc_interval &b) {
+// KACC_F_SMALL_NODES when every node fits one wavefront, else KACC_F_FAST_NODES
+// when every node fits the fast workgroup, else 0 (host batch, offsets already
+// validated).
+uint32_t node_size_flags(const kacc_interval &b) {
+  bool small = true;
   for (uint32_t n = 0; n < b.n_nodes; ++n) {
     const uint32_t rows = b.proc_off[n + 1] - b.proc_off[n];
     const uint32_t agg = (b.ctr_off[n + 1] - b.ctr_off[n]) + (b.vm_off[n + 1] - b.vm_off[n]) +
                          (b.pod_off[n + 1] - b.pod_off[n]);
-    if (rows > KACC_FAST_MAX_PROCS || agg > KACC_FAST_MAX_AGGREGATES) return false;
+    if (rows > KACC_FAST_MAX_PROCS || agg > KACC_FAST_MAX_AGGREGATES) return 0u;
+    small = small && rows <= KACC_SMALL_MAX_PROCS && agg <= KACC_SMALL_MAX_AGGREGATES;
   }
-  return true;
+  return small ? (KACC_F_SMALL_NODES | KACC_F_FAST_NODES) : KACC_F_FAST_NODES;
 }
 
 }  // namespace
@@ -2000,8 +2367,7 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (rc != KACC_OK || bt->host.n_nodes == 0) return rc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   kacc_interval dv = bt->dev;
-  dv.flags = (bt->host.flags & ~KACC_F_TRUSTED_LAYOUT) |
-             (all_nodes_fast(bt->host) ? KACC_F_FAST_NODES : 0u);
+  dv.flags = (bt->host.flags & ~KACC_F_TRUSTED_LAYOUT) | node_size_flags(bt->host);
   // honour optional arrays the caller switched off
   if (!bt->host.node_status) dv.node_status = nullptr;
   if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;

@@ -33,8 +33,12 @@ def main():
     s = torch.cuda.Stream()
     torch.cuda.set_stream(s)
     frag = float(os.environ.get("FRAG", "0"))  # slot fragmentation (+ node_proc_span)
-    layout = fleet.config_layout(cfg, fragment_slots=frag, fragment_sorted=bool(os.environ.get("FRAG_SORTED")),
-                                 nodes=int(os.environ["NODES"]) if os.environ.get("NODES") else None)
+    if os.environ.get("PROCS"):  # config-3 shape (Z=4) with PROCS processes per node
+        layout = fleet.make_layout(int(os.environ.get("NODES", "10000")), int(os.environ["PROCS"]), 4,
+                                   fleet.SEED, fragment_slots=frag)
+    else:
+        layout = fleet.config_layout(cfg, fragment_slots=frag, fragment_sorted=bool(os.environ.get("FRAG_SORTED")),
+                                     nodes=int(os.environ["NODES"]) if os.environ.get("NODES") else None)
     sim = fleet.FleetSim(layout)
     acc = accel.Accel(layout.zones, **layout.capacities())
     stream = current_stream_handle()
