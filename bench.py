@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5],
-                    help="BASELINE config; 4 = a 100k-node fleet split over the ranks")
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5],
+                    help="BASELINE config; 4 = a 100k-node fleet split over the ranks; "
+                         "1 = a fleet of config-1 nodes (500 procs, Z=2; 40k per GPU)")
     ap.add_argument("--nodes", type=int, default=None, help="override nodes per GPU")
     ap.add_argument("--distinct", type=int, default=4, help="distinct process-input sets cycled")
     ap.add_argument("--intervals", type=int, default=1,
@@ -137,7 +138,7 @@ def main():
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
     t_setup = time.time()
-    nodes = args.nodes or {2: 1000, 3: 10000, 4: -(-100000 // world), 5: 1000}[args.config]
+    nodes = args.nodes or {1: 40000, 2: 1000, 3: 10000, 4: -(-100000 // world), 5: 1000}[args.config]
     layout = fleet.config_layout(args.config, seed=fleet.SEED + 7919 * rank, nodes=nodes)
     sim = fleet.FleetSim(layout, seed=fleet.SEED + 7919 * rank)
     Z = layout.zones
@@ -311,7 +312,9 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "bytes_per_launch": bytes_per_launch,
-            "kernel": (f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, "
+            "kernel": (f"kacc::small_kernel<{Z}> (one launch per step, one wavefront per node: every node "
+                       f"fits KACC_F_SMALL_NODES)" if layout.fast_flag() & accel.KACC_F_SMALL_NODES else
+                       f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, "
                        f"KACC_F_FAST_NODES)" if layout.fast_flag() else
                        f"kacc::interval_kernel<{Z},0> + chunk_kernel<{Z},0> + pod_kernel<{Z},0> (big nodes "
                        f"chunked; HIP events bracket all three launches of the step)"),

@@ -103,14 +103,18 @@ class FleetLayout:
         return out
 
     def fast_flag(self) -> int:
-        """KACC_F_FAST_NODES when every node fits the fast path, else 0."""
-        from .accel import KACC_F_FAST_NODES, KACC_FAST_MAX_AGGREGATES, KACC_FAST_MAX_PROCS
+        """KACC_F_FAST_NODES when every node fits the fast path (| KACC_F_SMALL_NODES
+        when every node fits one wavefront), else 0."""
+        from .accel import (KACC_F_FAST_NODES, KACC_F_SMALL_NODES, KACC_FAST_MAX_AGGREGATES,
+                            KACC_FAST_MAX_PROCS, KACC_SMALL_MAX_AGGREGATES, KACC_SMALL_MAX_PROCS)
 
         rows = np.diff(self.proc_off.astype(np.int64))
         agg = (np.diff(self.ctr_off.astype(np.int64)) + np.diff(self.vm_off.astype(np.int64))
                + np.diff(self.pod_off.astype(np.int64)))
-        fits = bool(np.all(rows <= KACC_FAST_MAX_PROCS) and np.all(agg <= KACC_FAST_MAX_AGGREGATES))
-        return KACC_F_FAST_NODES if fits else 0
+        if not (np.all(rows <= KACC_FAST_MAX_PROCS) and np.all(agg <= KACC_FAST_MAX_AGGREGATES)):
+            return 0
+        small = bool(np.all(rows <= KACC_SMALL_MAX_PROCS) and np.all(agg <= KACC_SMALL_MAX_AGGREGATES))
+        return KACC_F_FAST_NODES | (KACC_F_SMALL_NODES if small else 0)
 
     def static_arrays(self) -> Dict[str, np.ndarray]:
         return dict(proc_off=self.proc_off, ctr_off=self.ctr_off, vm_off=self.vm_off,
@@ -264,8 +268,10 @@ def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
     ``fragment_slots`` > 0 places each node's processes on a random subset of
     its own slot range (the slot join's steady state under churn)."""
     if config == 1:  # single node, 500 procs -> 50 containers -> 20 pods, package+dram
-        return make_layout(1, 500, 2, seed, ctr_frac=0.8, procs_per_ctr=8, ctrs_per_pod=2.5,
-                           pod_frac=1.0, n_namespaces=4)
+        # (``nodes``: a fleet of such nodes — the small-node kernel's workload)
+        return make_layout(nodes or 1, 500, 2, seed, ctr_frac=0.8, procs_per_ctr=8, ctrs_per_pod=2.5,
+                           pod_frac=1.0, n_namespaces=4 if not nodes else None,
+                           fragment_slots=fragment_slots)
     if config == 2:
         return make_layout(nodes or 1000, 1000, 2, seed, fragment_slots=fragment_slots)
     if config in (3, 4):
