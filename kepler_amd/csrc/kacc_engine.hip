@@ -791,10 +791,15 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 template <int Z>
-__global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_interval b, const DevState st) {
+__global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(Z <= 2 ? 6 : 1))) void small_kernel(
+    const kacc_interval b, const DevState st) {
   constexpr bool kNT = true, kNtLd = true;  // as interval_kernel's production variant
   __shared__ double s_d_all[kSmallWaves][kSmallRows];
-  __shared__ uint32_t s_w_all[kSmallWaves][kSmallRows];
+  // slot words are read across lanes only by the transposed (sweep / contiguous
+  // group) paths; otherwise each lane keeps its own in w[] and the LDS per node
+  // drops from 8.4 KB to 6.4 KB (Z = 2: 6 nodes' workgroups per CU, not 4)
+  constexpr bool kSweepable = kTransposed<Z>;
+  __shared__ uint32_t s_w_all[kSmallWaves][kSweepable ? kSmallRows : 1];
   __shared__ double s_cd_all[kSmallWaves][kSmallAgg];
   __shared__ double s_ct_all[kSmallWaves][kSmallAgg];
   __shared__ uint16_t s_inv_all[kSmallWaves][kSmallRows];
@@ -845,7 +850,6 @@ __global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_inte
     d[k] = in ? __builtin_nontemporal_load(dcpu + r) : 0.0;
     w[k] = in ? __builtin_nontemporal_load(pslot + r) : 0xffffffffu;
   }
-  constexpr bool kSweepable = kTransposed<Z>;
   uint32_t smin = 0, span = 0;
   bool swept = false;
   if constexpr (kSweepable) {
@@ -880,7 +884,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_inte
         }
       }
       const uint32_t r = pos0 + lane;
-      const uint32_t wk = from_regs ? w[k] : (r < rows ? s_w[r] : 0xffffffffu);
+      const uint32_t wk = (from_regs || !kSweepable) ? w[k] : (r < rows ? s_w[r] : 0xffffffffu);
       const uint64_t sl = wk & KACC_SLOT_MASK;
       if constexpr (kTransposed<Z>) {
         const uint64_t g0 = uniform_u32(static_cast<uint32_t>(sl));
@@ -955,11 +959,11 @@ __global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_inte
     const uint32_t r = lane + 64u * k;
     if (r < rows) {
       s_d[r] = d[k];
-      s_w[r] = w[k];
+      if constexpr (kSweepable) s_w[r] = w[k];
     }
   }
   wave_sync();  // s_inv reset and the staged rows visible to every lane
-  if (swept) {
+  if (kSweepable && swept) {
 #pragma unroll
     for (int k = 0; k < kSmallGroups; ++k) {
       const uint32_t r = lane + 64u * k;
@@ -1093,7 +1097,11 @@ __global__ __launch_bounds__(64 * kSmallWaves) void small_kernel(const kacc_inte
       }
       const uint32_t r = pos0 + lane;
       if (r >= rows) continue;
-      const uint32_t wk = s_w[r];
+      uint32_t wk;
+      if constexpr (kSweepable)
+        wk = s_w[r];
+      else
+        wk = kb == 0 ? w[g] : w[kSmallBatch + g];  // this lane's own row
       const uint64_t sl = wk & KACC_SLOT_MASK;
       if (sl >= st.proc_slots) {
         raise_err(st.err, kErrSlot);
