@@ -791,7 +791,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 template <int Z>
-__global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(Z <= 2 ? 6 : 1))) void small_kernel(
+__global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(Z <= 2 ? 6 : Z <= 4 ? 5 : 1))) void small_kernel(
     const kacc_interval b, const DevState st) {
   constexpr bool kNT = true, kNtLd = true;  // as interval_kernel's production variant
   __shared__ double s_d_all[kSmallWaves][kSmallRows];

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into pmc_traffic.json.
 
-usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR SOURCE_LABEL OUT.json [CONFIG]
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR SOURCE_LABEL OUT.json [CONFIG [KERNEL]]
+
+KERNEL is a substring of the profiled kernel name (default "interval_kernel<4, 0>");
+an existing OUT.json keeps its other configs' entries.
 
 FETCH_SIZE is doubled (MI355X_MICROARCH.md §HBM: gfx950 tallies 128-B streaming
 reads at 64 B); both counters are KiB.  Per launch of kacc::interval_kernel<Z,0>.
@@ -28,19 +31,24 @@ def values(d, counter, kernel="interval_kernel<4, 0>"):
 def main():
     fdir, wdir, label, out = sys.argv[1:5]
     cfg = int(sys.argv[5]) if len(sys.argv) > 5 else 3
+    kernel = sys.argv[6] if len(sys.argv) > 6 else "interval_kernel<4, 0>"
     from kepler_amd import accel, fleet
 
-    layout = fleet.config_layout(cfg)
+    layout = fleet.config_layout(cfg, nodes=40000 if cfg == 1 else None)  # bench.py --config 1 fleet
     s = layout.sizes()
     alg = accel.interval_bytes(layout.zones, *[s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
-    fv, wv = values(fdir, "FETCH_SIZE"), values(wdir, "WRITE_SIZE")
+    fv, wv = values(fdir, "FETCH_SIZE", kernel), values(wdir, "WRITE_SIZE", kernel)
     if not fv or not wv:
-        raise SystemExit("no interval_kernel counter rows found")
+        raise SystemExit(f"no {kernel} counter rows found")
     fm, wm = statistics.median(fv), statistics.median(wv)
-    res = {
+    res = {}
+    if os.path.exists(out):
+        with open(out) as f:
+            res = json.load(f)
+    res.update({
         f"config{cfg}": {
             "n_procs": s["n_procs"],
-            "kernel": "kacc::interval_kernel<4,0>",
+            "kernel": "kacc::" + kernel.replace(" ", ""),
             "fetch_size_kib_median": fm,
             "write_size_kib_median": wm,
             "hbm_bytes_per_launch": (2.0 * fm + wm) * 1024.0,
@@ -51,7 +59,7 @@ def main():
             "source": label,
             "raw_kib": {"FETCH_SIZE": fv, "WRITE_SIZE": wv},
         }
-    }
+    })
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     r = res[f"config{cfg}"]
