@@ -10,9 +10,15 @@ node split + segmented CPU-time sums + process/container/VM/pod attribution
 Workload: BASELINE config 3 per GPU — 10k nodes x 2k processes, Z = 4 RAPL
 zones (package/core/uncore/dram), ~1.6k container processes / 200 containers /
 71 pods / 20 VMs per node, synthetic inputs (kepler_amd/fleet.py) resident in
-HBM before timing.  Scaling is weak: every rank owns its own 10k-node shard
-(node snapshots are independent), so N GPUs process N x 20M process rows per
-interval; only the namespace totals cross GPUs.
+HBM before timing.  Scaling is weak: the fleet has N x 10k nodes, cut into N
+node ranges by shard.plan_node_ranges (balanced process rows), and every rank
+generates and owns only its range (node snapshots are independent), so N GPUs
+process N x 20M process rows per interval.  Only the cluster totals cross GPUs:
+per-namespace and cluster node totals, all-reduced by the library's own RCCL
+communicator (kacc_cluster_join + kacc_allreduce_namespaces, the C ABI a cgo
+caller uses; at N = 1 the same call runs with a one-rank communicator).
+torch.distributed (gloo) is only the control plane: rank-0 unique-id
+broadcast, barriers, max-over-ranks timing.
 
 Prints ONE JSON line on rank 0.  Launch with N > 1 as
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -52,6 +58,10 @@ def parse():
     ap.add_argument("--cpu-nodes", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--node-order", action="store_true", help="launch heaviest nodes first")
+    ap.add_argument("--fragment", type=float, default=0.0,
+                    help="process slots on a random subset of each node's slot range of (1+F) x rows, "
+                         "with node_proc_span (the slot join's steady state under churn)")
+    ap.add_argument("--cpu-runs", type=int, default=0, help="CPU baseline: timed runs (0 = as many as fit)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -61,8 +71,47 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds):
-    """Go-faithful oracle (C++ restatement with Go's data structures), 1 thread."""
+def host_cpu():
+    """CPU model and core counts of this host (report them beside the CPU baseline)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        usable = os.cpu_count()
+    return dict(model=model, nproc=os.cpu_count(), usable=usable)
+
+
+def _median_rate(run, rows, budget_s, min_runs=5, max_runs=0):
+    """Warm-up call, then timed calls until the budget (>= min_runs); rows / median seconds."""
+    run(-1)  # warm-up (untimed)
+    times = []
+    t_end = time.perf_counter() + budget_s
+    k = 0
+    while len(times) < min_runs or (time.perf_counter() < t_end and (not max_runs or len(times) < max_runs)):
+        t0 = time.perf_counter()
+        run(k)
+        times.append(time.perf_counter() - t0)
+        k += 1
+    med = float(np.median(times))
+    return dict(value=rows / med, runs=len(times), median_s=med, min_s=float(np.min(times)),
+                max_s=float(np.max(times)), seconds=float(np.sum(times)))
+
+
+def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds, max_runs=0):
+    """The C++ restatement of the Go path on this host's cores (steady_clock-style timing of
+    the attribution call only; warm-up, then the median of >= 5 runs of one interval each).
+
+    gofaithful: Go's data structures (string-keyed maps, per-object zone maps), 1 thread —
+    the reference attributes on one goroutine; soa: the flat-array oracle, 1 thread;
+    soa_mt: the flat-array oracle over node ranges on the host's usable cores."""
     from kepler_amd import fleet
     from oracle.oracle import GoFaithful, Oracle
 
@@ -71,44 +120,58 @@ def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds):
     _, sizes, _ = subs[0]
     caps = dict(nodes=sizes["n_nodes"], proc_slots=sizes["n_procs"], ctr_slots=sizes["n_ctrs"],
                 vm_slots=sizes["n_vms"], pod_slots=sizes["n_pods"])
+    zidx = (nodes[:, None] * layout.zones + np.arange(layout.zones)).reshape(-1)
+
+    def batch(k):  # interval k >= 0 of the sample: distinct process inputs + fresh node counters
+        k = max(k, 0)
+        a = dict(subs[1 + k % (len(subs) - 1)][0])
+        na = node_steps[k % len(node_steps)]
+        for key in ("node_ts_ns", "node_usage_ratio", "node_status"):
+            a[key] = np.ascontiguousarray(na[key][nodes])
+        a["zone_energy"] = np.ascontiguousarray(na["zone_energy"][zidx])
+        return a
+
     out = {}
-    for name, cls in (("gofaithful", GoFaithful), ("soa", Oracle)):
+    for name, cls, budget in (("gofaithful", GoFaithful, seconds), ("soa", Oracle, min(seconds, 5.0))):
         o = cls(layout.zones, **caps)
         o.interval(subs[0][0], sizes)  # first read (untimed, as on the GPU)
-        done, t_run, k = 0, 0.0, 0
-        budget = seconds if name == "gofaithful" else min(seconds, 5.0)
-        while t_run < budget:
-            a = dict(subs[1 + k % (len(subs) - 1)][0])
-            na = node_steps[k % len(node_steps)]
-            for key in ("node_ts_ns", "node_usage_ratio", "node_status"):
-                a[key] = np.ascontiguousarray(na[key][nodes])
-            zidx = (nodes[:, None] * layout.zones + np.arange(layout.zones)).reshape(-1)
-            a["zone_energy"] = np.ascontiguousarray(na["zone_energy"][zidx])
-            t0 = time.perf_counter()
-            o.interval(a, sizes)
-            t_run += time.perf_counter() - t0
-            done += sizes["n_procs"]
-            k += 1
-        out[name] = dict(value=done / t_run, intervals=k, seconds=t_run)
-    # the flat-array port on the host's cores (node ranges per thread), on a
-    # 10x larger node sample: the strongest CPU number this repo can produce
-    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        pre = [batch(k) for k in range(8)]
+        out[name] = _median_rate(lambda k: o.interval(pre[max(k, 0) % 8], sizes), sizes["n_procs"], budget,
+                                 max_runs=max_runs)
+    # the flat-array port on the host's cores (node ranges per thread), on a 10x larger node
+    # sample: the strongest CPU number this repo can produce
+    threads = max(1, min(16, host_cpu()["usable"] or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
     nodes_mt = np.arange(min(10 * n_nodes, layout.n_nodes))
     subs_mt = [fleet.subset_interval(a, nodes_mt, layout.zones) for a in intervals[:3]]
     _, sizes_mt, _ = subs_mt[0]
     o = Oracle(layout.zones, nodes=sizes_mt["n_nodes"], proc_slots=sizes_mt["n_procs"],
                ctr_slots=sizes_mt["n_ctrs"], vm_slots=sizes_mt["n_vms"], pod_slots=sizes_mt["n_pods"])
     o.interval_mt(subs_mt[0][0], sizes_mt, threads)
-    done, t_run, k = 0, 0.0, 0
-    while t_run < 5.0:
-        a = subs_mt[1 + k % 2][0]
-        t0 = time.perf_counter()
-        o.interval_mt(a, sizes_mt, threads)
-        t_run += time.perf_counter() - t0
-        done += sizes_mt["n_procs"]
-        k += 1
-    out["soa_mt"] = dict(value=done / t_run, threads=threads, intervals=k, procs=sizes_mt["n_procs"])
+    out["soa_mt"] = _median_rate(lambda k: o.interval_mt(subs_mt[1 + max(k, 0) % 2][0], sizes_mt, threads),
+                                 sizes_mt["n_procs"], 5.0, max_runs=max_runs)
+    out["soa_mt"].update(threads=threads, procs=sizes_mt["n_procs"])
     return out, sizes
+
+
+def exchange_unique_id(rank, world, make_id):
+    """Rank 0's RCCL unique id, handed to every rank over the torch.distributed control group."""
+    uid = make_id() if rank == 0 else None
+    if world > 1:
+        import torch.distributed as dist
+
+        box = [uid]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    return uid
+
+
+def bench_nodes(config, world, nodes=None):
+    """Fleet size of a config at `world` GPUs: weak scaling (a fixed shard per GPU) except
+    config 4, whose 100k-node fleet is split over the GPUs (strong scaling)."""
+    if config == 4:
+        return nodes or 100_000
+    per = nodes or {1: 40000, 2: 1000, 3: 10000, 5: 1000}[config]
+    return per * world
 
 
 def main():
@@ -120,30 +183,25 @@ def main():
     import torch
     import torch.distributed as dist
 
-    # rehearsal of the N > 1 logic on a one-GPU box (never the driver's runs):
-    # KACC_BENCH_BACKEND=gloo KACC_BENCH_DEVICE=0 puts every rank on one device
-    backend = os.environ.get("KACC_BENCH_BACKEND", "nccl")
-    dev = int(os.environ.get("KACC_BENCH_DEVICE", local))
-    torch.cuda.set_device(dev)
+    torch.cuda.set_device(local)
     # an explicit stream: the engine launches on it and the HIP events below
     # time exactly that stream (a NULL handle would mean the context's stream)
     torch.cuda.set_stream(torch.cuda.Stream())
-    if world > 1:
-        if backend == "nccl":  # RCCL over xGMI
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend)
+    comm_stream = torch.cuda.Stream()  # the cluster all-reduce overlaps the next interval
+    if world > 1:  # control plane only (unique id, barriers, max over ranks); data path: RCCL
+        dist.init_process_group("gloo")
 
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
     t_setup = time.time()
-    nodes = args.nodes or {1: 40000, 2: 1000, 3: 10000, 4: -(-100000 // world), 5: 1000}[args.config]
-    layout = fleet.config_layout(args.config, seed=fleet.SEED + 7919 * rank, nodes=nodes)
-    sim = fleet.FleetSim(layout, seed=fleet.SEED + 7919 * rank)
+    total_nodes = bench_nodes(args.config, world, args.nodes)
+    lo, hi, layout = fleet.config_shard(args.config, world, rank, total_nodes, fragment_slots=args.fragment)
+    sim = fleet.FleetSim(layout, seed=fleet.SEED + lo)
     Z = layout.zones
     sizes = layout.sizes()
-    log(rank, f"[bench] layout {sizes} Z={Z} built in {time.time() - t_setup:.1f}s")
+    log(rank, f"[bench] rank 0 nodes [{lo}, {hi}) of {total_nodes}: {sizes} Z={Z} "
+              f"built in {time.time() - t_setup:.1f}s")
 
     K = max(1, args.intervals)
     n_steps = args.warmup + args.steps
@@ -154,10 +212,14 @@ def main():
     node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_ivs)]
     log(rank, f"[bench] inputs generated in {time.time() - t_setup:.1f}s")
 
-    acc = accel.Accel(Z, **layout.capacities(), device=dev)
+    acc = accel.Accel(Z, **layout.capacities(), device=local)
+    uid = exchange_unique_id(rank, world, accel.Cluster.unique_id)
+    cluster = accel.Cluster.join(acc, uid, world, rank)
     stream = current_stream_handle()
     assert stream != 0
     statics = to_device(layout.static_arrays())
+    if args.fragment > 0:  # the slot join's per-node spans: rows moved in slot order
+        statics.update(to_device({"node_proc_span": layout.proc_span()}))
     dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
                 for a in full]
     node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")
@@ -182,12 +244,14 @@ def main():
     ns_off, ns_slot = layout.namespace_csr()
     ns_t = to_device({"off": ns_off, "slot": ns_slot})
     n_ns = len(ns_off) - 1
-    # namespace totals double-buffered: step k's RCCL all-reduce (async, on the
-    # process group's stream) overlaps step k+1's interval kernel; buffer k % 2
-    # is rewritten only after the all-reduce of step k-2 has been waited for.
+    # cluster totals double-buffered: step k's all-reduce (comm stream) overlaps step k+1's
+    # interval; buffer k % 2 is rewritten only after the all-reduce of step k-2 is done
     ns_e = [torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
     ns_p = [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
-    pending = [None, None]
+    nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+    nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+    done = [None, None]
+    cs = comm_stream.cuda_stream
 
     def step(k, ev=None):
         if ev is not None:
@@ -199,25 +263,16 @@ def main():
         if ev is not None:
             ev[1].record()
         b = k % 2
-        if pending[b] is not None:  # stream-level wait (no host sync)
-            for w in pending[b]:
-                w.wait()
-            pending[b] = None
-        acc.namespace_totals(n_ns, ns_t["off"].data_ptr(), ns_t["slot"].data_ptr(), ns_e[b].data_ptr(),
-                             ns_p[b].data_ptr(), stream)
-        if world > 1:  # cluster-wide namespace totals over xGMI (RCCL): u64 sum is exact
-            pending[b] = [dist.all_reduce(ns_e[b], async_op=True), dist.all_reduce(ns_p[b], async_op=True)]
-
-    def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                for w in pending[b]:
-                    w.wait()
-                pending[b] = None
+        if done[b] is not None:  # stream-level wait (no host sync)
+            torch.cuda.current_stream().wait_event(done[b])
+        cluster.allreduce_namespaces(n_ns, [ns_t["off"].data_ptr()], [ns_t["slot"].data_ptr()],
+                                     [ns_e[b].data_ptr()], [ns_p[b].data_ptr()], [nd_e[b].data_ptr()],
+                                     [nd_p[b].data_ptr()], streams=[stream], comm_streams=[cs])
+        done[b] = torch.cuda.Event()
+        done[b].record(comm_stream)
 
     for k in range(args.warmup):
         step(k)
-    drain()
     acc.sync(stream)
     torch.cuda.synchronize()
     log(rank, f"[bench] warmup done, setup {time.time() - t_setup:.1f}s")
@@ -230,8 +285,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, events[i])
-    drain()  # every all-reduce of the timed steps is inside the timed region
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -252,13 +306,13 @@ def main():
     copy_gbps = 2 * src.numel() * 8 / (float(np.median(cps[1:])) * 1e-3) / 1e9
     del src, dst
 
-    wall_t = torch.tensor([wall], dtype=torch.float64, device="cuda")
-    procs_t = torch.tensor([sizes["n_procs"], sizes["n_nodes"]], dtype=torch.float64, device="cuda")
+    wall_t = torch.tensor([wall], dtype=torch.float64)
+    procs_t = torch.tensor([sizes["n_procs"], sizes["n_nodes"]], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(procs_t)
     wall_max = float(wall_t.item())
-    total_procs, total_nodes = (float(x) for x in procs_t.tolist())
+    total_procs, total_nodes_done = (float(x) for x in procs_t.tolist())
 
     bytes_per_launch = accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
                                             sizes["n_vms"], sizes["n_pods"])
@@ -270,7 +324,7 @@ def main():
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        ent = pmc.get(f"config{args.config}")
+        ent = pmc.get(f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else ""))
         if ent and ent.get("n_procs") == sizes["n_procs"]:
             traffic = ent.get("hbm_bytes_per_launch")
 
@@ -290,8 +344,10 @@ def main():
         "config": {
             "workload": f"config{args.config}: {sizes['n_nodes']} nodes x "
                         f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs, Z={Z} per GPU"
-                        + (f", {K} intervals per step (kacc_run_intervals)" if K > 1 else ""),
+                        + (f", {K} intervals per step (kacc_run_intervals)" if K > 1 else "")
+                        + (f", fragmented slots ({args.fragment:g}, node_proc_span)" if args.fragment else ""),
             "intervals_per_step": K,
+            "fleet_nodes": total_nodes,
             "nodes_per_gpu": sizes["n_nodes"],
             "procs_per_gpu": sizes["n_procs"],
             "containers_per_gpu": sizes["n_ctrs"],
@@ -299,10 +355,11 @@ def main():
             "pods_per_gpu": sizes["n_pods"],
             "zones": Z,
             "namespaces": n_ns,
-            "parallelism": f"node-sharded x{world} (namespace totals all-reduced over "
-                           f"{'RCCL' if backend == 'nccl' else backend})",
+            "fragment_slots": args.fragment,
+            "parallelism": f"node-sharded x{world} (shard.plan_node_ranges); namespace + cluster node "
+                           f"totals all-reduced over RCCL by kacc_allreduce_namespaces",
         },
-        "node_snapshots_per_s": total_nodes * K * args.steps / wall_max,
+        "node_snapshots_per_s": total_nodes_done * K * args.steps / wall_max,
         "kernel_ms": k_avg_ms,
         "roofline": {
             "bound": "hbm",
@@ -325,19 +382,29 @@ def main():
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res, cs = cpu_baseline(layout, [prime] + full, node_steps, args.cpu_nodes, args.cpu_seconds)
+        res, cs_ = cpu_baseline(layout, [prime] + full, node_steps, args.cpu_nodes, args.cpu_seconds,
+                                max_runs=args.cpu_runs)
         gf = res["gofaithful"]
+        hc = host_cpu()
         result["cpu_baseline"] = {
             "value": gf["value"],
             "unit": "proc-attr/s",
             "cores": 1,
             "kind": "port",
-            "sample": f"go-faithful C++ restatement of the Go path (oracle/kor_gf_interval: string-keyed "
-                      f"maps, per-object zone maps), first {cs['n_nodes']} nodes of the same fleet "
-                      f"({cs['n_procs']} procs, Z={Z}), {gf['intervals']} intervals in {gf['seconds']:.1f}s",
+            "sample": f"C++ restatement of the Go path with Go's data structures (oracle/kor_gf_interval: "
+                      f"string-keyed maps, per-object zone maps), 1 thread, first {cs_['n_nodes']} nodes of the "
+                      f"same fleet ({cs_['n_procs']} procs, Z={Z}) per run: median of {gf['runs']} timed runs "
+                      f"after a warm-up ({gf['seconds']:.1f} s)",
+            "cpu_model": hc["model"],
+            "nproc": hc["nproc"],
+            "usable_cores": hc["usable"],
+            "median_s": gf["median_s"],
+            "runs": gf["runs"],
             "soa_port_1thread": res["soa"]["value"],
             "soa_port_threads": {"value": res["soa_mt"]["value"], "threads": res["soa_mt"]["threads"],
-                                 "sample": f"{res['soa_mt']['procs']} procs, {res['soa_mt']['intervals']} intervals"},
+                                 "runs": res["soa_mt"]["runs"],
+                                 "sample": f"{res['soa_mt']['procs']} procs per run, median of "
+                                           f"{res['soa_mt']['runs']} runs"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
 
@@ -347,6 +414,7 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    cluster.close()
     acc.close()
     if world > 1:
         dist.destroy_process_group()

@@ -40,12 +40,13 @@
 #define KEPLER_ACCEL_H
 
 #include <stdint.h>
+#include <stddef.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define KACC_ABI_VERSION 1u
+#define KACC_ABI_VERSION 2u
 #define KACC_MAX_ZONES 8u
 
 /* Status codes. */
@@ -207,7 +208,15 @@ typedef enum kacc_table {
 uint32_t kacc_abi_version(void);
 int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out);
 void kacc_destroy(kacc_ctx *ctx);
+/* Message of the last failed call on ctx, or (ctx NULL) of the last failed
+ * call made without a context (kacc_create, kacc_create_multi, ...) on ANY
+ * thread of the process: a cgo caller needs no runtime.LockOSThread between
+ * the failing call and this one.  The pointer stays valid until the next
+ * failing call; kacc_last_error_copy() copies the message into buf (len
+ * bytes incl. the NUL, truncated) under the library's lock and returns the
+ * full message length — the form to use from cgo.                           */
 const char *kacc_last_error(const kacc_ctx *ctx);
+size_t kacc_last_error_copy(const kacc_ctx *ctx, char *buf, size_t len);
 int kacc_get_config(const kacc_ctx *ctx, kacc_config *out);
 
 /* Zero every state table (fresh PowerMonitor, snapshot == nil). */
@@ -231,15 +240,26 @@ int kacc_validate_host(const kacc_ctx *ctx, const kacc_interval *host_batch);
 
 /* ---- pinned host batch path (what the cgo shim uses) -------------------- */
 typedef struct kacc_batch kacc_batch;
-/* Allocates pinned host arrays for a batch of the given sizes.  *view points
- * at the batch's own descriptor: its arrays are writable pinned host memory
- * (cast away const) that the caller fills; the caller may also set `flags`
- * and set the optional node_status / node_cpu_delta / node_order to NULL.   */
-int kacc_batch_alloc(kacc_ctx *ctx, uint32_t n_nodes, uint32_t n_procs, uint32_t n_ctrs,
-                     uint32_t n_vms, uint32_t n_pods, kacc_batch **out, kacc_interval **view);
+/* Shape of a pinned batch (SURVEY §8(b) kacc_shape): row capacities of each
+ * interval and the number of consecutive intervals one submit runs (a replay
+ * of `intervals` collection intervals, as kacc_run_intervals; 1 = live).     */
+typedef struct kacc_shape {
+  uint32_t n_nodes, n_procs, n_ctrs, n_vms, n_pods;
+  uint32_t intervals;
+} kacc_shape;
+/* Allocates pinned host arrays (and their device twins) for shape->intervals
+ * intervals of the given capacities.  *views points at the batch's own
+ * descriptors, views[0 .. intervals-1]: their arrays are writable pinned host
+ * memory (cast away const) that the caller fills.  Per view the caller may
+ * set `flags`, lower n_nodes / n_procs / n_ctrs / n_vms / n_pods (never above
+ * the shape: only the used prefix of each array is copied) and set the
+ * optional node_status / node_cpu_delta / node_order / node_proc_span to
+ * NULL; every other pointer is fixed (submit rejects a moved pointer).      */
+int kacc_batch_alloc(kacc_ctx *ctx, const kacc_shape *shape, kacc_batch **out, kacc_interval **views);
 /* Validate (host, multi-threaded), copy H2D on the context's copy stream and
- * launch on the context stream (asynchronous).  With two batches the copies
- * of one overlap the kernel of the other (fill B, submit B, wait A, ...).   */
+ * launch the batch's intervals in order on the context stream (asynchronous).
+ * With two batches the copies of one overlap the kernels of the other (fill
+ * B, submit B, wait A, ...).                                                 */
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *batch);
 /* Wait for this batch's interval; afterwards it may be refilled and
  * resubmitted.  Reports device range errors raised up to this interval.    */
@@ -264,6 +284,72 @@ int kacc_table_upload(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
 int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *ns_pod_off,
                           const uint32_t *ns_pod_slot, uint64_t *out_energy, double *out_power,
                           void *stream);
+
+/* ---- multi-GPU cluster: node shards on several GPUs, totals over RCCL ------
+ * SURVEY §8(b)/(e).  Kepler itself has no collectives (each node exports its
+ * own metrics; cluster sums are PromQL's `sum by (namespace)`); here a fleet
+ * is cut into contiguous node shards (one engine context each, no data-path
+ * traffic between them) and only these cross GPUs, over RCCL (xGMI):
+ *   - per-namespace totals over pods (Pod.Namespace, resource/types.go:106-110):
+ *     u64 energy per zone (modular sum: exact, order independent) and f64
+ *     power per zone (sum order fixed per shard; across shards RCCL's order,
+ *     <= 1e-12 relative to any other order);
+ *   - cluster node totals per zone (monitor/types.go:27-40):
+ *     node energy u64 [2*Z] = { Σ ActiveEnergyTotal[z] }, { Σ IdleEnergyTotal[z] }
+ *     node power  f64 [3*Z] = { Σ Power[z] }, { Σ ActivePower[z] }, { Σ IdlePower[z] }
+ *     over every node of each shard's node table;
+ *   - the pods themselves (a pod lives on one node: a gather, not a sum).
+ * RCCL ranks are GPUs.  A process may hold several shards of one GPU (their
+ * partial vectors are added on that GPU in shard order before the collective)
+ * and several GPUs (ncclCommInitAll), or one shard per process
+ * (ncclCommInitRank: the one-process-per-GPU launch of torchrun / MPI).
+ * Per-shard arguments are arrays indexed by local shard; every collective is
+ * enqueued on the shard's stream (streams[s], or the context's stream when
+ * `streams` or streams[s] is NULL) after the work already queued there.
+ * Errors: details via kacc_last_error(first local shard's context).         */
+typedef struct kacc_cluster kacc_cluster;
+#define KACC_UNIQUE_ID_BYTES 128
+/* One process, n shards: shard i = a new context on devices[i] with
+ * capacities cfgs[i] (equal zones); shards of one device must be contiguous
+ * in `devices`.  ctxs[i] receives shard i's context, owned by the cluster
+ * (destroyed by kacc_cluster_destroy, never by kacc_destroy).               */
+int kacc_create_multi(const int *devices, int n, const kacc_config *cfgs, kacc_cluster **out,
+                      kacc_ctx **ctxs);
+/* One process per GPU: rank 0 creates the id and hands it to every rank
+ * (any side channel: torch.distributed, MPI, a file); each rank then joins
+ * with its own context (not owned by the cluster).                          */
+int kacc_cluster_unique_id(uint8_t id[KACC_UNIQUE_ID_BYTES]);
+int kacc_cluster_join(kacc_ctx *ctx, const uint8_t id[KACC_UNIQUE_ID_BYTES], int nranks, int rank,
+                      kacc_cluster **out);
+void kacc_cluster_destroy(kacc_cluster *c);
+/* nranks: GPUs in the cluster; rank: this process's first GPU; n_shards: local shards. */
+int kacc_cluster_info(const kacc_cluster *c, int *nranks, int *rank, int *n_shards);
+/* Cluster namespace totals (and, when out_node_* are non-NULL, cluster node
+ * totals): each shard sums its own pods (kacc_namespace_totals over
+ * ns_pod_off[s] / ns_pod_slot[s]: the shard's pod slots grouped by the global
+ * namespace index, n_ns the same on every shard), then the sums are
+ * all-reduced; every local shard receives the cluster result in its own
+ * out_energy[s] / out_power[s] [n_ns*Z] and out_node_energy[s] [2*Z] /
+ * out_node_power[s] [3*Z] (device pointers on the shard's GPU).  Async: the
+ * partial sums run on streams[s]; the collective runs on comm_streams[s] when
+ * given (after the partial sums), so the next interval can be queued on
+ * streams[s] at once and overlap it — the outputs are complete when
+ * comm_streams[s] (else streams[s]) reaches this point.                    */
+int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                              const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
+                              double *const *out_power, uint64_t *const *out_node_energy,
+                              double *const *out_node_power, void *const *streams,
+                              void *const *comm_streams);
+/* Cluster pod gather: shard s contributes n_pods[s] (HOST) pods, its slots
+ * pod_slot[s] (device), in that order; every local shard receives all pods of
+ * the cluster in (rank, shard) order — energy u64 / power f64 [total*Z] into
+ * out_energy[s] / out_power[s] (device, capacity out_cap pods).  *total
+ * (HOST) = pods in the cluster; first (HOST [n_shards], optional) = the
+ * global index of each local shard's first pod.  Blocks on the count
+ * exchange; KACC_ERANGE when total > out_cap.                               */
+int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *const *pod_slot,
+                     uint64_t out_cap, uint64_t *const *out_energy, double *const *out_power,
+                     uint64_t *total, uint64_t *first, void *const *streams);
 
 /* ---- slot join: workload IDs -> slot words on the device ------------------
  * SURVEY §8f row 1, the step before the path.  Replaces, for a whole fleet,

@@ -12,7 +12,6 @@ from __future__ import annotations
 import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_int, c_uint32, c_uint64, c_void_p
-from dataclasses import dataclass
 from typing import Optional
 
 import numpy as np
@@ -20,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libkepler_accel.so")
 
-KACC_ABI_VERSION = 1
+KACC_ABI_VERSION = 2
 KACC_MAX_ZONES = 8
 KACC_OK = 0
 KACC_EINVAL = -1
@@ -45,6 +44,7 @@ KACC_FAST_MAX_AGGREGATES = 512
 KACC_F_SMALL_NODES = 0x8
 KACC_SMALL_MAX_PROCS = 512
 KACC_SMALL_MAX_AGGREGATES = 128
+KACC_UNIQUE_ID_BYTES = 128
 
 # kacc_table enum, in header order: (name, numpy dtype)
 TABLES = [
@@ -111,6 +111,14 @@ EXPORTS = [
     "kacc_table_download",
     "kacc_table_upload",
     "kacc_namespace_totals",
+    "kacc_create_multi",
+    "kacc_cluster_unique_id",
+    "kacc_cluster_join",
+    "kacc_cluster_destroy",
+    "kacc_cluster_info",
+    "kacc_allreduce_namespaces",
+    "kacc_gather_pods",
+    "kacc_last_error_copy",
     "kacc_interval_bytes",
 ]
 
@@ -176,6 +184,10 @@ ARRAY_DTYPES = {
 }
 
 
+class KaccShape(ctypes.Structure):
+    _fields_ = [(n, c_uint32) for n in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods", "intervals")]
+
+
 class KaccInterval(ctypes.Structure):
     _fields_ = [
         ("n_nodes", c_uint32),
@@ -223,10 +235,19 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_run_intervals.argtypes = [c_void_p, POINTER(KaccInterval), ctypes.c_uint32, c_void_p]
     lib.kacc_sync.argtypes = [c_void_p, c_void_p]
     lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
-    lib.kacc_batch_alloc.argtypes = [
-        c_void_p, c_uint32, c_uint32, c_uint32, c_uint32, c_uint32,
-        POINTER(c_void_p), POINTER(POINTER(KaccInterval)),
-    ]
+    lib.kacc_batch_alloc.argtypes = [c_void_p, POINTER(KaccShape), POINTER(c_void_p), POINTER(POINTER(KaccInterval))]
+    lib.kacc_last_error_copy.argtypes = [c_void_p, c_char_p, ctypes.c_size_t]
+    lib.kacc_last_error_copy.restype = ctypes.c_size_t
+    lib.kacc_create_multi.argtypes = [POINTER(c_int), c_int, POINTER(KaccConfig), POINTER(c_void_p),
+                                      POINTER(c_void_p)]
+    lib.kacc_cluster_unique_id.argtypes = [c_char_p]
+    lib.kacc_cluster_join.argtypes = [c_void_p, c_char_p, c_int, c_int, POINTER(c_void_p)]
+    lib.kacc_cluster_destroy.argtypes = [c_void_p]
+    lib.kacc_cluster_destroy.restype = None
+    lib.kacc_cluster_info.argtypes = [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]
+    lib.kacc_allreduce_namespaces.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 8
+    lib.kacc_gather_pods.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_void_p), c_uint64, POINTER(c_void_p),
+                                     POINTER(c_void_p), POINTER(c_uint64), POINTER(c_uint64), POINTER(c_void_p)]
     lib.kacc_batch_submit.argtypes = [c_void_p, c_void_p]
     lib.kacc_batch_wait.argtypes = [c_void_p, c_void_p]
     lib.kacc_batch_free.argtypes = [c_void_p, c_void_p]
@@ -263,6 +284,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         raise ImportError("libkepler_accel ABI version mismatch")
     _lib = lib
     return lib
+
+
+def last_error(ctx=None) -> str:
+    """kacc_last_error_copy: the message of the last failed call (ctx None: without a context)."""
+    lib = load()
+    buf = ctypes.create_string_buffer(1024)
+    lib.kacc_last_error_copy(ctx, buf, len(buf))
+    return buf.value.decode()
 
 
 def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int) -> int:
@@ -306,10 +335,23 @@ class Accel:
         h = c_void_p()
         rc = self.lib.kacc_create(device, ctypes.byref(self.cfg), ctypes.byref(h))
         if rc != KACC_OK:
-            raise AccelError(rc, self.lib.kacc_last_error(None).decode())
+            raise AccelError(rc, last_error(None))
         self.ctx = h
         self.zones = zones
         self.device = device
+        self.owned = True
+
+    @classmethod
+    def _wrap(cls, handle: int, zones: int, device: int, cfg: "KaccConfig") -> "Accel":
+        """A context owned by a Cluster (kacc_create_multi): never kacc_destroy'ed here."""
+        self = cls.__new__(cls)
+        self.lib = load()
+        self.cfg = cfg
+        self.ctx = c_void_p(handle)
+        self.zones = zones
+        self.device = device
+        self.owned = False
+        return self
 
     # -- plumbing ---------------------------------------------------------
     def _check(self, rc: int) -> None:
@@ -318,7 +360,8 @@ class Accel:
 
     def close(self) -> None:
         if self.ctx:
-            self.lib.kacc_destroy(self.ctx)
+            if self.owned:
+                self.lib.kacc_destroy(self.ctx)
             self.ctx = None
 
     def __enter__(self):
@@ -530,43 +573,81 @@ class Tracker:
             pass
 
 
-@dataclass
+def _field_count(name: str, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int, zones: int) -> int:
+    """Elements of kacc_interval array `name` for these sizes (kacc_engine.hip kBatchFields)."""
+    if name in ("zone_energy", "zone_max"):
+        return n_nodes * zones
+    if name == "node_proc_span":
+        return 2 * n_nodes
+    if name.endswith("_off"):
+        return n_nodes + 1
+    if name.startswith("node_"):
+        return n_nodes
+    return {"proc": n_procs, "ctr": n_ctrs, "vm": n_vms, "pod": n_pods}[name.split("_", 1)[0]]
+
+
 class HostBatch:
-    """A pinned-host batch (kacc_batch_*): the path a cgo caller takes."""
+    """A pinned-host batch of `intervals` consecutive intervals (kacc_batch_*): the cgo path."""
 
-    accel: Accel
-    handle: c_void_p
-    view: "ctypes._Pointer"
+    def __init__(self, accel: Accel, handle: c_void_p, views, shape: KaccShape):
+        self.accel = accel
+        self.handle = handle
+        self.views = views
+        self.shape = shape
+        self.intervals = shape.intervals
+        self.orig = [{name: getattr(views[k], name) for name in INTERVAL_ARRAYS} for k in range(shape.intervals)]
 
-    orig: dict = None
+    @property
+    def view(self):  # interval 0's descriptor (single-interval batches)
+        return ctypes.pointer(self.views[0])
 
     @classmethod
-    def alloc(cls, accel: Accel, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int):
+    def alloc(cls, accel: Accel, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int,
+              intervals: int = 1):
         h = c_void_p()
         v = POINTER(KaccInterval)()
-        accel._check(accel.lib.kacc_batch_alloc(accel.ctx, n_nodes, n_procs, n_ctrs, n_vms, n_pods,
-                                                ctypes.byref(h), ctypes.byref(v)))
-        orig = {name: getattr(v.contents, name) for name in INTERVAL_ARRAYS}
-        return cls(accel, h, v, orig)
+        shape = KaccShape(n_nodes, n_procs, n_ctrs, n_vms, n_pods, intervals)
+        accel._check(accel.lib.kacc_batch_alloc(accel.ctx, ctypes.byref(shape), ctypes.byref(h), ctypes.byref(v)))
+        return cls(accel, h, v, shape)
 
-    def array(self, name: str, count: int) -> np.ndarray:
-        addr = getattr(self.view.contents, name)
+    def capacity(self, name: str) -> int:
+        sh = self.shape
+        return _field_count(name, sh.n_nodes, sh.n_procs, sh.n_ctrs, sh.n_vms, sh.n_pods, self.accel.zones)
+
+    def array(self, name: str, count: int, k: int = 0) -> np.ndarray:
+        if count > self.capacity(name):
+            raise ValueError(f"{name}: {count} elements exceed the batch capacity {self.capacity(name)}")
+        addr = self.orig[k][name]
         dt = np.dtype(ARRAY_DTYPES[name])
-        buf = (ctypes.c_char * (count * dt.itemsize)).from_address(addr)
+        buf = (ctypes.c_char * max(count * dt.itemsize, 1)).from_address(addr)
         return np.frombuffer(buf, dtype=dt, count=count)
 
-    def fill(self, arrays: dict, flags: int = 0) -> None:
-        v = self.view.contents
+    def fill(self, arrays: dict, flags: int = 0, k: int = 0, sizes: Optional[dict] = None) -> None:
+        """Copy `arrays` into interval k's pinned views; `sizes` (default: the shape) sets the view's
+        row counts, which may be below the shape's capacities."""
+        v = self.views[k]
+        sh = self.shape
+        sz = sizes or dict(n_nodes=sh.n_nodes, n_procs=sh.n_procs, n_ctrs=sh.n_ctrs, n_vms=sh.n_vms,
+                           n_pods=sh.n_pods)
+        for key in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods"):
+            if sz[key] > getattr(sh, key):
+                raise ValueError(f"{key}={sz[key]} exceeds the batch shape {getattr(sh, key)}")
+            setattr(v, key, sz[key])
         v.flags = flags
         for name in INTERVAL_ARRAYS:
-            setattr(v, name, self.orig[name])
+            setattr(v, name, self.orig[k][name])
             a = arrays.get(name)
             if a is None:
                 if name in OPTIONAL_ARRAYS:
                     setattr(v, name, None)
                     continue
                 raise ValueError(name)
-            self.array(name, a.size)[:] = a
+            a = np.asarray(a)
+            need = _field_count(name, sz["n_nodes"], sz["n_procs"], sz["n_ctrs"], sz["n_vms"], sz["n_pods"],
+                                self.accel.zones)
+            if a.size != need:
+                raise ValueError(f"{name}: {a.size} elements, the view's sizes need {need}")
+            self.array(name, a.size, k)[:] = a
 
     def submit(self) -> None:
         self.accel._check(self.accel.lib.kacc_batch_submit(self.accel.ctx, self.handle))
@@ -578,3 +659,99 @@ class HostBatch:
         if self.handle:
             self.accel.lib.kacc_batch_free(self.accel.ctx, self.handle)
             self.handle = None
+
+
+def _ptrs(values) -> "ctypes.Array":
+    return (c_void_p * len(values))(*[c_void_p(v or None) for v in values])
+
+
+class Cluster:
+    """Cluster totals over RCCL (kacc_create_multi / kacc_cluster_join, kacc_allreduce_namespaces,
+    kacc_gather_pods).  ``shards`` are the local Accel contexts, in shard order."""
+
+    def __init__(self, handle: c_void_p, shards, owns: bool):
+        self.lib = load()
+        self.handle = handle
+        self.shards = list(shards)
+        self.owns = owns
+
+    @classmethod
+    def create_multi(cls, devices, zones: int, capacities) -> "Cluster":
+        """One process, one shard per entry of ``devices`` (capacities: per-shard dicts of Accel's
+        nodes / proc_slots / ctr_slots / vm_slots / pod_slots)."""
+        lib = load()
+        n = len(devices)
+        devs = (c_int * n)(*devices)
+        cfgs = (KaccConfig * n)(*[KaccConfig(zones, 0, c["nodes"], c["proc_slots"], c["ctr_slots"], c["vm_slots"],
+                                             c["pod_slots"]) for c in capacities])
+        h = c_void_p()
+        ctxs = (c_void_p * n)()
+        rc = lib.kacc_create_multi(devs, n, cfgs, ctypes.byref(h), ctxs)
+        if rc != KACC_OK:
+            raise AccelError(rc, last_error(None))
+        shards = [Accel._wrap(ctxs[i], zones, devices[i], cfgs[i]) for i in range(n)]
+        return cls(h, shards, True)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load()
+        buf = ctypes.create_string_buffer(KACC_UNIQUE_ID_BYTES)
+        rc = lib.kacc_cluster_unique_id(buf)
+        if rc != KACC_OK:
+            raise AccelError(rc, last_error(None))
+        return buf.raw
+
+    @classmethod
+    def join(cls, accel: Accel, uid: bytes, nranks: int, rank: int) -> "Cluster":
+        """One process per GPU: this rank's context joins the cluster named by ``uid``."""
+        h = c_void_p()
+        accel._check(accel.lib.kacc_cluster_join(accel.ctx, ctypes.create_string_buffer(uid, KACC_UNIQUE_ID_BYTES),
+                                                 nranks, rank, ctypes.byref(h)))
+        return cls(h, [accel], False)
+
+    def info(self):
+        a, b, c = c_int(), c_int(), c_int()
+        self.lib.kacc_cluster_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
+
+    def _check(self, rc: int) -> None:
+        if rc != KACC_OK:
+            raise AccelError(rc, self.shards[0].last_error())
+
+    def allreduce_namespaces(self, n_ns: int, ns_pod_off, ns_pod_slot, out_energy, out_power,
+                             out_node_energy=None, out_node_power=None, streams=None, comm_streams=None) -> None:
+        """Per-shard lists of device pointers; node totals when out_node_* are given."""
+        n = len(self.shards)
+        if n_ns and not (len(ns_pod_off) == len(ns_pod_slot) == len(out_energy) == len(out_power) == n):
+            raise ValueError("one namespace CSR and output pair per local shard")
+        node = out_node_energy is not None
+        self._check(self.lib.kacc_allreduce_namespaces(
+            self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_slot) if n_ns else None,
+            _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
+            _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
+            _ptrs(streams) if streams else None, _ptrs(comm_streams) if comm_streams else None))
+
+    def gather_pods(self, n_pods, pod_slot, out_cap: int, out_energy, out_power, streams=None):
+        """Returns (total pods, first global pod index of each local shard)."""
+        n = len(self.shards)
+        cnt = (c_uint32 * n)(*n_pods)
+        total = c_uint64()
+        first = (c_uint64 * n)()
+        self._check(self.lib.kacc_gather_pods(self.handle, cnt, _ptrs(pod_slot), out_cap, _ptrs(out_energy),
+                                              _ptrs(out_power), ctypes.byref(total), first,
+                                              _ptrs(streams) if streams else None))
+        return total.value, list(first)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.kacc_cluster_destroy(self.handle)
+            self.handle = None
+            if self.owns:
+                for s in self.shards:
+                    s.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

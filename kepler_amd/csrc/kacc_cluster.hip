@@ -1,0 +1,558 @@
+// Cluster totals across GPUs over RCCL (SURVEY §8(b) kacc_create_multi /
+// kacc_allreduce_namespaces, §8(e)).
+//
+// Kepler has no collectives: every node exports its own metrics and cluster
+// sums are left to PromQL (`sum by (namespace)`).  The north star moves the
+// fleet onto GPUs as contiguous node shards (kepler_amd/shard.py), so the
+// attribution itself never crosses a GPU; the only cross-GPU quantities are
+//   * per-namespace totals over pods (grouped by Pod.Namespace,
+//     internal/resource/types.go:106-110): u64 energy per zone (modular, exact
+//     in any order) and f64 power per zone;
+//   * cluster node totals per zone: Σ NodeUsage.ActiveEnergyTotal /
+//     IdleEnergyTotal (u64) and Σ Power / ActivePower / IdlePower (f64)
+//     (monitor/types.go:27-40);
+//   * the pods themselves (a pod lives on exactly one node, so "cluster pod
+//     totals" are a gather, not a reduction).
+//
+// A cluster is a set of shards (engine contexts).  RCCL ranks are GPUs: a
+// process may hold several shards on one GPU (their partial vectors are first
+// added on that GPU, in shard order) and several GPUs (ncclCommInitAll), or
+// one shard per process (ncclCommInitRank, the one-process-per-GPU launch).
+// Every collective is enqueued on the shard's stream: nothing here blocks the
+// host except kacc_gather_pods' count exchange.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "kacc_internal.hpp"
+
+namespace kacc {
+namespace cluster {
+
+constexpr int kThreads = 256;
+
+// Cluster node totals of one context: block b reduces table b / Z, zone b % Z
+// over the context's nodes.  Lane l sums nodes l, l+256, ... in order, then a
+// halving tree (l += l+s, s = 128..1): a fixed order, so the f64 sums are
+// reproducible run to run; u64 sums are modular and order independent.
+//   out_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal
+//   out_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower
+template <int Z>
+__global__ __launch_bounds__(kThreads) void node_totals_kernel(uint64_t n_nodes, const uint64_t *active_total,
+                                                               const uint64_t *idle_total, const double *power,
+                                                               const double *active_power,
+                                                               const double *idle_power, uint64_t *out_e,
+                                                               double *out_p) {
+  __shared__ double red_p[kThreads];
+  __shared__ unsigned long long red_e[kThreads];
+  const uint32_t tab = blockIdx.x / Z, z = blockIdx.x % Z, t = threadIdx.x;
+  if (tab < 2) {
+    const uint64_t *src = tab == 0 ? active_total : idle_total;
+    unsigned long long s = 0;
+    for (uint64_t n = t; n < n_nodes; n += kThreads) s += src[n * Z + z];
+    red_e[t] = s;
+  } else {
+    const double *src = tab == 2 ? power : tab == 3 ? active_power : idle_power;
+    double s = 0.0;
+    for (uint64_t n = t; n < n_nodes; n += kThreads) s = s + src[n * Z + z];
+    red_p[t] = s;
+  }
+  __syncthreads();
+  for (uint32_t s = kThreads / 2; s >= 1; s >>= 1) {
+    if (t < s) {
+      if (tab < 2)
+        red_e[t] += red_e[t + s];
+      else
+        red_p[t] = red_p[t] + red_p[t + s];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (tab < 2)
+      out_e[tab * Z + z] = red_e[0];
+    else
+      out_p[(tab - 2) * Z + z] = red_p[0];
+  }
+}
+
+// acc += add, element-wise (u64 modular, f64 one rounding per element).
+__global__ __launch_bounds__(kThreads) void accumulate_kernel(uint64_t n_e, uint64_t *acc_e, const uint64_t *add_e,
+                                                              uint64_t n_p, double *acc_p, const double *add_p) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n_e) acc_e[i] += add_e[i];
+  if (i < n_p) acc_p[i] = acc_p[i] + add_p[i];
+}
+
+// Pod rows of one shard into the gathered vector: row base + i = the pod in
+// slot pod_slot[i] (energy and power per zone, bit copies).
+template <int Z>
+__global__ __launch_bounds__(kThreads) void pod_pack_kernel(uint32_t q, const uint32_t *pod_slot, uint64_t cap,
+                                                            const uint64_t *pe, const double *pp, uint64_t base,
+                                                            uint64_t *out_e, double *out_p, uint32_t *err) {
+  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
+  if (i >= q) return;
+  const uint64_t s = pod_slot[i] & KACC_SLOT_MASK;
+  const uint64_t o = (base + i) * Z;
+  if (s >= cap) {
+    atomicOr(err, 1u << 3);  // the namespace / pod-list range bit of kacc_sync
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      out_e[o + z] = 0;
+      out_p[o + z] = 0.0;
+    }
+    return;
+  }
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    out_e[o + z] = pe[s * Z + z];
+    out_p[o + z] = pp[s * Z + z];
+  }
+}
+
+}  // namespace cluster
+}  // namespace kacc
+
+struct kacc_cluster {
+  int nranks = 0;          // RCCL ranks (GPUs) in the whole cluster
+  int rank0 = 0;           // rank of this process's first local GPU
+  bool owns_shards = false;
+  uint32_t zones = 0;
+  std::vector<kacc_ctx *> shards;    // local shards, in order
+  std::vector<int> dev_first;        // per local GPU: its first shard (shards of a GPU are contiguous)
+  std::vector<int> dev_count;        //                and how many
+  std::vector<ncclComm_t> comms;     // per local GPU
+  std::vector<hipEvent_t> events;    // per shard
+  std::vector<uint64_t *> d_count;   // per local GPU: [1 + nranks] u64 (pod-gather count exchange)
+};
+
+namespace {
+
+int nccl_fail(kacc_ctx *ctx, ncclResult_t r, const char *what) {
+  return kacc_fail(ctx, KACC_EHIP, "%s: %s", what, ncclGetErrorString(r));
+}
+
+#define KACC_NCCL(ctx, call)                                  \
+  do {                                                        \
+    ncclResult_t r_ = (call);                                 \
+    if (r_ != ncclSuccess) return nccl_fail((ctx), r_, #call); \
+  } while (0)
+
+// Events and the count-exchange scratch of a new cluster.
+int cluster_scratch(kacc_cluster *c) {
+  kacc_ctx *c0 = c->shards[0];
+  c->events.assign(c->shards.size(), nullptr);
+  for (size_t s = 0; s < c->shards.size(); ++s) {
+    KACC_HIP(c0, hipSetDevice(c->shards[s]->device));
+    KACC_HIP(c0, hipEventCreateWithFlags(&c->events[s], hipEventDisableTiming));
+  }
+  c->d_count.assign(c->dev_first.size(), nullptr);
+  for (size_t d = 0; d < c->dev_first.size(); ++d) {
+    KACC_HIP(c0, hipSetDevice(c->shards[c->dev_first[d]]->device));
+    KACC_HIP(c0, hipMalloc(&c->d_count[d], 8 * (1 + static_cast<size_t>(c->nranks))));
+  }
+  return KACC_OK;
+}
+
+hipStream_t shard_stream(const kacc_cluster *c, void *const *streams, size_t s) {
+  return (streams && streams[s]) ? static_cast<hipStream_t>(streams[s]) : c->shards[s]->stream;
+}
+
+template <int Z>
+void launch_node_totals(kacc_ctx *x, uint64_t *oe, double *op, hipStream_t st) {
+  hipLaunchKernelGGL((kacc::cluster::node_totals_kernel<Z>), dim3(5 * Z), dim3(kacc::cluster::kThreads), 0, st,
+                     x->cfg.nodes, (const uint64_t *)x->tables[KACC_T_NODE_ACTIVE_TOTAL],
+                     (const uint64_t *)x->tables[KACC_T_NODE_IDLE_TOTAL], (const double *)x->tables[KACC_T_NODE_POWER],
+                     (const double *)x->tables[KACC_T_NODE_ACTIVE_POWER],
+                     (const double *)x->tables[KACC_T_NODE_IDLE_POWER], oe, op);
+}
+
+void node_totals(kacc_ctx *x, uint64_t *oe, double *op, hipStream_t st) {
+  switch (x->cfg.zones) {
+    case 1: launch_node_totals<1>(x, oe, op, st); break;
+    case 2: launch_node_totals<2>(x, oe, op, st); break;
+    case 3: launch_node_totals<3>(x, oe, op, st); break;
+    case 4: launch_node_totals<4>(x, oe, op, st); break;
+    case 5: launch_node_totals<5>(x, oe, op, st); break;
+    case 6: launch_node_totals<6>(x, oe, op, st); break;
+    case 7: launch_node_totals<7>(x, oe, op, st); break;
+    default: launch_node_totals<8>(x, oe, op, st); break;
+  }
+}
+
+template <int Z>
+void launch_pod_pack(kacc_ctx *x, uint32_t q, const uint32_t *slot, uint64_t base, uint64_t *oe, double *op,
+                     hipStream_t st) {
+  const uint32_t grid = (q + kacc::cluster::kThreads - 1) / kacc::cluster::kThreads;
+  hipLaunchKernelGGL((kacc::cluster::pod_pack_kernel<Z>), dim3(grid), dim3(kacc::cluster::kThreads), 0, st, q,
+                     slot, x->cfg.pod_slots, (const uint64_t *)x->tables[KACC_T_POD_ENERGY],
+                     (const double *)x->tables[KACC_T_POD_POWER], base, oe, op, x->d_err);
+}
+
+void pod_pack(kacc_ctx *x, uint32_t q, const uint32_t *slot, uint64_t base, uint64_t *oe, double *op,
+              hipStream_t st) {
+  switch (x->cfg.zones) {
+    case 1: launch_pod_pack<1>(x, q, slot, base, oe, op, st); break;
+    case 2: launch_pod_pack<2>(x, q, slot, base, oe, op, st); break;
+    case 3: launch_pod_pack<3>(x, q, slot, base, oe, op, st); break;
+    case 4: launch_pod_pack<4>(x, q, slot, base, oe, op, st); break;
+    case 5: launch_pod_pack<5>(x, q, slot, base, oe, op, st); break;
+    case 6: launch_pod_pack<6>(x, q, slot, base, oe, op, st); break;
+    case 7: launch_pod_pack<7>(x, q, slot, base, oe, op, st); break;
+    default: launch_pod_pack<8>(x, q, slot, base, oe, op, st); break;
+  }
+}
+
+void accumulate(uint64_t n_e, uint64_t *acc_e, const uint64_t *add_e, uint64_t n_p, double *acc_p,
+                const double *add_p, hipStream_t st) {
+  const uint64_t n = std::max(n_e, n_p);
+  if (!n) return;
+  const uint32_t grid = static_cast<uint32_t>((n + kacc::cluster::kThreads - 1) / kacc::cluster::kThreads);
+  hipLaunchKernelGGL(kacc::cluster::accumulate_kernel, dim3(grid), dim3(kacc::cluster::kThreads), 0, st, n_e,
+                     acc_e, add_e, n_p, acc_p, add_p);
+}
+
+// Shards of one GPU: the later shards' vectors are added into the first one's
+// (in shard order), on the first shard's stream after the others' work.
+int local_combine(kacc_cluster *c, void *const *streams, uint64_t *const *e, uint64_t n_e, double *const *p,
+                  uint64_t n_p) {
+  kacc_ctx *c0 = c->shards[0];
+  for (size_t d = 0; d < c->dev_first.size(); ++d) {
+    const int f = c->dev_first[d], cnt = c->dev_count[d];
+    if (cnt < 2) continue;
+    KACC_HIP(c0, hipSetDevice(c->shards[f]->device));
+    hipStream_t sf = shard_stream(c, streams, f);
+    for (int s = f + 1; s < f + cnt; ++s) {
+      hipStream_t ss = shard_stream(c, streams, s);
+      if (ss != sf) {
+        KACC_HIP(c0, hipEventRecord(c->events[s], ss));
+        KACC_HIP(c0, hipStreamWaitEvent(sf, c->events[s], 0));
+      }
+      accumulate(n_e, e[f], e[s], n_p, p[f], p[s], sf);
+    }
+  }
+  return KACC_OK;
+}
+
+// The first shard's result of each GPU copied to the GPU's other shards.
+int local_broadcast(kacc_cluster *c, void *const *streams, uint64_t *const *e, uint64_t n_e, double *const *p,
+                    uint64_t n_p) {
+  kacc_ctx *c0 = c->shards[0];
+  for (size_t d = 0; d < c->dev_first.size(); ++d) {
+    const int f = c->dev_first[d], cnt = c->dev_count[d];
+    if (cnt < 2) continue;
+    KACC_HIP(c0, hipSetDevice(c->shards[f]->device));
+    hipStream_t sf = shard_stream(c, streams, f);
+    KACC_HIP(c0, hipEventRecord(c->events[f], sf));
+    for (int s = f + 1; s < f + cnt; ++s) {
+      hipStream_t ss = shard_stream(c, streams, s);
+      KACC_HIP(c0, hipStreamWaitEvent(ss, c->events[f], 0));
+      if (n_e) KACC_HIP(c0, hipMemcpyAsync(e[s], e[f], 8 * n_e, hipMemcpyDeviceToDevice, ss));
+      if (n_p) KACC_HIP(c0, hipMemcpyAsync(p[s], p[f], 8 * n_p, hipMemcpyDeviceToDevice, ss));
+    }
+  }
+  return KACC_OK;
+}
+
+// One in-place all-reduce (sum) of e [n_e] u64 and p [n_p] f64 per local GPU.
+int allreduce(kacc_cluster *c, void *const *streams, uint64_t *const *e, uint64_t n_e, double *const *p,
+              uint64_t n_p) {
+  kacc_ctx *c0 = c->shards[0];
+  KACC_NCCL(c0, ncclGroupStart());
+  for (size_t d = 0; d < c->dev_first.size(); ++d) {
+    const int f = c->dev_first[d];
+    hipStream_t sf = shard_stream(c, streams, f);
+    if (n_e) {
+      const ncclResult_t r = ncclAllReduce(e[f], e[f], n_e, ncclUint64, ncclSum, c->comms[d], sf);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(c0, r, "ncclAllReduce(u64)");
+      }
+    }
+    if (n_p) {
+      const ncclResult_t r = ncclAllReduce(p[f], p[f], n_p, ncclFloat64, ncclSum, c->comms[d], sf);
+      if (r != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(c0, r, "ncclAllReduce(f64)");
+      }
+    }
+  }
+  KACC_NCCL(c0, ncclGroupEnd());
+  return KACC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int kacc_create_multi(const int *devices, int n, const kacc_config *cfgs, kacc_cluster **out, kacc_ctx **ctxs) {
+  if (!devices || n <= 0 || !cfgs || !out || !ctxs) return kacc_fail(nullptr, KACC_EINVAL, "NULL argument");
+  *out = nullptr;
+  for (int i = 0; i < n; ++i) {
+    ctxs[i] = nullptr;
+    if (cfgs[i].zones != cfgs[0].zones) return kacc_fail(nullptr, KACC_EINVAL, "shards must share Z");
+    for (int j = 0; j < i; ++j)  // shards of one GPU contiguous: the gather order is the shard order
+      if (devices[j] == devices[i] && devices[i - 1] != devices[i])
+        return kacc_fail(nullptr, KACC_EINVAL, "shards of device %d are not contiguous", devices[i]);
+  }
+  auto *c = new kacc_cluster;
+  c->owns_shards = true;
+  c->zones = cfgs[0].zones;
+  std::vector<int> devlist;
+  for (int i = 0; i < n; ++i) {
+    kacc_ctx *x = nullptr;
+    const int rc = kacc_create(devices[i], &cfgs[i], &x);
+    if (rc != KACC_OK) {
+      const std::string why = kacc_last_error(nullptr);
+      kacc_cluster_destroy(c);
+      return kacc_fail(nullptr, rc, "shard %d: %s", i, why.c_str());
+    }
+    c->shards.push_back(x);
+    if (i == 0 || devices[i] != devices[i - 1]) {
+      c->dev_first.push_back(i);
+      c->dev_count.push_back(0);
+      devlist.push_back(devices[i]);
+    }
+    ++c->dev_count.back();
+  }
+  c->nranks = static_cast<int>(devlist.size());
+  c->rank0 = 0;
+  c->comms.assign(devlist.size(), nullptr);
+  const ncclResult_t r = ncclCommInitAll(c->comms.data(), c->nranks, devlist.data());
+  if (r != ncclSuccess) {
+    c->comms.clear();
+    kacc_cluster_destroy(c);
+    return kacc_fail(nullptr, KACC_EHIP, "ncclCommInitAll over %d GPUs: %s", static_cast<int>(devlist.size()),
+                     ncclGetErrorString(r));
+  }
+  if (cluster_scratch(c) != KACC_OK) {
+    const std::string why = c->shards[0]->err;
+    kacc_cluster_destroy(c);
+    return kacc_fail(nullptr, KACC_EHIP, "cluster scratch: %s", why.c_str());
+  }
+  for (int i = 0; i < n; ++i) ctxs[i] = c->shards[i];
+  *out = c;
+  return KACC_OK;
+}
+
+int kacc_cluster_unique_id(uint8_t id[KACC_UNIQUE_ID_BYTES]) {
+  if (!id) return kacc_fail(nullptr, KACC_EINVAL, "NULL argument");
+  static_assert(sizeof(ncclUniqueId) == KACC_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId u;
+  const ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) return kacc_fail(nullptr, KACC_EHIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  std::memcpy(id, &u, sizeof(u));
+  return KACC_OK;
+}
+
+int kacc_cluster_join(kacc_ctx *ctx, const uint8_t id[KACC_UNIQUE_ID_BYTES], int nranks, int rank,
+                      kacc_cluster **out) {
+  if (!ctx || !id || !out) return KACC_EINVAL;
+  *out = nullptr;
+  if (nranks <= 0 || rank < 0 || rank >= nranks)
+    return kacc_fail(ctx, KACC_EINVAL, "rank %d of %d", rank, nranks);
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  auto *c = new kacc_cluster;
+  c->owns_shards = false;
+  c->zones = ctx->cfg.zones;
+  c->shards.push_back(ctx);
+  c->dev_first.push_back(0);
+  c->dev_count.push_back(1);
+  c->nranks = nranks;
+  c->rank0 = rank;
+  c->comms.assign(1, nullptr);
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  const ncclResult_t r = ncclCommInitRank(&c->comms[0], nranks, u, rank);
+  if (r != ncclSuccess) {
+    c->comms.clear();
+    kacc_cluster_destroy(c);
+    return kacc_fail(ctx, KACC_EHIP, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+  }
+  const int rc = cluster_scratch(c);
+  if (rc != KACC_OK) {
+    kacc_cluster_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return KACC_OK;
+}
+
+void kacc_cluster_destroy(kacc_cluster *c) {
+  if (!c) return;
+  for (size_t d = 0; d < c->comms.size(); ++d) {
+    if (!c->comms[d]) continue;
+    (void)hipSetDevice(c->shards[c->dev_first[d]]->device);
+    (void)hipDeviceSynchronize();
+    (void)ncclCommDestroy(c->comms[d]);
+  }
+  for (size_t d = 0; d < c->d_count.size(); ++d)
+    if (c->d_count[d]) {
+      (void)hipSetDevice(c->shards[c->dev_first[d]]->device);
+      (void)hipFree(c->d_count[d]);
+    }
+  for (size_t s = 0; s < c->events.size(); ++s)
+    if (c->events[s]) {
+      (void)hipSetDevice(c->shards[s]->device);
+      (void)hipEventDestroy(c->events[s]);
+    }
+  if (c->owns_shards)
+    for (kacc_ctx *x : c->shards) kacc_destroy(x);
+  delete c;
+}
+
+int kacc_cluster_info(const kacc_cluster *c, int *nranks, int *rank, int *n_shards) {
+  if (!c) return KACC_EINVAL;
+  if (nranks) *nranks = c->nranks;
+  if (rank) *rank = c->rank0;
+  if (n_shards) *n_shards = static_cast<int>(c->shards.size());
+  return KACC_OK;
+}
+
+int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                              const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
+                              double *const *out_power, uint64_t *const *out_node_energy,
+                              double *const *out_node_power, void *const *streams,
+                              void *const *comm_streams) {
+  if (!c) return KACC_EINVAL;
+  kacc_ctx *c0 = c->shards[0];
+  const size_t ns = c->shards.size();
+  const uint64_t Z = c->zones;
+  const bool nodes = out_node_energy && out_node_power;
+  if ((out_node_energy != nullptr) != (out_node_power != nullptr))
+    return kacc_fail(c0, KACC_EINVAL, "node totals need both output arrays");
+  if (n_ns && (!ns_pod_off || !ns_pod_slot || !out_energy || !out_power))
+    return kacc_fail(c0, KACC_EINVAL, "NULL argument");
+  for (size_t s = 0; s < ns; ++s) {
+    if (n_ns && (!ns_pod_off[s] || !ns_pod_slot[s] || !out_energy[s] || !out_power[s]))
+      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL namespace array", s);
+    if (nodes && (!out_node_energy[s] || !out_node_power[s]))
+      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL node-total array", s);
+  }
+  // 1. partial vectors of every shard, on its stream
+  for (size_t s = 0; s < ns; ++s) {
+    kacc_ctx *x = c->shards[s];
+    hipStream_t st = shard_stream(c, streams, s);
+    if (n_ns) {
+      const int rc = kacc_namespace_totals(x, n_ns, ns_pod_off[s], ns_pod_slot[s], out_energy[s], out_power[s], st);
+      if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
+    }
+    if (nodes) {
+      KACC_HIP(c0, hipSetDevice(x->device));
+      (void)hipGetLastError();
+      node_totals(x, out_node_energy[s], out_node_power[s], st);
+      KACC_HIP(c0, hipGetLastError());
+    }
+  }
+  // 2. shards of one GPU (on the compute streams)
+  int rc = KACC_OK;
+  if (n_ns && (rc = local_combine(c, streams, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
+  if (nodes && (rc = local_combine(c, streams, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
+  // the collective may run on other streams: they wait for the partial sums,
+  // and the caller's next interval on the compute stream overlaps it
+  void *const *cs = comm_streams ? comm_streams : streams;
+  if (comm_streams)
+    for (size_t s = 0; s < ns; ++s) {
+      hipStream_t a = shard_stream(c, streams, s), b = shard_stream(c, comm_streams, s);
+      if (a == b) continue;
+      KACC_HIP(c0, hipSetDevice(c->shards[s]->device));
+      KACC_HIP(c0, hipEventRecord(c->events[s], a));
+      KACC_HIP(c0, hipStreamWaitEvent(b, c->events[s], 0));
+    }
+  // 3. across GPUs (RCCL), 4. back to every shard
+  if (n_ns && (rc = allreduce(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
+  if (nodes && (rc = allreduce(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
+  if (n_ns && (rc = local_broadcast(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
+  if (nodes && (rc = local_broadcast(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK)
+    return rc;
+  return KACC_OK;
+}
+
+int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *const *pod_slot, uint64_t out_cap,
+                     uint64_t *const *out_energy, double *const *out_power, uint64_t *total, uint64_t *first,
+                     void *const *streams) {
+  if (!c) return KACC_EINVAL;
+  kacc_ctx *c0 = c->shards[0];
+  if (!n_pods || !pod_slot || !out_energy || !out_power || !total) return kacc_fail(c0, KACC_EINVAL, "NULL argument");
+  const size_t nd = c->dev_first.size();
+  const uint64_t Z = c->zones;
+  // 1. pods per local GPU, exchanged: every rank learns every rank's count
+  std::vector<uint64_t> local(nd, 0);
+  for (size_t d = 0; d < nd; ++d)
+    for (int s = c->dev_first[d]; s < c->dev_first[d] + c->dev_count[d]; ++s) local[d] += n_pods[s];
+  for (size_t d = 0; d < nd; ++d) {
+    KACC_HIP(c0, hipSetDevice(c->shards[c->dev_first[d]]->device));
+    KACC_HIP(c0, hipMemcpyAsync(c->d_count[d], &local[d], 8, hipMemcpyHostToDevice,
+                                shard_stream(c, streams, c->dev_first[d])));
+  }
+  KACC_NCCL(c0, ncclGroupStart());
+  for (size_t d = 0; d < nd; ++d) {
+    const ncclResult_t r = ncclAllGather(c->d_count[d], c->d_count[d] + 1, 1, ncclUint64, c->comms[d],
+                                         shard_stream(c, streams, c->dev_first[d]));
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return nccl_fail(c0, r, "ncclAllGather(counts)");
+    }
+  }
+  KACC_NCCL(c0, ncclGroupEnd());
+  std::vector<uint64_t> counts(c->nranks, 0);
+  {
+    const int f = c->dev_first[0];
+    KACC_HIP(c0, hipSetDevice(c->shards[f]->device));
+    hipStream_t sf = shard_stream(c, streams, f);
+    KACC_HIP(c0, hipStreamSynchronize(sf));
+    KACC_HIP(c0, hipMemcpy(counts.data(), c->d_count[0] + 1, 8 * counts.size(), hipMemcpyDeviceToHost));
+  }
+  std::vector<uint64_t> off(c->nranks + 1, 0);
+  for (int r = 0; r < c->nranks; ++r) off[r + 1] = off[r] + counts[r];
+  *total = off[c->nranks];
+  if (off[c->nranks] > out_cap)
+    return kacc_fail(c0, KACC_ERANGE, "gathered pods %llu exceed out_cap %llu", (unsigned long long)off[c->nranks],
+                     (unsigned long long)out_cap);
+  // 2. every local shard packs its pods at its global position
+  for (size_t d = 0; d < nd; ++d) {
+    const int f = c->dev_first[d];
+    uint64_t base = off[c->rank0 + static_cast<int>(d)];
+    hipStream_t sf = shard_stream(c, streams, f);
+    KACC_HIP(c0, hipSetDevice(c->shards[f]->device));
+    for (int s = f; s < f + c->dev_count[d]; ++s) {
+      if (first) first[s] = base;
+      if (n_pods[s]) {
+        if (!pod_slot[s]) return kacc_fail(c0, KACC_EINVAL, "shard %d: NULL pod_slot", s);
+        hipStream_t ss = shard_stream(c, streams, s);
+        (void)hipGetLastError();
+        pod_pack(c->shards[s], n_pods[s], pod_slot[s], base, out_energy[f], out_power[f], ss);
+        KACC_HIP(c0, hipGetLastError());
+        if (ss != sf) {
+          KACC_HIP(c0, hipEventRecord(c->events[s], ss));
+          KACC_HIP(c0, hipStreamWaitEvent(sf, c->events[s], 0));
+        }
+      }
+      base += n_pods[s];
+    }
+  }
+  // 3. all-gather-v: one in-place broadcast per rank, its exact block
+  KACC_NCCL(c0, ncclGroupStart());
+  for (int r = 0; r < c->nranks; ++r) {
+    if (!counts[r]) continue;
+    for (size_t d = 0; d < nd; ++d) {
+      const int f = c->dev_first[d];
+      hipStream_t sf = shard_stream(c, streams, f);
+      uint64_t *e = out_energy[f] + off[r] * Z;
+      double *p = out_power[f] + off[r] * Z;
+      ncclResult_t rr = ncclBroadcast(e, e, counts[r] * Z, ncclUint64, r, c->comms[d], sf);
+      if (rr == ncclSuccess) rr = ncclBroadcast(p, p, counts[r] * Z, ncclFloat64, r, c->comms[d], sf);
+      if (rr != ncclSuccess) {
+        (void)ncclGroupEnd();
+        return nccl_fail(c0, rr, "ncclBroadcast(pods)");
+      }
+    }
+  }
+  KACC_NCCL(c0, ncclGroupEnd());
+  return local_broadcast(c, streams, out_energy, off[c->nranks] * Z, out_power, off[c->nranks] * Z);
+}
+
+}  // extern "C"

@@ -24,8 +24,10 @@
 #include <atomic>
 #include <thread>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -1745,7 +1747,12 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
 // =============================================================================
 namespace {
 
-thread_local std::string g_create_error;
+// Errors of calls without a context (kacc_create, kacc_create_multi, ...):
+// process-wide, not thread-local — a cgo caller's next C call may run on
+// another OS thread (goroutines migrate).  kacc_last_error_copy() reads it
+// under the lock.
+std::mutex g_err_mu;
+std::string g_create_error;
 
 struct TableDesc {
   uint32_t elem;   // bytes
@@ -1769,10 +1776,12 @@ int kacc_fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
-  if (ctx)
+  if (ctx) {
     ctx->err = buf;
-  else
+  } else {
+    std::lock_guard<std::mutex> lk(g_err_mu);
     g_create_error = buf;
+  }
   return code;
 }
 
@@ -2078,7 +2087,25 @@ extern "C" {
 uint32_t kacc_abi_version(void) { return KACC_ABI_VERSION; }
 
 const char *kacc_last_error(const kacc_ctx *ctx) {
-  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+  if (ctx) return ctx->err.c_str();
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  return g_create_error.c_str();
+}
+
+size_t kacc_last_error_copy(const kacc_ctx *ctx, char *buf, size_t len) {
+  std::string msg;
+  if (ctx) {
+    msg = ctx->err;
+  } else {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    msg = g_create_error;
+  }
+  if (buf && len) {
+    const size_t n = std::min(len - 1, msg.size());
+    std::memcpy(buf, msg.data(), n);
+    buf[n] = '\0';
+  }
+  return msg.size();
 }
 
 int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
@@ -2096,7 +2123,10 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
   ctx->cfg = *cfg;
   int rc = KACC_OK;
   auto bail = [&](int code) {
-    g_create_error = ctx->err;
+    {
+      std::lock_guard<std::mutex> lk(g_err_mu);
+      g_create_error = ctx->err;
+    }
     kacc_destroy(ctx);
     return code;
   };
@@ -2293,105 +2323,162 @@ int kacc_validate_host(const kacc_ctx *cctx, const kacc_interval *b) {
   return KACC_OK;
 }
 
-int kacc_batch_alloc(kacc_ctx *ctx, uint32_t N, uint32_t P, uint32_t C, uint32_t V, uint32_t Q,
-                     kacc_batch **out, kacc_interval **view) {
-  if (!ctx || !out || !view) return KACC_EINVAL;
-  if (N > ctx->cfg.nodes) return fail(ctx, KACC_EINVAL, "n_nodes exceeds capacity");
+}  // extern "C"
+
+namespace {
+
+// Pointer fields of kacc_interval with their element size and count rule.
+enum BatchDim { kDimN, kDimNZ, kDimN1, kDim2N, kDimP, kDimC, kDimV, kDimQ };
+struct BatchField {
+  size_t off;  // offsetof(kacc_interval, field)
+  uint32_t elem;
+  BatchDim dim;
+  bool optional;
+};
+#define KACC_BF(f, e, d, o) BatchField{offsetof(kacc_interval, f), e, d, o}
+const BatchField kBatchFields[] = {
+    KACC_BF(node_ts_ns, 8, kDimN, false),       KACC_BF(node_usage_ratio, 8, kDimN, false),
+    KACC_BF(node_status, 4, kDimN, true),       KACC_BF(node_cpu_delta, 8, kDimN, true),
+    KACC_BF(node_order, 4, kDimN, true),        KACC_BF(node_proc_span, 4, kDim2N, true),
+    KACC_BF(zone_energy, 8, kDimNZ, false),     KACC_BF(zone_max, 8, kDimNZ, false),
+    KACC_BF(proc_off, 4, kDimN1, false),        KACC_BF(ctr_off, 4, kDimN1, false),
+    KACC_BF(vm_off, 4, kDimN1, false),          KACC_BF(pod_off, 4, kDimN1, false),
+    KACC_BF(proc_cpu_delta, 8, kDimP, false),   KACC_BF(proc_slot, 4, kDimP, false),
+    KACC_BF(ctr_proc_end, 4, kDimC, false),     KACC_BF(ctr_slot, 4, kDimC, false),
+    KACC_BF(vm_proc_end, 4, kDimV, false),      KACC_BF(vm_slot, 4, kDimV, false),
+    KACC_BF(pod_ctr_end, 4, kDimQ, false),      KACC_BF(pod_slot, 4, kDimQ, false),
+};
+#undef KACC_BF
+
+const void *&field_ptr(kacc_interval &b, const BatchField &f) {
+  return *reinterpret_cast<const void **>(reinterpret_cast<char *>(&b) + f.off);
+}
+
+size_t field_bytes(const BatchField &f, uint64_t N, uint64_t P, uint64_t C, uint64_t V, uint64_t Q, uint64_t Z) {
+  uint64_t n = 0;
+  switch (f.dim) {
+    case kDimN: n = N; break;
+    case kDimNZ: n = N * Z; break;
+    case kDimN1: n = N + 1; break;
+    case kDim2N: n = 2 * N; break;
+    case kDimP: n = P; break;
+    case kDimC: n = C; break;
+    case kDimV: n = V; break;
+    case kDimQ: n = Q; break;
+  }
+  return static_cast<size_t>(n * f.elem);
+}
+
+}  // namespace
+
+extern "C" {
+
+int kacc_batch_alloc(kacc_ctx *ctx, const kacc_shape *shape, kacc_batch **out, kacc_interval **views) {
+  if (!ctx || !shape || !out || !views) return KACC_EINVAL;
+  *out = nullptr;
+  *views = nullptr;
+  if (shape->intervals == 0) return fail(ctx, KACC_EINVAL, "a batch needs >= 1 interval");
+  if (shape->n_nodes > ctx->cfg.nodes) return fail(ctx, KACC_EINVAL, "n_nodes exceeds capacity");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   auto *bt = new kacc_batch;
-  const uint64_t Z = ctx->cfg.zones;
-  struct F {
-    const void **h;
-    const void **d;
-    size_t bytes;
-  };
-  kacc_interval &h = bt->host;
-  kacc_interval &d = bt->dev;
-  h.n_nodes = d.n_nodes = N;
-  h.n_procs = d.n_procs = P;
-  h.n_ctrs = d.n_ctrs = C;
-  h.n_vms = d.n_vms = V;
-  h.n_pods = d.n_pods = Q;
-  const F fields[] = {
-      {(const void **)&h.node_ts_ns, (const void **)&d.node_ts_ns, 8ull * N},
-      {(const void **)&h.node_usage_ratio, (const void **)&d.node_usage_ratio, 8ull * N},
-      {(const void **)&h.node_status, (const void **)&d.node_status, 4ull * N},
-      {(const void **)&h.node_cpu_delta, (const void **)&d.node_cpu_delta, 8ull * N},
-      {(const void **)&h.node_order, (const void **)&d.node_order, 4ull * N},
-      {(const void **)&h.node_proc_span, (const void **)&d.node_proc_span, 8ull * N},
-      {(const void **)&h.zone_energy, (const void **)&d.zone_energy, 8ull * N * Z},
-      {(const void **)&h.zone_max, (const void **)&d.zone_max, 8ull * N * Z},
-      {(const void **)&h.proc_off, (const void **)&d.proc_off, 4ull * (N + 1)},
-      {(const void **)&h.ctr_off, (const void **)&d.ctr_off, 4ull * (N + 1)},
-      {(const void **)&h.vm_off, (const void **)&d.vm_off, 4ull * (N + 1)},
-      {(const void **)&h.pod_off, (const void **)&d.pod_off, 4ull * (N + 1)},
-      {(const void **)&h.proc_cpu_delta, (const void **)&d.proc_cpu_delta, 8ull * P},
-      {(const void **)&h.proc_slot, (const void **)&d.proc_slot, 4ull * P},
-      {(const void **)&h.ctr_proc_end, (const void **)&d.ctr_proc_end, 4ull * C},
-      {(const void **)&h.ctr_slot, (const void **)&d.ctr_slot, 4ull * C},
-      {(const void **)&h.vm_proc_end, (const void **)&d.vm_proc_end, 4ull * V},
-      {(const void **)&h.vm_slot, (const void **)&d.vm_slot, 4ull * V},
-      {(const void **)&h.pod_ctr_end, (const void **)&d.pod_ctr_end, 4ull * Q},
-      {(const void **)&h.pod_slot, (const void **)&d.pod_slot, 4ull * Q},
-  };
-  hipError_t ee = hipEventCreateWithFlags(&bt->copied, hipEventDisableTiming);
-  if (ee == hipSuccess) ee = hipEventCreateWithFlags(&bt->done, hipEventDisableTiming);
-  if (ee == hipSuccess) ee = hipHostMalloc(reinterpret_cast<void **>(&bt->h_err), sizeof(uint32_t), hipHostMallocDefault);
-  if (ee != hipSuccess) {
+  bt->cap = *shape;
+  const uint64_t Z = ctx->cfg.zones, K = shape->intervals;
+  bt->host.assign(K, kacc_interval{});
+  bt->dev.assign(K, kacc_interval{});
+  hipError_t e = hipEventCreateWithFlags(&bt->copied, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&bt->done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&bt->h_err), sizeof(uint32_t), hipHostMallocDefault);
+  if (e != hipSuccess) {
     kacc_batch_free(ctx, bt);
-    return fail(ctx, KACC_EHIP, "batch events: %s", hipGetErrorString(ee));
+    return fail(ctx, KACC_EHIP, "batch events: %s", hipGetErrorString(e));
   }
   *bt->h_err = 0;
-  for (const F &f : fields) {
-    const size_t bytes = std::max<size_t>(f.bytes, 8);
-    void *hp = nullptr, *dp = nullptr;
-    hipError_t e = hipHostMalloc(&hp, bytes, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipMalloc(&dp, bytes);
-    if (e != hipSuccess) {
-      if (hp) (void)hipHostFree(hp);
-      kacc_batch_free(ctx, bt);
-      return fail(ctx, KACC_ENOMEM, "batch allocation (%zu B): %s", bytes, hipGetErrorString(e));
+  for (uint64_t k = 0; k < K; ++k) {
+    kacc_interval &h = bt->host[k], &d = bt->dev[k];
+    h.n_nodes = d.n_nodes = shape->n_nodes;
+    h.n_procs = d.n_procs = shape->n_procs;
+    h.n_ctrs = d.n_ctrs = shape->n_ctrs;
+    h.n_vms = d.n_vms = shape->n_vms;
+    h.n_pods = d.n_pods = shape->n_pods;
+    for (const BatchField &f : kBatchFields) {
+      const size_t bytes = std::max<size_t>(
+          field_bytes(f, shape->n_nodes, shape->n_procs, shape->n_ctrs, shape->n_vms, shape->n_pods, Z), 8);
+      void *hp = nullptr, *dp = nullptr;
+      e = hipHostMalloc(&hp, bytes, hipHostMallocDefault);
+      if (hp) bt->allocs.push_back(hp);
+      if (e == hipSuccess) e = hipMalloc(&dp, bytes);
+      if (dp) bt->dev_allocs.push_back(dp);
+      if (e != hipSuccess) {
+        kacc_batch_free(ctx, bt);
+        return fail(ctx, KACC_ENOMEM, "batch allocation (%zu B): %s", bytes, hipGetErrorString(e));
+      }
+      std::memset(hp, 0, bytes);
+      field_ptr(h, f) = hp;
+      field_ptr(d, f) = dp;
     }
-    std::memset(hp, 0, bytes);
-    *f.h = hp;
-    *f.d = dp;
-    bt->bufs.emplace_back(hp, dp);
-    bt->sizes.push_back(f.bytes);
-    bt->fields.push_back(f.h);
   }
+  bt->orig = bt->host;
   *out = bt;
-  *view = &bt->host;
+  *views = bt->host.data();
   return KACC_OK;
 }
 
 // Two (or more) batches pipeline: the H2D copies of a batch run on the copy
-// stream while the previous batch's interval kernel runs on the context
-// stream; the kernel waits for its own copies (event), and a batch's device
-// buffers are not overwritten before its previous kernel has read them.
+// stream while the previous batch's interval kernels run on the context
+// stream; the kernels wait for their own copies (event), and a batch's device
+// buffers are not overwritten before its previous kernels have read them.
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (!ctx || !bt) return KACC_EINVAL;
-  int rc = (bt->host.flags & KACC_F_TRUSTED_LAYOUT) ? check_shape(ctx, &bt->host)
-                                                    : kacc_validate_host(ctx, &bt->host);
-  if (rc != KACC_OK || bt->host.n_nodes == 0) return rc;
+  const uint32_t K = bt->cap.intervals;
+  const uint64_t Z = ctx->cfg.zones;
+  std::vector<kacc_interval> dv(K);
+  uint64_t max_nodes = 0, max_procs = 0, max_pods = 0;
+  for (uint32_t k = 0; k < K; ++k) {
+    kacc_interval &h = bt->host[k];
+    // a view's sizes may shrink (only the used prefix is copied), never grow
+    if (h.n_nodes > bt->cap.n_nodes || h.n_procs > bt->cap.n_procs || h.n_ctrs > bt->cap.n_ctrs ||
+        h.n_vms > bt->cap.n_vms || h.n_pods > bt->cap.n_pods)
+      return fail(ctx, KACC_EINVAL, "interval %u: view sizes exceed the batch shape", k);
+    for (const BatchField &f : kBatchFields) {
+      const void *p = field_ptr(h, f);
+      if (p != field_ptr(bt->orig[k], f) && !(f.optional && p == nullptr))
+        return fail(ctx, KACC_EINVAL, "interval %u: a view pointer was moved (views are fixed)", k);
+    }
+    int rc = (h.flags & KACC_F_TRUSTED_LAYOUT) ? check_shape(ctx, &h) : kacc_validate_host(ctx, &h);
+    if (rc != KACC_OK) return K > 1 ? fail(ctx, rc, "interval %u: %s", k, std::string(ctx->err).c_str()) : rc;
+    dv[k] = bt->dev[k];
+    dv[k].n_nodes = h.n_nodes;
+    dv[k].n_procs = h.n_procs;
+    dv[k].n_ctrs = h.n_ctrs;
+    dv[k].n_vms = h.n_vms;
+    dv[k].n_pods = h.n_pods;
+    dv[k].flags = (h.flags & ~KACC_F_TRUSTED_LAYOUT) | (h.n_nodes ? node_size_flags(h) : 0u);
+    for (const BatchField &f : kBatchFields)  // honour optional arrays the caller switched off
+      if (!field_ptr(h, f)) field_ptr(dv[k], f) = nullptr;
+    max_nodes = std::max<uint64_t>(max_nodes, h.n_nodes);
+    max_procs = std::max<uint64_t>(max_procs, h.n_procs);
+    max_pods = std::max<uint64_t>(max_pods, h.n_pods);
+  }
   KACC_HIP(ctx, hipSetDevice(ctx->device));
-  kacc_interval dv = bt->dev;
-  dv.flags = (bt->host.flags & ~KACC_F_TRUSTED_LAYOUT) | node_size_flags(bt->host);
-  // honour optional arrays the caller switched off
-  if (!bt->host.node_status) dv.node_status = nullptr;
-  if (!bt->host.node_cpu_delta) dv.node_cpu_delta = nullptr;
-  if (!bt->host.node_order) dv.node_order = nullptr;
-  if (!bt->host.node_proc_span) dv.node_proc_span = nullptr;
   if (bt->submitted) KACC_HIP(ctx, hipStreamWaitEvent(ctx->copy_stream, bt->done, 0));
-  for (size_t i = 0; i < bt->bufs.size(); ++i) {
-    if (!bt->sizes[i] || !*bt->fields[i]) continue;  // empty, or an optional array switched off
-    KACC_HIP(ctx, hipMemcpyAsync(bt->bufs[i].second, bt->bufs[i].first, bt->sizes[i],
-                                 hipMemcpyHostToDevice, ctx->copy_stream));
+  for (uint32_t k = 0; k < K; ++k) {
+    kacc_interval &h = bt->host[k];
+    for (const BatchField &f : kBatchFields) {
+      const void *hp = field_ptr(h, f);
+      const size_t bytes = field_bytes(f, h.n_nodes, h.n_procs, h.n_ctrs, h.n_vms, h.n_pods, Z);
+      if (!hp || !bytes || !h.n_nodes) continue;  // switched off, or empty
+      KACC_HIP(ctx, hipMemcpyAsync(const_cast<void *>(field_ptr(bt->dev[k], f)), hp, bytes, hipMemcpyHostToDevice,
+                                   ctx->copy_stream));
+    }
   }
   KACC_HIP(ctx, hipEventRecord(bt->copied, ctx->copy_stream));
-  if ((rc = ensure_items(ctx, dv.n_nodes, dv.n_procs, dv.n_pods)) != KACC_OK) return rc;
+  int rc = ensure_items(ctx, max_nodes, max_procs, max_pods);
+  if (rc != KACC_OK) return rc;
   KACC_HIP(ctx, hipStreamWaitEvent(ctx->stream, bt->copied, 0));
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  launch(ctx->cfg.zones, dv, dev_state(ctx), ctx->stream);
+  const kacc::DevState ds = dev_state(ctx);
+  for (uint32_t k = 0; k < K; ++k)
+    if (dv[k].n_nodes) launch(ctx->cfg.zones, dv[k], ds, ctx->stream);
   KACC_HIP(ctx, hipGetLastError());
   KACC_HIP(ctx, hipMemcpyAsync(bt->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   KACC_HIP(ctx, hipEventRecord(bt->done, ctx->stream));
@@ -2418,15 +2505,14 @@ void kacc_batch_free(kacc_ctx *ctx, kacc_batch *bt) {
   if (!bt) return;
   if (ctx) (void)hipSetDevice(ctx->device);
   if (bt->done && bt->submitted) (void)hipEventSynchronize(bt->done);
-  for (auto &b : bt->bufs) {
-    if (b.first) (void)hipHostFree(b.first);
-    if (b.second) (void)hipFree(b.second);
-  }
+  for (void *p : bt->allocs) (void)hipHostFree(p);
+  for (void *p : bt->dev_allocs) (void)hipFree(p);
   if (bt->copied) (void)hipEventDestroy(bt->copied);
   if (bt->done) (void)hipEventDestroy(bt->done);
   if (bt->h_err) (void)hipHostFree(bt->h_err);
   delete bt;
 }
+
 
 int kacc_table_info(const kacc_ctx *ctx, kacc_table t, uint64_t *elem_bytes, uint64_t *count) {
   if (!ctx || t < 0 || t >= KACC_T_COUNT) return KACC_EINVAL;

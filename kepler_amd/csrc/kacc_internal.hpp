@@ -32,11 +32,12 @@ struct kacc_ctx {
 };
 
 struct kacc_batch {
-  kacc_interval host{};
-  kacc_interval dev{};
-  std::vector<std::pair<void *, void *>> bufs;  // {pinned host, device}
-  std::vector<size_t> sizes;
-  std::vector<const void *const *> fields;  // the view's pointer of each buffer (NULL = switched off)
+  kacc_shape cap{};                 // capacities of every interval + the interval count
+  std::vector<kacc_interval> host;  // [intervals] the caller's views (pinned host pointers)
+  std::vector<kacc_interval> dev;   // [intervals] the same arrays on the device
+  std::vector<kacc_interval> orig;  // [intervals] the views as allocated (pointers are fixed)
+  std::vector<void *> allocs;       // pinned host buffers
+  std::vector<void *> dev_allocs;   // device buffers
   hipEvent_t copied = nullptr;  // H2D of the last submit done (copy stream)
   hipEvent_t done = nullptr;    // the last submit's kernels + error word copy done
   uint32_t *h_err = nullptr;    // pinned: device error word after the last submit

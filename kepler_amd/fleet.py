@@ -278,14 +278,38 @@ def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
         return make_layout(nodes or 10000, 2000, 4, seed, fragment_slots=fragment_slots,
                            fragment_sorted=fragment_sorted)
     if config == 5:
-        rng = np.random.default_rng(seed ^ 5)
-        n = nodes or 1000
-        # truncated Pareto(alpha=1.5) on [10k, 50k] procs per node
-        u = rng.random(n)
-        a, lo, hi = 1.5, 10_000.0, 50_000.0
-        p = lo / (1 - u * (1 - (lo / hi) ** a)) ** (1 / a)
-        return make_layout(n, p.astype(np.int64), 4, seed, procs_per_vm=2, vm_frac=0.02)
+        p = config_procs_per_node(5, nodes or 1000, seed)
+        return make_layout(len(p), p, 4, seed, procs_per_vm=2, vm_frac=0.02)
     raise ValueError(config)
+
+
+def config_procs_per_node(config: int, nodes: int, seed: int = SEED) -> np.ndarray:
+    """Processes per node of a BASELINE config's fleet of ``nodes`` nodes (cheap: no layout)."""
+    if config == 5:
+        # truncated Pareto(alpha=1.5) on [10k, 50k] procs per node
+        rng = np.random.default_rng(seed ^ 5)
+        u = rng.random(nodes)
+        a, lo, hi = 1.5, 10_000.0, 50_000.0
+        return (lo / (1 - u * (1 - (lo / hi) ** a)) ** (1 / a)).astype(np.int64)
+    per = {1: 500, 2: 1000, 3: 2000, 4: 2000}[config]
+    return np.full(nodes, per, dtype=np.int64)
+
+
+def config_shard(config: int, world: int, rank: int, nodes: int, seed: int = SEED,
+                 fragment_slots: float = 0.0):
+    """Rank `rank`'s node range of a `nodes`-node fleet of BASELINE config `config`, cut by
+    shard.plan_node_ranges over the fleet's per-node process counts (balanced rows; config 5
+    is skewed).  Each rank generates only its own nodes (seeded by the range start), so a
+    100k-node fleet is never materialised on one host.  Returns (lo, hi, layout)."""
+    from .shard import plan_node_ranges
+
+    b = plan_node_ranges(config_procs_per_node(config, nodes, seed), world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    s = seed + lo
+    if config == 5:
+        p = config_procs_per_node(5, nodes, seed)[lo:hi]
+        return lo, hi, make_layout(hi - lo, p, 4, s, procs_per_vm=2, vm_frac=0.02, fragment_slots=fragment_slots)
+    return lo, hi, config_layout(config, seed=s, nodes=hi - lo, fragment_slots=fragment_slots)
 
 
 @dataclass

@@ -59,12 +59,19 @@ int main(void) {
   cfg.proc_slots = 4;
   cfg.ctr_slots = cfg.vm_slots = cfg.pod_slots = 1;
   if (kacc_create(0, &cfg, &ctx) != KACC_OK) {
-    fprintf(stderr, "kacc_create: %s\n", kacc_last_error(NULL));
+    char msg[256];
+    kacc_last_error_copy(NULL, msg, sizeof msg); /* the cgo form: no thread affinity */
+    fprintf(stderr, "kacc_create: %s\n", msg);
     return 1;
   }
   kacc_batch *b = NULL;
   kacc_interval *v = NULL;
-  CHECK(kacc_batch_alloc(ctx, 1, 2, 0, 0, 0, &b, &v));
+  kacc_shape shape;
+  memset(&shape, 0, sizeof shape);
+  shape.n_nodes = 1;
+  shape.n_procs = 2;
+  shape.intervals = 1;
+  CHECK(kacc_batch_alloc(ctx, &shape, &b, &v));
   const int64_t t0 = 1000000000000ll;
   fill(v, t0, 0.0, 1000000000ull, 500000000ull, KACC_SLOT_NEW);
   CHECK(kacc_batch_submit(ctx, b));

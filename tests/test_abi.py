@@ -74,6 +74,47 @@ def test_interval_bytes_formula(lib):
     assert accel.interval_bytes(z, n, p, c, v, q) == n * 460 + p * 108 + c * 128 + v * 112 + q * 128
 
 
+def test_create_error_visible_from_another_thread(lib):
+    """kacc_create's error is process-wide: a cgo caller's next C call may land on
+    another OS thread (goroutine migration) and must still see the message."""
+    import threading
+
+    cfg = accel.KaccConfig(99, 0, 1, 1, 1, 1, 1)  # zones out of range
+    rc = []
+    t = threading.Thread(target=lambda: rc.append(lib.kacc_create(0, ctypes.byref(cfg), ctypes.byref(ctypes.c_void_p()))))
+    t.start()
+    t.join()
+    assert rc == [accel.KACC_EINVAL]
+    assert "zones must be" in accel.last_error(None)
+    buf = ctypes.create_string_buffer(8)
+    full = lib.kacc_last_error_copy(None, buf, len(buf))
+    assert full > 7 and len(buf.value) == 7  # truncated, NUL-terminated
+
+
+def test_create_multi_bad_arguments(lib):
+    """kacc_create_multi rejects non-contiguous shards of one device before creating anything."""
+    cfg = (accel.KaccConfig * 3)(*[accel.KaccConfig(2, 0, 1, 1, 1, 1, 1)] * 3)
+    devs = (ctypes.c_int * 3)(0, 1, 0)
+    ctxs = (ctypes.c_void_p * 3)()
+    h = ctypes.c_void_p()
+    assert lib.kacc_create_multi(devs, 3, cfg, ctypes.byref(h), ctxs) == accel.KACC_EINVAL
+    assert "not contiguous" in accel.last_error(None)
+    assert lib.kacc_allreduce_namespaces(None, 0, None, None, None, None, None, None, None, None) == accel.KACC_EINVAL
+
+
+def test_struct_layout_shape(tmp_path):
+    c = tmp_path / "shape.c"
+    c.write_text("""
+#include <stddef.h>
+#include <stdio.h>
+#include "kepler_accel.h"
+int main(void) { printf("%zu %zu\\n", sizeof(kacc_shape), offsetof(kacc_shape, intervals)); return 0; }""")
+    exe = tmp_path / "shape"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    size, off = (int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
+    assert size == ctypes.sizeof(accel.KaccShape) and off == accel.KaccShape.intervals.offset
+
+
 def test_bad_arguments_do_not_crash(lib):
     cfg = accel.KaccConfig(0, 0, 1, 1, 1, 1, 1)  # zones = 0 is invalid
     h = ctypes.c_void_p()

@@ -62,3 +62,44 @@ def test_two_rank_namespace_totals(tmp_path, oracle_lib):
     e_full, p_full = o.namespace_totals(*L.namespace_csr())
     np.testing.assert_array_equal(np.load(tmp_path / "e.npy"), e_full)
     np.testing.assert_allclose(np.load(tmp_path / "p.npy"), p_full, rtol=1e-12)
+
+
+def _bench_worker(rank, world, port, out_dir):
+    """bench.py's N > 1 control logic on gloo: the rank-0 unique id reaches every rank,
+    and every rank generates only its plan_node_ranges cut of the fleet."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from kepler_amd import fleet
+
+    uid = bench.exchange_unique_id(rank, world, lambda: bytes(range(128)))
+    res = {}
+    for config in (3, 4, 5):
+        total = bench.bench_nodes(config, world, nodes=60 if config != 4 else 90)
+        lo, hi, L = fleet.config_shard(config, world, rank, total)
+        res[config] = (lo, hi, L.n_nodes, L.n_procs, total)
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), np.array([uid == bytes(range(128))] +
+                                                            [x for c in (3, 4, 5) for x in res[c]], dtype=np.int64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_control_plane_two_ranks(tmp_path):
+    from kepler_amd import fleet, shard
+
+    world = 2
+    mp.start_processes(_bench_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    rows = [np.load(tmp_path / f"r{r}.npy") for r in range(world)]
+    assert all(r[0] == 1 for r in rows)  # both ranks hold rank 0's id
+    for j, config in enumerate((3, 4, 5)):
+        got = [r[1 + 5 * j: 6 + 5 * j] for r in rows]
+        total = got[0][4]
+        b = shard.plan_node_ranges(fleet.config_procs_per_node(config, int(total)), world)
+        for r in range(world):
+            lo, hi, n_nodes, n_procs, _ = got[r]
+            assert (lo, hi) == (b[r], b[r + 1]) and n_nodes == hi - lo
+            assert n_procs == fleet.config_procs_per_node(config, int(total))[lo:hi].sum()
+        assert got[0][0] == 0 and got[-1][1] == total  # the ranks tile the fleet
+    # weak scaling for configs 3 / 5, strong for config 4
+    assert rows[0][1 + 4] == 120 and rows[0][6 + 4] == 90

@@ -1,0 +1,258 @@
+"""Multi-GPU path through the C ABI (BASELINE config 4) — MI355X only.
+
+A fleet is cut into node shards by shard.plan_node_ranges (shard.shard), every
+shard runs in its own engine context, and the cluster totals cross the shards
+through kacc_create_multi / kacc_allreduce_namespaces / kacc_gather_pods: the
+real RCCL path, here with several shards on the one GPU of the box (their
+partial vectors are added on the GPU, then all-reduced over a one-rank
+communicator).  Nodes are independent, so every shard's state must equal the
+unsharded oracle's (bit-exact); namespace totals: u64 bit-exact, f64 <= 1e-12
+relative (the north star's totals bar: the sum order differs from one
+context's); gathered pods: bit-exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from kepler_amd import accel, fleet, shard
+from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu_ready():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    accel.load()
+    torch.cuda.set_stream(torch.cuda.Stream())
+
+
+def _gather_rows(acc, name, idx, per):
+    """Rows idx (each `per` elements) of a device table, one download per consecutive run."""
+    idx = np.asarray(idx, dtype=np.int64)
+    if not len(idx):
+        return np.zeros(0, dtype=dict(accel.TABLES)[name])
+    cuts = np.flatnonzero(np.diff(idx) != 1) + 1
+    parts = []
+    for run in np.split(idx, cuts):
+        parts.append(acc.download(name, int(run[0]) * per, len(run) * per))
+    return np.concatenate(parts)
+
+
+def _check_shard_tables(shard_acc, sl, lo, hi, maps, want_state, zones, nodes_total):
+    """Shard tables (compact slots) == the unsharded tables at the original slots / nodes."""
+    for name, _ in accel.TABLES:
+        kind = name.split("_")[0]
+        got = shard_acc.download(name)
+        full = want_state[name]
+        n_rows = (hi - lo) if kind == "node" else sl.capacities()[f"{kind}_slots"]
+        per = len(got) // max(n_rows, 1) if n_rows else 1
+        if kind == "node":
+            idx = np.arange(lo, hi)
+        else:
+            idx = maps[kind]
+        if len(idx) == 0:
+            continue
+        want = full.reshape(-1, per)[idx]
+        np.testing.assert_array_equal(got.reshape(-1, per)[: len(idx)], want, err_msg=f"shard [{lo},{hi}) {name}")
+
+
+def _namespace_csr_device(layouts):
+    out = []
+    for sl in layouts:
+        off, slots = sl.namespace_csr()
+        out.append(to_device({"o": off, "s": slots}))
+    return out
+
+
+@pytest.mark.parametrize("world", [8, 3])
+def test_sharded_fleet_matches_unsharded_oracle(world):
+    """One fleet (skewed, VMs, churn, read errors, Z = 4) cut `world` ways; each shard in its
+    own context; namespace + cluster node totals through kacc_allreduce_namespaces and the
+    pods through kacc_gather_pods, against the unsharded oracle."""
+    from oracle.oracle import Oracle
+
+    L = fleet.make_layout(96, [2000, 300, 0, 1, 4096, 700, 12000, 64] * 12, 4, seed=41, n_namespaces=13,
+                          vm_frac=0.03, procs_per_vm=2, shuffle_slots=True)
+    shards = shard.shard(L, world)
+    cl = accel.Cluster.create_multi([0] * world, L.zones, [sl.capacities() for _, _, sl in shards])
+    assert cl.info() == (1, 0, world)  # one GPU: one RCCL rank holding `world` shards
+    ora = Oracle(L.zones, **L.capacities())
+    sim = fleet.FleetSim(L, seed=41, churn=0.04, read_error_frac=0.05)
+    s = current_stream_handle()
+    for k in range(4):
+        a = sim.next_interval()
+        ora.interval(a, L.sizes())
+        keep = []
+        for (lo, hi, sl), acc in zip(shards, cl.shards):
+            sub, sizes, maps = fleet.subset_interval(a, np.arange(lo, hi), L.zones)
+            t = to_device(sub)
+            keep.append(t)
+            acc.run_interval(interval_from_tensors(t, sizes, sl.fast_flag()), s)
+        for acc in cl.shards:
+            acc.sync(s)
+    for (lo, hi, sl), acc in zip(shards, cl.shards):
+        _, _, maps = fleet.subset_interval(a, np.arange(lo, hi), L.zones)
+        _check_shard_tables(acc, sl, lo, hi, maps, ora.state, L.zones, L.n_nodes)
+
+    Z = L.zones
+    n_ns = L.n_namespaces
+    csr = _namespace_csr_device([sl for _, _, sl in shards])
+    oe = [torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(world)]
+    op = [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(world)]
+    ne = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(world)]
+    npw = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(world)]
+    comm = torch.cuda.Stream()
+    cl.allreduce_namespaces(n_ns, [c["o"].data_ptr() for c in csr], [c["s"].data_ptr() for c in csr],
+                            [x.data_ptr() for x in oe], [x.data_ptr() for x in op],
+                            [x.data_ptr() for x in ne], [x.data_ptr() for x in npw],
+                            streams=[s] * world, comm_streams=[comm.cuda_stream] * world)
+    torch.cuda.synchronize()
+    e_o, p_o = ora.namespace_totals(*L.namespace_csr())
+    assert np.count_nonzero(e_o) > 0 and np.count_nonzero(p_o) > 0
+    for r in range(world):  # every shard holds the cluster result
+        np.testing.assert_array_equal(oe[r].cpu().numpy().view(np.uint64), e_o, err_msg=f"shard {r}")
+        np.testing.assert_allclose(op[r].cpu().numpy(), p_o, rtol=1e-12, atol=0, err_msg=f"shard {r}")
+    # cluster node totals: Σ over every node of the unsharded tables
+    st = ora.state
+    want_e = np.concatenate([st[t].reshape(-1, Z).sum(axis=0, dtype=np.uint64)
+                             for t in ("node_active_total", "node_idle_total")])
+    want_p = np.concatenate([st[t].reshape(-1, Z).sum(axis=0)
+                             for t in ("node_power", "node_active_power", "node_idle_power")])
+    for r in range(world):
+        np.testing.assert_array_equal(ne[r].cpu().numpy().view(np.uint64), want_e)
+        np.testing.assert_allclose(npw[r].cpu().numpy(), want_p, rtol=1e-12, atol=0)
+
+    # pod gather: every shard receives all pods in (shard, pod) order = the fleet's pod order
+    slots = [to_device({"s": sl.pod_slot})["s"] for _, _, sl in shards]
+    ge = [torch.zeros(L.n_pods * Z, dtype=torch.int64, device="cuda") for _ in range(world)]
+    gp = [torch.zeros(L.n_pods * Z, dtype=torch.float64, device="cuda") for _ in range(world)]
+    total, first = cl.gather_pods([sl.n_pods for _, _, sl in shards], [x.data_ptr() for x in slots], L.n_pods,
+                                  [x.data_ptr() for x in ge], [x.data_ptr() for x in gp], streams=[s] * world)
+    torch.cuda.synchronize()
+    assert total == L.n_pods
+    assert first == [int(L.pod_off[lo]) for lo, _, _ in shards]
+    want_pe = st["pod_energy"].reshape(-1, Z)[L.pod_slot].reshape(-1)
+    want_pp = st["pod_power"].reshape(-1, Z)[L.pod_slot].reshape(-1)
+    for r in range(world):
+        np.testing.assert_array_equal(ge[r].cpu().numpy().view(np.uint64), want_pe)
+        np.testing.assert_array_equal(gp[r].cpu().numpy().view(np.uint64), want_pp.view(np.uint64))
+    # a too-small output is refused, not overrun
+    with pytest.raises(accel.AccelError) as ei:
+        cl.gather_pods([sl.n_pods for _, _, sl in shards], [x.data_ptr() for x in slots], L.n_pods - 1,
+                       [x.data_ptr() for x in ge], [x.data_ptr() for x in gp])
+    assert ei.value.code == accel.KACC_ERANGE
+    cl.close()
+
+
+def test_cluster_join_one_rank():
+    """The one-process-per-GPU entry (kacc_cluster_unique_id + kacc_cluster_join, what
+    bench.py --gpus N uses) with a one-rank communicator == the context's own totals."""
+    from oracle.oracle import Oracle
+
+    L = fleet.make_layout(20, [500, 2000, 3, 0] * 5, 2, seed=5, n_namespaces=4)
+    acc = accel.Accel(L.zones, **L.capacities())
+    ora = Oracle(L.zones, **L.capacities())
+    sim = fleet.FleetSim(L, seed=5)
+    s = current_stream_handle()
+    for _ in range(3):
+        a = sim.next_interval()
+        t = to_device(a)
+        acc.run_interval(interval_from_tensors(t, L.sizes(), L.fast_flag()), s)
+        ora.interval(a, L.sizes())
+    acc.sync(s)
+    cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
+    assert cl.info() == (1, 0, 1)
+    off, slots = L.namespace_csr()
+    d = to_device({"o": off, "s": slots})
+    Z = L.zones
+    oe = torch.zeros(L.n_namespaces * Z, dtype=torch.int64, device="cuda")
+    op = torch.zeros(L.n_namespaces * Z, dtype=torch.float64, device="cuda")
+    cl.allreduce_namespaces(L.n_namespaces, [d["o"].data_ptr()], [d["s"].data_ptr()], [oe.data_ptr()],
+                            [op.data_ptr()], streams=[s])
+    torch.cuda.synchronize()
+    e_o, p_o = ora.namespace_totals(off, slots)
+    np.testing.assert_array_equal(oe.cpu().numpy().view(np.uint64), e_o)
+    np.testing.assert_array_equal(op.cpu().numpy(), p_o)  # one shard: the namespace kernel's own order
+    cl.close()
+    acc.close()
+
+
+@pytest.mark.timeout(900)
+def test_config4_full_size_sharded_8_ways():
+    """BASELINE config 4 at full size on one GPU: a 100k-node x 2k-process fleet (200M rows,
+    Z = 4) cut 8 ways by plan_node_ranges into 8 contexts, 2 intervals.  Size-independent
+    properties: every shard's tables == the unsharded context's tables at the same nodes /
+    slots (sharding invariance, bit-exact); the all-reduced namespace totals == the
+    unsharded context's (u64 exact, f64 <= 1e-12); oracle parity on a node sample."""
+    from oracle.oracle import Oracle
+
+    L = fleet.config_layout(4, nodes=100_000)
+    Z = L.zones
+    world = 8
+    shards = shard.shard(L, world)
+    assert [hi - lo for lo, hi, _ in shards] == [12_500] * 8
+    full = accel.Accel(Z, **L.capacities())
+    cl = accel.Cluster.create_multi([0] * world, Z, [sl.capacities() for _, _, sl in shards])
+    sim = fleet.FleetSim(L, seed=44)
+    rng = np.random.default_rng(4)
+    sample = np.sort(rng.choice(L.n_nodes, 24, replace=False))
+    ora = None
+    s = current_stream_handle()
+    for k in range(2):
+        a = sim.next_interval()
+        t = to_device(a)
+        full.run_interval(interval_from_tensors(t, L.sizes(), L.fast_flag()), s)
+        full.sync(s)
+        del t
+        for (lo, hi, sl), acc in zip(shards, cl.shards):
+            sub, sizes, _ = fleet.subset_interval(a, np.arange(lo, hi), Z)
+            ts = to_device(sub)
+            acc.run_interval(interval_from_tensors(ts, sizes, sl.fast_flag()), s)
+            acc.sync(s)
+            del ts
+        osub, osizes, omaps = fleet.subset_interval(a, sample, Z)
+        if ora is None:
+            ora = Oracle(Z, nodes=len(sample), proc_slots=osizes["n_procs"], ctr_slots=osizes["n_ctrs"],
+                         vm_slots=osizes["n_vms"], pod_slots=osizes["n_pods"])
+        ora.interval(osub, osizes)
+        print(f"config4 interval {k} done", flush=True)
+    # sharding invariance (slots are consecutive per node in config 4: shard slot i = slot p0 + i)
+    for (lo, hi, sl), acc in zip(shards, cl.shards):
+        base = {"node": lo, "proc": int(L.proc_off[lo]), "ctr": int(L.ctr_off[lo]), "vm": int(L.vm_off[lo]),
+                "pod": int(L.pod_off[lo])}
+        for name, _ in accel.TABLES:
+            kind = name.split("_")[0]
+            got = acc.download(name)
+            if not len(got):
+                continue
+            n_rows = (hi - lo) if kind == "node" else sl.capacities()[f"{kind}_slots"]
+            per = len(got) // n_rows
+            want = full.download(name, base[kind] * per, len(got))
+            np.testing.assert_array_equal(got, want, err_msg=f"shard [{lo},{hi}) {name}")
+    # sampled oracle parity of the unsharded context
+    for name, _ in accel.TABLES:
+        kind = name.split("_")[0]
+        cap = L.n_nodes if kind == "node" else L.capacities()[f"{kind}_slots"]
+        per = full.table_info(name)[1] // cap
+        got = _gather_rows(full, name, omaps[kind], per)
+        np.testing.assert_array_equal(got, ora.state[name], err_msg=name)
+    # cluster namespace totals (RCCL path) == one context's namespace kernel
+    n_ns = L.n_namespaces
+    csr = _namespace_csr_device([sl for _, _, sl in shards])
+    oe = [torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(world)]
+    op = [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(world)]
+    cl.allreduce_namespaces(n_ns, [c["o"].data_ptr() for c in csr], [c["s"].data_ptr() for c in csr],
+                            [x.data_ptr() for x in oe], [x.data_ptr() for x in op], streams=[s] * world)
+    off, slots = L.namespace_csr()
+    d = to_device({"o": off, "s": slots})
+    fe = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
+    fp = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
+    full.namespace_totals(n_ns, d["o"].data_ptr(), d["s"].data_ptr(), fe.data_ptr(), fp.data_ptr(), s)
+    torch.cuda.synchronize()
+    for r in (0, world - 1):
+        np.testing.assert_array_equal(oe[r].cpu().numpy(), fe.cpu().numpy())
+        np.testing.assert_allclose(op[r].cpu().numpy(), fp.cpu().numpy(), rtol=1e-12, atol=0)
+    cl.close()
+    full.close()
