@@ -412,42 +412,48 @@ int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, co
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                    uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream);
 
-/* ---- terminated-workload tracker ----------------------
+/* ---- terminated-workload trackers ---------------------
  * TerminatedResourceTracker (internal/monitor/terminated_resource_tracker.go)
- * for one workload kind, on the device: the top max_size terminated workloads
- * by their final energy in the target zone (the meter's primary zone,
- * monitor.go:123-144): max_size 0 disables (:82), an ID already tracked is
- * ignored (:90), energy below min_energy is dropped (:102), below capacity an
- * item is pushed (:116), at capacity it must beat the minimum (:124);
- * Clear() after an export (process.go:80-84).
+ * for one workload kind, on the device — ONE TRACKER PER NODE, as every
+ * node's PowerMonitor owns its own (monitor.go:123-144): per node, the top
+ * max_size terminated workloads of that node by their final energy in the
+ * target zone (the meter's primary zone): max_size 0 disables (:82), an ID
+ * already tracked is ignored (:90), energy below min_energy is dropped
+ * (:102), below capacity an item is pushed (:116), at capacity it must beat
+ * the node's minimum (:124); Clear() after an export (process.go:80-84), for
+ * every node or for the nodes of a mask (each node exports on its own).
  *
  * kacc_tracker_add() takes one interval's terminated workloads — the per-node
  * segments of kacc_slot_join — and reads their final values from the kind's
- * state tables (the slots are not reused before the next join).  A batch is
- * added as Go's loop over procs.Terminated (process.go:89-99) would add it in
- * the map order "descending target-zone energy, then node, then slot"; Go's
+ * state tables (the slots are not reused before the next join).  A node's
+ * batch is added as Go's loop over procs.Terminated (process.go:89-99) would
+ * add it in the map order "descending target-zone energy, then slot"; Go's
  * map order is unspecified, and for any batch whose energies differ at the
  * retention boundary the retained set is the same for every order.  Ties at
  * the boundary keep items already tracked first (Go's heap requires a strictly
  * higher energy to evict), then the batch order.  Tracked items are frozen
- * copies (energy and power per zone), as Add(prev.Clone()) keeps.           */
+ * copies (energy and power per zone), as Add(prev.Clone()) keeps.  Nodes are
+ * those of the context (kacc_config.nodes): the device holds nodes x max_size
+ * items (x capacity for an unlimited tracker).                              */
 typedef struct kacc_tracker kacc_tracker;
 #define KACC_TRACKER_MAX_BOUNDED 8192u /* largest max_size > 0 supported */
-/* max_size: > 0 top-N (<= KACC_TRACKER_MAX_BOUNDED), 0 disabled, < 0 unlimited
- * (at most `capacity` items, more raise ERANGE).  zone: target zone index in
- * the kind's [slot*Z + z] tables.  min_energy: minEnergyThreshold in µJ.     */
+/* max_size: > 0 top-N per node (<= KACC_TRACKER_MAX_BOUNDED), 0 disabled,
+ * < 0 unlimited (at most `capacity` items per node, more raise ERANGE).
+ * zone: target zone index in the kind's [slot*Z + z] tables.  min_energy:
+ * minEnergyThreshold in µJ.                                                 */
 int kacc_tracker_create(kacc_ctx *ctx, kacc_kind kind, int64_t max_size, uint32_t capacity,
                         uint32_t zone, uint64_t min_energy, kacc_tracker **out);
 void kacc_tracker_destroy(kacc_tracker *t); /* safe before or after kacc_destroy(ctx) */
-int kacc_tracker_clear(kacc_tracker *t, void *stream);
+/* node_mask: DEVICE [nodes], nonzero = clear that node's tracker; NULL = all. */
+int kacc_tracker_clear(kacc_tracker *t, const uint32_t *node_mask, void *stream);
 /* m: the slot map whose kacc_slot_join produced term_key / term_slot /
  * term_count (device pointers); asynchronous on `stream`.                    */
 int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *term_key,
                      const uint32_t *term_slot, const uint32_t *term_count, void *stream);
-/* Items(): synchronous.  *count = tracked items; when the arrays are non-NULL
- * (HOST, sized >= *count; energy/power [*count * Z]) they receive key, node,
- * and the frozen per-zone energy (µJ) and power (µW); highest energy first
- * (bounded trackers and unlimited ones holding <= 8192 items).              */
+/* Items(): synchronous.  *count = tracked items of all nodes; when the arrays
+ * are non-NULL (HOST, sized >= *count; energy/power [*count * Z]) they receive
+ * key, node and the frozen per-zone energy (µJ) and power (µW): node by node
+ * in node order, each node's items highest energy first.                    */
 int kacc_tracker_items(kacc_tracker *t, uint32_t *count, uint64_t *key, uint32_t *node,
                        uint64_t *energy, double *power);
 
@@ -465,7 +471,9 @@ void kacc_zone_agg_destroy(kacc_zone_agg *z); /* safe before or after kacc_destr
  * readings [n_nodes*Z*sockets] sub-zone counters, [node][zone][socket];
  * sub_status (optional, same shape) nonzero = that sub-zone's read failed:
  * the zone's Energy() returns the error there (:104-108), the node's interval
- * fails: KACC_NODE_READ_ERROR is ORed into node_status [n_nodes].  Outputs
+ * fails.  node_status [n_nodes]: the KACC_NODE_READ_ERROR bit of every node is
+ * written — set when one of its zones failed, cleared otherwise (other bits
+ * are kept), so the same array can be passed every interval.  Outputs
  * out_energy / out_max [n_nodes*Z] = the batch's zone_energy / zone_max.      */
 int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_t *sub_status,
                        uint64_t *out_energy, uint64_t *out_max, uint32_t *node_status, void *stream);

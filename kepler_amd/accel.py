@@ -271,7 +271,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                         POINTER(c_void_p)]
     lib.kacc_tracker_destroy.argtypes = [c_void_p]
     lib.kacc_tracker_destroy.restype = None
-    lib.kacc_tracker_clear.argtypes = [c_void_p, c_void_p]
+    lib.kacc_tracker_clear.argtypes = [c_void_p, c_void_p, c_void_p]
     lib.kacc_tracker_add.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kacc_tracker_items.argtypes = [c_void_p, POINTER(c_uint32), c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kacc_slotmap_create.argtypes = [c_void_p, c_int, c_uint32, c_void_p, POINTER(c_void_p)]
@@ -538,8 +538,10 @@ class Tracker:
                                                   ctypes.byref(h)))
         self.handle = h
 
-    def clear(self, stream: int = 0) -> None:
-        self.accel._check(self.lib.kacc_tracker_clear(self.handle, c_void_p(stream or None)))
+    def clear(self, stream: int = 0, node_mask_ptr: int = 0) -> None:
+        """Clear every node's tracker, or the nodes whose (device) mask entry is nonzero."""
+        self.accel._check(self.lib.kacc_tracker_clear(self.handle, c_void_p(node_mask_ptr or None),
+                                                      c_void_p(stream or None)))
 
     def add(self, slotmap: "SlotMap", term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int,
             stream: int = 0) -> None:
@@ -548,7 +550,8 @@ class Tracker:
                                                     c_void_p(stream or None)))
 
     def items(self):
-        """(key u64[n], node u32[n], energy u64[n, Z], power f64[n, Z]), highest energy first."""
+        """(key u64[n], node u32[n], energy u64[n, Z], power f64[n, Z]): node by node, each node's
+        items highest energy first."""
         n = c_uint32()
         self.accel._check(self.lib.kacc_tracker_items(self.handle, ctypes.byref(n), None, None, None, None))
         k = np.zeros(max(n.value, 1), np.uint64)

@@ -1,27 +1,31 @@
-// Terminated-workload tracker on the device.
+// Terminated-workload trackers on the device, one per node.
 //
 // Reference: TerminatedResourceTracker (internal/monitor/
 // terminated_resource_tracker.go): a min-heap of the max_size highest-energy
 // terminated workloads; Add() drops a disabled tracker (:82), a tracked ID
 // (:90), energy below the threshold (:102), pushes below capacity (:116) and
-// evicts the minimum for a strictly higher energy at capacity (:124).  The
-// monitor adds every terminated workload found in the previous snapshot
-// (process.go:87-99) and clears the tracker after an export (process.go:80-84).
+// evicts the minimum for a strictly higher energy at capacity (:124).  Every
+// node's PowerMonitor owns its own tracker (monitor.go:123-144): it adds the
+// terminated workloads of that node's previous snapshot (process.go:87-99)
+// and is cleared after that node's export (process.go:80-84).  So the fleet
+// engine keeps one bounded set PER NODE — the top max_size of that node
+// only — never a fleet-wide top-N.
 //
 // One interval's batch (the slot join's per-node terminated segments, values
 // read from the kind's state tables) is added as Go would add it in the map
-// order "descending target-zone energy, then node, then slot".  In that order
-// the heap simply keeps the max_size best of (tracked ∪ batch), ties at the
-// boundary going to tracked items first (eviction needs a strictly higher
-// energy) and then to the batch order — so the batch is a top-N selection:
-//   filter    one workgroup per node: threshold, "beats the current minimum"
-//             when full, not already tracked; survivors compacted in slot
-//             order + a 65536-bin histogram of a monotone 16-bit energy key
-//   pick      one workgroup: the boundary bin of the max_size-th item
-//   collect   items above the boundary bin -> keep list, in it -> tie list
-//   finalize  one workgroup: exact order of the ties (bitonic sort in LDS),
-//             the new set sorted (energy desc, tracked first, node, slot),
-//             frozen zone values copied, dedupe hash rebuilt
+// order "descending target-zone energy, then slot".  In that order a node's
+// heap keeps the max_size best of (tracked ∪ batch), ties at the boundary
+// going to tracked items first (eviction needs a strictly higher energy) and
+// then to the batch order.  Each node's set is kept sorted (energy desc, then
+// insertion order), so one add is, per node (one workgroup each):
+//   filter  threshold, "beats the current minimum" when full, not tracked;
+//           survivors compacted in LDS (chunks of kChunk in slot order —
+//           equivalent, since the batch order breaks ties by slot)
+//   sort    survivors by (energy desc, slot) — bitonic in LDS
+//   merge   ranks by binary search (tracked i -> i + #survivors strictly
+//           above; survivor j -> j + #tracked at or above), then in place:
+//           tracked items only move to later positions, so they are moved
+//           in blocks from the end (read block, barrier, write block)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,30 +37,9 @@
 namespace kacc {
 namespace trk {
 
-constexpr int kThreads = 256;       // filter / collect workgroups
-constexpr int kFinThreads = 1024;   // pick / finalize workgroup
-constexpr uint32_t kBins = 65536;
-constexpr uint32_t kSortCap = KACC_TRACKER_MAX_BOUNDED;  // ties / set sorted in LDS
-constexpr uint64_t kOld = 1ull << 63;                    // sort key: 0 = tracked item
-constexpr uint32_t kErrTie = 1u << 9;   // more boundary ties than kSortCap
-constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its capacity
-
-struct State {
-  uint32_t size;      // items in the current set
-  uint32_t parity;    // current set buffer
-  uint64_t min_full;  // target-zone energy of the lowest item (set full)
-  uint32_t keep_n, tie_n;
-  uint32_t pick_bin, keep_all, need, pad;
-};
-
-struct Entry {
-  uint64_t e;     // target-zone energy
-  uint64_t key;   // workload ID
-  uint32_t node;
-  uint32_t ref;   // slot (batch item) or index in the current set (tracked)
-  uint32_t old;   // 1: tracked item
-  uint32_t pad;
-};
+constexpr int kThreads = 256;
+constexpr uint32_t kChunk = 1024;  // batch items filtered / sorted per step
+constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node capacity
 
 struct Args {
   const uint64_t *tab_e;
@@ -68,225 +51,33 @@ struct Args {
   const uint64_t *term_key;
   const uint32_t *term_slot;
   const uint32_t *term_count;
-  uint64_t *surv_e, *surv_key;
-  uint32_t *surv_slot, *surv_cnt;
-  uint32_t *hist;
-  Entry *keep, *ties;
-  uint64_t *set_key[2];
-  uint32_t *set_node[2];
-  uint64_t *set_e[2];
-  double *set_p[2];
-  uint64_t *hkey;
-  uint32_t *hnode;
-  uint32_t hmask;
-  State *st;
+  uint64_t *set_key;  // [nodes * cap]
+  uint64_t *set_e;    // [nodes * cap * Z] frozen per-zone energy
+  double *set_p;      // [nodes * cap * Z] frozen per-zone power
+  uint32_t *size;     // [nodes]
   uint32_t *err;
 };
 
-// Monotone 16-bit key: 6-bit exponent, 10-bit mantissa (e = 0 and 1 share 0).
-__device__ __forceinline__ uint32_t bin_of(uint64_t e) {
-  if (e == 0) return 0;
-  const uint32_t msb = 63u - static_cast<uint32_t>(__clzll(static_cast<long long>(e)));
-  const uint32_t mant = msb >= 10 ? static_cast<uint32_t>(e >> (msb - 10)) & 1023u
-                                  : static_cast<uint32_t>(e << (10 - msb)) & 1023u;
-  return msb * 1024u + mant;
-}
-
-__device__ __forceinline__ uint32_t hbucket(uint64_t key, uint32_t node, uint32_t hmask) {
-  uint64_t x = key ^ (static_cast<uint64_t>(node) * 0x9E3779B97F4A7C15ull);
-  x ^= x >> 31;
-  x *= 0xbf58476d1ce4e5b9ull;
-  x ^= x >> 29;
-  return static_cast<uint32_t>(x) & hmask;
-}
-
-__device__ bool tracked(const Args &a, uint64_t key, uint32_t node) {
-  uint32_t b = hbucket(key, node, a.hmask);
-  for (uint32_t p = 0; p <= a.hmask; ++p, b = (b + 1) & a.hmask) {
-    const uint64_t k = a.hkey[b];
-    if (k == KACC_KEY_EMPTY) return false;
-    if (k == key && a.hnode[b] == node) return true;
-  }
-  return false;
-}
-
-template <int T>
-__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t *s_wave, uint32_t &total) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) s_wave[wave] = x;
-  __syncthreads();
-  uint32_t base = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < T / 64; ++w) {
-    const uint32_t t = s_wave[w];
-    if (w < wave) base += t;
-    tot += t;
-  }
-  __syncthreads();
-  total = tot;
-  return base + x - v;
-}
-
-// ---- filter: one workgroup per node (+ one for the tracked items) ------------------
-__global__ __launch_bounds__(kThreads) void filter_kernel(const Args a) {
-  __shared__ uint32_t s_wave[kThreads / 64];
-  const uint32_t tid = threadIdx.x;
-  const State st = *a.st;
-  if (blockIdx.x == a.n_nodes) {  // tracked items stay candidates of the selection
-    const uint32_t cur = st.parity & 1u;
-    for (uint32_t i = tid; i < st.size; i += kThreads)
-      atomicAdd(&a.hist[bin_of(a.set_e[cur][static_cast<uint64_t>(i) * a.Z + a.z0])], 1u);
-    return;
-  }
-  const uint32_t n = blockIdx.x;
-  const uint32_t base = a.slot_off[n];
-  const uint32_t c = min(a.term_count[n], a.slot_off[n + 1] - base);
-  const bool full = a.max_size > 0 && st.size >= static_cast<uint64_t>(a.max_size);
-  uint32_t done = 0;
-  for (uint32_t i0 = 0; i0 < c; i0 += kThreads) {
-    const uint32_t i = i0 + tid;
-    bool pass = false;
-    uint64_t e = 0, key = 0;
-    uint32_t slot = 0;
-    if (i < c) {
-      slot = a.term_slot[base + i];
-      key = a.term_key[base + i];
-      e = a.tab_e[static_cast<uint64_t>(slot) * a.Z + a.z0];
-      pass = e >= a.min_e                       // terminated_resource_tracker.go:102
-             && !(full && e <= st.min_full)     // :124 needs a strictly higher energy
-             && !tracked(a, key, n);            // :90
-    }
-    uint32_t tot;
-    const uint32_t pos = done + block_scan<kThreads>(pass ? 1u : 0u, s_wave, tot);
-    if (pass) {
-      a.surv_e[base + pos] = e;
-      a.surv_key[base + pos] = key;
-      a.surv_slot[base + pos] = slot;
-      atomicAdd(&a.hist[bin_of(e)], 1u);
-    }
-    done += tot;
-  }
-  if (tid == 0) a.surv_cnt[n] = done;
-}
-
-// ---- pick: the boundary bin of the max_size-th best item --------------------------
-__global__ __launch_bounds__(kFinThreads) void pick_kernel(const Args a) {
-  __shared__ uint32_t s_sum[kFinThreads];
-  constexpr uint32_t kPer = kBins / kFinThreads;  // 64 bins per thread
-  const uint32_t tid = threadIdx.x;
-  uint32_t s = 0;
-  for (uint32_t j = 0; j < kPer; ++j) s += a.hist[tid * kPer + j];
-  s_sum[tid] = s;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t tot = 0;
-    for (uint32_t t = 0; t < kFinThreads; ++t) tot += s_sum[t];
-    State *st = a.st;
-    st->keep_n = 0;
-    st->tie_n = 0;
-    st->need = 0;
-    st->pick_bin = 0;
-    if (a.max_size < 0 || tot <= static_cast<uint64_t>(a.max_size)) {
-      st->keep_all = 1;
-    } else {
-      st->keep_all = 0;
-      const uint32_t K = static_cast<uint32_t>(a.max_size);
-      uint32_t above = 0, t = kFinThreads;
-      while (t > 0 && above + s_sum[t - 1] < K) above += s_sum[--t];
-      // thread t - 1 holds the boundary: walk its bins from the top
-      const uint32_t tb = t - 1;
-      uint32_t b = tb * kPer + kPer;
-      while (b > tb * kPer) {
-        const uint32_t h = a.hist[b - 1];
-        if (above + h >= K) break;
-        above += h;
-        --b;
-      }
-      st->pick_bin = b - 1;
-      st->need = K - above;
-    }
-  }
-}
-
-// ---- collect: above the boundary -> keep, in it -> ties ----------------------------
-__device__ __forceinline__ void route(const Args &a, const State &st, const Entry &x, uint32_t lim) {
-  const uint32_t b = bin_of(x.e);
-  if (st.keep_all || b > st.pick_bin) {
-    const uint32_t i = atomicAdd(&a.st->keep_n, 1u);
-    if (i < lim) a.keep[i] = x;
-    else atomicOr(a.err, kErrCap);
-  } else if (b == st.pick_bin) {
-    const uint32_t i = atomicAdd(&a.st->tie_n, 1u);
-    if (i < kSortCap) a.ties[i] = x;
-    else atomicOr(a.err, kErrTie);
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void collect_kernel(const Args a) {
-  const State st = *a.st;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lim = a.cap;
-  if (blockIdx.x == a.n_nodes) {
-    const uint32_t cur = st.parity & 1u;
-    for (uint32_t i = tid; i < st.size; i += kThreads) {
-      Entry x;
-      x.e = a.set_e[cur][static_cast<uint64_t>(i) * a.Z + a.z0];
-      x.key = a.set_key[cur][i];
-      x.node = a.set_node[cur][i];
-      x.ref = i;
-      x.old = 1;
-      x.pad = 0;
-      route(a, st, x, lim);
-    }
-    return;
-  }
-  const uint32_t n = blockIdx.x;
-  const uint32_t base = a.slot_off[n];
-  const uint32_t c = a.surv_cnt[n];
-  for (uint32_t i = tid; i < c; i += kThreads) {
-    Entry x;
-    x.e = a.surv_e[base + i];
-    x.key = a.surv_key[base + i];
-    x.node = n;
-    x.ref = a.surv_slot[base + i];
-    x.old = 0;
-    x.pad = 0;
-    route(a, st, x, lim);
-  }
-}
-
-// ---- finalize: exact order in LDS, the new set, dedupe hash -----------------------
-// Sort keys: k1 = ~energy (ascending = energy desc), k2 = batch flag, node, ref.
-__device__ __forceinline__ void sort_keys(const Entry &x, uint64_t &k1, uint64_t &k2) {
-  k1 = ~x.e;
-  k2 = (x.old ? 0ull : kOld) | (static_cast<uint64_t>(x.node) << 31) | (x.ref & 0x7fffffffu);
-}
-
-// Bitonic sort of n (<= kSortCap) (k1, k2, idx) triples in LDS, ascending.
-__device__ void bitonic(uint64_t *k1, uint64_t *k2, uint16_t *ix, uint32_t n) {
+// Bitonic sort of n (<= kChunk) (k1, k2, idx) triples in LDS, ascending.
+__device__ void bitonic(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t n) {
   uint32_t m = 1;
   while (m < n) m <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < m; i += kFinThreads) {
+  for (uint32_t i = n + threadIdx.x; i < m; i += kThreads) {
     k1[i] = ~0ull;
-    k2[i] = ~0ull;
+    k2[i] = ~0u;
     ix[i] = 0xffffu;
   }
   __syncthreads();
   for (uint32_t size = 2; size <= m; size <<= 1) {
     for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < m; i += kFinThreads) {
+      for (uint32_t i = threadIdx.x; i < m; i += kThreads) {
         const uint32_t j = i ^ stride;
         if (j <= i) continue;
         const bool up = (i & size) == 0;
         const bool gt = k1[i] > k1[j] || (k1[i] == k1[j] && k2[i] > k2[j]);
         if (gt == up) {
-          const uint64_t t1 = k1[i], t2 = k2[i];
+          const uint64_t t1 = k1[i];
+          const uint32_t t2 = k2[i];
           const uint16_t t3 = ix[i];
           k1[i] = k1[j];
           k2[i] = k2[j];
@@ -301,70 +92,170 @@ __device__ void bitonic(uint64_t *k1, uint64_t *k2, uint16_t *ix, uint32_t n) {
   }
 }
 
-__global__ __launch_bounds__(kFinThreads) void finalize_kernel(const Args a) {
-  __shared__ uint64_t s_k1[kSortCap], s_k2[kSortCap];
-  __shared__ uint16_t s_ix[kSortCap];
-  const uint32_t tid = threadIdx.x;
-  const State st = *a.st;
-  const uint32_t cur = st.parity & 1u, nxt = cur ^ 1u;
-  uint32_t n_keep = min(st.keep_n, a.cap);
-  // 1: the first `need` ties in exact order join the keep list
-  if (!st.keep_all && st.need > 0) {
-    const uint32_t nt = min(st.tie_n, kSortCap);
-    for (uint32_t i = tid; i < nt; i += kFinThreads) {
-      sort_keys(a.ties[i], s_k1[i], s_k2[i]);
-      s_ix[i] = static_cast<uint16_t>(i);
-    }
-    __syncthreads();
-    bitonic(s_k1, s_k2, s_ix, nt);
-    const uint32_t take = min(st.need, nt);
-    for (uint32_t i = tid; i < take; i += kFinThreads)
-      if (n_keep + i < a.cap) a.keep[n_keep + i] = a.ties[s_ix[i]];
-    n_keep = min(n_keep + take, a.cap);
-    __syncthreads();  // keep entries visible to the whole workgroup
-  }
-  // 2: the new set, sorted when it fits LDS (always for max_size > 0)
-  const bool sorted = n_keep <= kSortCap;
-  if (sorted) {
-    for (uint32_t i = tid; i < n_keep; i += kFinThreads) {
-      sort_keys(a.keep[i], s_k1[i], s_k2[i]);
-      s_ix[i] = static_cast<uint16_t>(i);
-    }
-    __syncthreads();
-    bitonic(s_k1, s_k2, s_ix, n_keep);
-  }
-  for (uint32_t i = tid; i < n_keep; i += kFinThreads) {
-    const Entry x = a.keep[sorted ? s_ix[i] : i];
-    a.set_key[nxt][i] = x.key;
-    a.set_node[nxt][i] = x.node;
-    for (uint32_t z = 0; z < a.Z; ++z) {  // frozen copy: Add(prev.Clone())
-      const uint64_t src = static_cast<uint64_t>(x.ref) * a.Z + z;
-      a.set_e[nxt][static_cast<uint64_t>(i) * a.Z + z] = x.old ? a.set_e[cur][src] : a.tab_e[src];
-      a.set_p[nxt][static_cast<uint64_t>(i) * a.Z + z] = x.old ? a.set_p[cur][src] : a.tab_p[src];
-    }
-  }
-  // 3: dedupe hash of the new set
-  for (uint32_t b = tid; b <= a.hmask; b += kFinThreads) a.hkey[b] = KACC_KEY_EMPTY;
-  __syncthreads();
-  for (uint32_t i = tid; i < n_keep; i += kFinThreads) {
-    const Entry x = a.keep[sorted ? s_ix[i] : i];
-    uint32_t b = hbucket(x.key, x.node, a.hmask);
-    for (uint32_t p = 0; p <= a.hmask; ++p, b = (b + 1) & a.hmask) {
-      if (atomicCAS(reinterpret_cast<unsigned long long *>(a.hkey + b), KACC_KEY_EMPTY,
-                    static_cast<unsigned long long>(x.key)) == KACC_KEY_EMPTY) {
-        a.hnode[b] = x.node;
-        break;
+__global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
+  __shared__ uint64_t s_key[kChunk];    // survivors (filter order), then sort keys ~energy
+  __shared__ uint64_t s_e[kChunk];
+  __shared__ uint32_t s_slot[kChunk];
+  __shared__ uint64_t s_k1[kChunk];
+  __shared__ uint32_t s_k2[kChunk];
+  __shared__ uint16_t s_ix[kChunk];
+  __shared__ uint32_t s_rank[kChunk];
+  __shared__ uint64_t s_tk[kChunk];     // a block of tracked keys (duplicate check)
+  __shared__ uint32_t s_cnt;
+  const uint32_t n = blockIdx.x, tid = threadIdx.x;
+  const uint32_t Z = a.Z, z0 = a.z0, cap = a.cap;
+  const uint64_t base = static_cast<uint64_t>(n) * cap;
+  const uint32_t b0 = a.slot_off[n];
+  const uint32_t c = min(a.term_count[n], a.slot_off[n + 1] - b0);
+  const uint32_t K = a.max_size > 0 ? static_cast<uint32_t>(a.max_size) : cap;
+  uint32_t size = min(a.size[n], cap);
+  for (uint32_t c0 = 0; c0 < c; c0 += kChunk) {
+    const uint32_t m0 = min(kChunk, c - c0);
+    const bool full = a.max_size > 0 && size >= K;
+    const uint64_t min_full = full ? a.set_e[(base + size - 1) * Z + z0] : 0ull;
+    // ---- filter (terminated_resource_tracker.go:90-124) ----------------------------
+    uint64_t key[kChunk / kThreads], e[kChunk / kThreads];
+    uint32_t slot[kChunk / kThreads];
+    bool pass[kChunk / kThreads];
+#pragma unroll
+    for (uint32_t u = 0; u < kChunk / kThreads; ++u) {
+      const uint32_t i = tid + u * kThreads;
+      pass[u] = false;
+      key[u] = e[u] = 0;
+      slot[u] = 0;
+      if (i < m0) {
+        slot[u] = a.term_slot[b0 + c0 + i];
+        key[u] = a.term_key[b0 + c0 + i];
+        e[u] = a.tab_e[static_cast<uint64_t>(slot[u]) * Z + z0];
+        pass[u] = e[u] >= a.min_e && !(full && e[u] <= min_full);  // :102, :124
       }
     }
+    for (uint32_t t0 = 0; t0 < size; t0 += kChunk) {  // :90 already tracked
+      const uint32_t tn = min(kChunk, size - t0);
+      __syncthreads();
+      for (uint32_t t = tid; t < tn; t += kThreads) s_tk[t] = a.set_key[base + t0 + t];
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < kChunk / kThreads; ++u)
+        if (pass[u])
+          for (uint32_t t = 0; t < tn; ++t)
+            if (s_tk[t] == key[u]) pass[u] = false;
+    }
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < kChunk / kThreads; ++u) {  // compaction order is irrelevant: sorted next
+      if (!pass[u]) continue;
+      const uint32_t j = atomicAdd(&s_cnt, 1u);
+      s_key[j] = key[u];
+      s_e[j] = e[u];
+      s_slot[j] = slot[u];
+    }
+    __syncthreads();
+    const uint32_t m = s_cnt;
+    if (m == 0) continue;  // block-uniform
+    // ---- sort survivors: energy desc, then slot (the batch order) -------------------
+    for (uint32_t j = tid; j < m; j += kThreads) {
+      s_k1[j] = ~s_e[j];
+      s_k2[j] = s_slot[j];
+      s_ix[j] = static_cast<uint16_t>(j);
+    }
+    __syncthreads();
+    bitonic(s_k1, s_k2, s_ix, m);
+    // ---- ranks (before anything moves) ----------------------------------------------
+    uint32_t new_size = size + m;
+    if (a.max_size > 0) {
+      new_size = min(new_size, K);
+    } else if (new_size > cap) {  // unlimited: per-node capacity exceeded
+      if (tid == 0) atomicOr(a.err, kErrCap);
+      new_size = cap;
+    }
+    for (uint32_t j = tid; j < m; j += kThreads) {  // survivor j: + #tracked with e >= its e
+      const uint64_t ej = ~s_k1[j];
+      uint32_t lo = 0, hi = size;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.set_e[(base + mid) * Z + z0] >= ej)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      s_rank[j] = j + lo;
+    }
+    __syncthreads();
+    // ---- tracked items move to later ranks: blocks from the end ----------------------
+    for (int64_t blk = static_cast<int64_t>(size) - 1 - ((static_cast<int64_t>(size) - 1) % kThreads); blk >= 0;
+         blk -= kThreads) {
+      const uint32_t i = static_cast<uint32_t>(blk) + tid;
+      const bool have = i < size;
+      uint32_t r = 0;
+      uint64_t k = 0;
+      uint64_t E[KACC_MAX_ZONES];
+      double P[KACC_MAX_ZONES];
+      if (have) {  // i + #survivors with a strictly higher energy (ties: tracked first)
+        const uint64_t ei = a.set_e[(base + i) * Z + z0];
+        uint32_t lo = 0, hi = m;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (~s_k1[mid] > ei)
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        r = i + lo;
+        k = a.set_key[base + i];
+        for (uint32_t z = 0; z < Z; ++z) {
+          E[z] = a.set_e[(base + i) * Z + z];
+          P[z] = a.set_p[(base + i) * Z + z];
+        }
+      }
+      __syncthreads();
+      if (have && r != i && r < new_size) {
+        a.set_key[base + r] = k;
+        for (uint32_t z = 0; z < Z; ++z) {
+          a.set_e[(base + r) * Z + z] = E[z];
+          a.set_p[(base + r) * Z + z] = P[z];
+        }
+      }
+      __syncthreads();
+    }
+    // ---- survivors take their ranks (frozen copies: Add(prev.Clone())) -------------
+    for (uint32_t j = tid; j < m; j += kThreads) {
+      const uint32_t r = s_rank[j];
+      if (r >= new_size) continue;
+      const uint32_t src = s_ix[j];
+      const uint64_t sl = s_slot[src];
+      a.set_key[base + r] = s_key[src];
+      for (uint32_t z = 0; z < Z; ++z) {
+        a.set_e[(base + r) * Z + z] = a.tab_e[sl * Z + z];
+        a.set_p[(base + r) * Z + z] = a.tab_p[sl * Z + z];
+      }
+    }
+    size = new_size;
+    __syncthreads();
   }
-  __syncthreads();
-  if (tid == 0) {
-    State *s = a.st;
-    s->size = n_keep;
-    s->parity = nxt;
-    const bool full = a.max_size > 0 && n_keep >= static_cast<uint64_t>(a.max_size);
-    s->min_full = full ? a.set_e[nxt][static_cast<uint64_t>(n_keep - 1) * a.Z + a.z0] : 0ull;
+  if (tid == 0) a.size[n] = size;
+}
+
+// Items(): the nodes' sets packed node by node (offsets from the host).
+__global__ __launch_bounds__(kThreads) void pack_kernel(const Args a, const uint64_t *off, uint64_t *out_key,
+                                                        uint32_t *out_node, uint64_t *out_e, double *out_p) {
+  const uint32_t n = blockIdx.x;
+  const uint64_t o = off[n], cnt = off[n + 1] - o, base = static_cast<uint64_t>(n) * a.cap;
+  for (uint64_t i = threadIdx.x; i < cnt; i += kThreads) {
+    out_key[o + i] = a.set_key[base + i];
+    out_node[o + i] = n;
+    for (uint32_t z = 0; z < a.Z; ++z) {
+      out_e[(o + i) * a.Z + z] = a.set_e[(base + i) * a.Z + z];
+      out_p[(o + i) * a.Z + z] = a.set_p[(base + i) * a.Z + z];
+    }
   }
+}
+
+// Clear(): every node, or the nodes with mask[n] != 0 (process.go:80-84).
+__global__ __launch_bounds__(kThreads) void clear_kernel(uint32_t *size, uint32_t n_nodes, const uint32_t *mask) {
+  const uint32_t n = blockIdx.x * kThreads + threadIdx.x;
+  if (n < n_nodes && (!mask || mask[n])) size[n] = 0;
 }
 
 }  // namespace trk
@@ -378,21 +269,12 @@ struct kacc_tracker {
   int device = 0;
   kacc_kind kind = KACC_KIND_PROC;
   int64_t max_size = 0;
-  uint32_t cap = 0, zone = 0, Z = 0, hmask = 0;
+  uint32_t cap = 0, zone = 0, Z = 0, nodes = 0;
   uint64_t min_e = 0;
-  kacc::trk::State *d_state = nullptr;
-  uint64_t *d_set_key[2] = {};
-  uint32_t *d_set_node[2] = {};
-  uint64_t *d_set_e[2] = {};
-  double *d_set_p[2] = {};
-  uint64_t *d_hkey = nullptr;
-  uint32_t *d_hnode = nullptr;
-  uint32_t *d_hist = nullptr;
-  kacc::trk::Entry *d_keep = nullptr, *d_ties = nullptr;
-  // per-node survivors, sized like the slot map that feeds the tracker
-  uint32_t surv_slots = 0, surv_nodes = 0;
-  uint64_t *d_surv_e = nullptr, *d_surv_key = nullptr;
-  uint32_t *d_surv_slot = nullptr, *d_surv_cnt = nullptr;
+  uint64_t *d_set_key = nullptr;
+  uint64_t *d_set_e = nullptr;
+  double *d_set_p = nullptr;
+  uint32_t *d_size = nullptr;
 };
 
 namespace {
@@ -406,14 +288,21 @@ void kind_tables(const kacc_ctx *ctx, kacc_kind k, const uint64_t **e, const dou
   *p = static_cast<const double *>(ctx->tables[base + 1]);
 }
 
-void free_surv(kacc_tracker *t) {
-  (void)hipFree(t->d_surv_e);
-  (void)hipFree(t->d_surv_key);
-  (void)hipFree(t->d_surv_slot);
-  (void)hipFree(t->d_surv_cnt);
-  t->d_surv_e = t->d_surv_key = nullptr;
-  t->d_surv_slot = t->d_surv_cnt = nullptr;
-  t->surv_slots = t->surv_nodes = 0;
+kacc::trk::Args tracker_args(const kacc_tracker *t) {
+  kacc::trk::Args a{};
+  kind_tables(t->ctx, t->kind, &a.tab_e, &a.tab_p);
+  a.min_e = t->min_e;
+  a.max_size = t->max_size;
+  a.Z = t->Z;
+  a.z0 = t->zone;
+  a.cap = t->cap;
+  a.n_nodes = t->nodes;
+  a.set_key = t->d_set_key;
+  a.set_e = t->d_set_e;
+  a.set_p = t->d_set_p;
+  a.size = t->d_size;
+  a.err = t->ctx->d_err;
+  return a;
 }
 
 }  // namespace
@@ -439,32 +328,23 @@ int kacc_tracker_create(kacc_ctx *ctx, kacc_kind kind, int64_t max_size, uint32_
   t->cap = std::max<uint32_t>(cap, 1);
   t->zone = zone;
   t->Z = ctx->cfg.zones;
+  t->nodes = static_cast<uint32_t>(std::max<uint64_t>(ctx->cfg.nodes, 1));
   t->min_e = min_energy;
-  uint32_t hb = 64;
-  while (hb < 2 * t->cap) hb <<= 1;
-  t->hmask = hb - 1;
-  const size_t c = t->cap, Z = t->Z;
+  const size_t items = static_cast<size_t>(t->nodes) * t->cap, Z = t->Z;
   hipError_t e = hipSuccess;
   auto A = [&](void **p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, std::max<size_t>(bytes, 8));
   };
-  A(reinterpret_cast<void **>(&t->d_state), sizeof(kacc::trk::State));
-  for (int p = 0; p < 2; ++p) {
-    A(reinterpret_cast<void **>(&t->d_set_key[p]), 8 * c);
-    A(reinterpret_cast<void **>(&t->d_set_node[p]), 4 * c);
-    A(reinterpret_cast<void **>(&t->d_set_e[p]), 8 * c * Z);
-    A(reinterpret_cast<void **>(&t->d_set_p[p]), 8 * c * Z);
-  }
-  A(reinterpret_cast<void **>(&t->d_hkey), 8ull * hb);
-  A(reinterpret_cast<void **>(&t->d_hnode), 4ull * hb);
-  A(reinterpret_cast<void **>(&t->d_hist), 4ull * kacc::trk::kBins);
-  A(reinterpret_cast<void **>(&t->d_keep), sizeof(kacc::trk::Entry) * (c + kacc::trk::kSortCap));
-  A(reinterpret_cast<void **>(&t->d_ties), sizeof(kacc::trk::Entry) * kacc::trk::kSortCap);
+  A(reinterpret_cast<void **>(&t->d_set_key), 8 * items);
+  A(reinterpret_cast<void **>(&t->d_set_e), 8 * items * Z);
+  A(reinterpret_cast<void **>(&t->d_set_p), 8 * items * Z);
+  A(reinterpret_cast<void **>(&t->d_size), 4ull * t->nodes);
   if (e != hipSuccess) {
     kacc_tracker_destroy(t);
-    return kacc_fail(ctx, KACC_ENOMEM, "tracker allocation: %s", hipGetErrorString(e));
+    return kacc_fail(ctx, KACC_ENOMEM, "tracker allocation (%u nodes x %u): %s", t->nodes, t->cap,
+                     hipGetErrorString(e));
   }
-  const int rc = kacc_tracker_clear(t, nullptr);
+  const int rc = kacc_tracker_clear(t, nullptr, nullptr);
   if (rc != KACC_OK) {
     kacc_tracker_destroy(t);
     return rc;
@@ -478,29 +358,26 @@ void kacc_tracker_destroy(kacc_tracker *t) {
   if (!t) return;
   (void)hipSetDevice(t->device);
   (void)hipDeviceSynchronize();
-  (void)hipFree(t->d_state);
-  for (int p = 0; p < 2; ++p) {
-    (void)hipFree(t->d_set_key[p]);
-    (void)hipFree(t->d_set_node[p]);
-    (void)hipFree(t->d_set_e[p]);
-    (void)hipFree(t->d_set_p[p]);
-  }
-  (void)hipFree(t->d_hkey);
-  (void)hipFree(t->d_hnode);
-  (void)hipFree(t->d_hist);
-  (void)hipFree(t->d_keep);
-  (void)hipFree(t->d_ties);
-  free_surv(t);
+  (void)hipFree(t->d_set_key);
+  (void)hipFree(t->d_set_e);
+  (void)hipFree(t->d_set_p);
+  (void)hipFree(t->d_size);
   delete t;
 }
 
-int kacc_tracker_clear(kacc_tracker *t, void *stream) {
+int kacc_tracker_clear(kacc_tracker *t, const uint32_t *node_mask, void *stream) {
   if (!t) return KACC_EINVAL;
   kacc_ctx *ctx = t->ctx;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  KACC_HIP(ctx, hipMemsetAsync(t->d_state, 0, sizeof(kacc::trk::State), st));
-  KACC_HIP(ctx, hipMemsetAsync(t->d_hkey, 0xff, 8ull * (t->hmask + 1), st));
+  if (!node_mask) {
+    KACC_HIP(ctx, hipMemsetAsync(t->d_size, 0, 4ull * t->nodes, st));
+    return KACC_OK;
+  }
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(kacc::trk::clear_kernel, dim3((t->nodes + kacc::trk::kThreads - 1) / kacc::trk::kThreads),
+                     dim3(kacc::trk::kThreads), 0, st, t->d_size, t->nodes, node_mask);
+  KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
 
@@ -511,61 +388,19 @@ int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *ter
   if (m->ctx != ctx || m->kind != t->kind)
     return kacc_fail(ctx, KACC_EINVAL, "tracker and slot map differ in context or kind");
   if (t->max_size == 0 || m->n_nodes == 0) return KACC_OK;  // tracker.go:82 disabled
+  if (m->n_nodes > t->nodes)
+    return kacc_fail(ctx, KACC_EINVAL, "slot map has %u nodes, the tracker %u", m->n_nodes, t->nodes);
   if (!term_key || !term_slot || !term_count) return kacc_fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  if (m->total_slots > t->surv_slots || m->n_nodes > t->surv_nodes) {
-    KACC_HIP(ctx, hipDeviceSynchronize());
-    free_surv(t);
-    const size_t ns = std::max<uint32_t>(m->total_slots, 1), nn = m->n_nodes;
-    hipError_t e = hipMalloc(&t->d_surv_e, 8 * ns);
-    if (e == hipSuccess) e = hipMalloc(&t->d_surv_key, 8 * ns);
-    if (e == hipSuccess) e = hipMalloc(&t->d_surv_slot, 4 * ns);
-    if (e == hipSuccess) e = hipMalloc(&t->d_surv_cnt, 4 * nn);
-    if (e != hipSuccess) {
-      free_surv(t);
-      return kacc_fail(ctx, KACC_ENOMEM, "tracker scratch: %s", hipGetErrorString(e));
-    }
-    t->surv_slots = static_cast<uint32_t>(ns);
-    t->surv_nodes = m->n_nodes;
-  }
-  kacc::trk::Args a{};
-  kind_tables(ctx, t->kind, &a.tab_e, &a.tab_p);
-  a.min_e = t->min_e;
-  a.max_size = t->max_size;
-  a.Z = t->Z;
-  a.z0 = t->zone;
-  a.cap = t->cap;
+  kacc::trk::Args a = tracker_args(t);
   a.n_nodes = m->n_nodes;
   a.slot_off = m->d_slot_off;
   a.term_key = term_key;
   a.term_slot = term_slot;
   a.term_count = term_count;
-  a.surv_e = t->d_surv_e;
-  a.surv_key = t->d_surv_key;
-  a.surv_slot = t->d_surv_slot;
-  a.surv_cnt = t->d_surv_cnt;
-  a.hist = t->d_hist;
-  a.keep = t->d_keep;
-  a.ties = t->d_ties;
-  for (int p = 0; p < 2; ++p) {
-    a.set_key[p] = t->d_set_key[p];
-    a.set_node[p] = t->d_set_node[p];
-    a.set_e[p] = t->d_set_e[p];
-    a.set_p[p] = t->d_set_p[p];
-  }
-  a.hkey = t->d_hkey;
-  a.hnode = t->d_hnode;
-  a.hmask = t->hmask;
-  a.st = t->d_state;
-  a.err = ctx->d_err;
-  using namespace kacc::trk;
-  KACC_HIP(ctx, hipMemsetAsync(t->d_hist, 0, 4ull * kBins, st));
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  hipLaunchKernelGGL(filter_kernel, dim3(m->n_nodes + 1), dim3(kThreads), 0, st, a);
-  hipLaunchKernelGGL(pick_kernel, dim3(1), dim3(kFinThreads), 0, st, a);
-  hipLaunchKernelGGL(collect_kernel, dim3(m->n_nodes + 1), dim3(kThreads), 0, st, a);
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(kFinThreads), 0, st, a);
+  hipLaunchKernelGGL(kacc::trk::node_add_kernel, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0, st, a);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
@@ -576,16 +411,36 @@ int kacc_tracker_items(kacc_tracker *t, uint32_t *count, uint64_t *key, uint32_t
   kacc_ctx *ctx = t->ctx;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipDeviceSynchronize());  // adds may run on any stream
-  kacc::trk::State s{};
-  KACC_HIP(ctx, hipMemcpy(&s, t->d_state, sizeof(s), hipMemcpyDeviceToHost));
-  *count = s.size;
-  const uint32_t cur = s.parity & 1u;
-  const size_t n = s.size, Z = t->Z;
-  if (n == 0) return KACC_OK;
-  if (key) KACC_HIP(ctx, hipMemcpy(key, t->d_set_key[cur], 8 * n, hipMemcpyDeviceToHost));
-  if (node) KACC_HIP(ctx, hipMemcpy(node, t->d_set_node[cur], 4 * n, hipMemcpyDeviceToHost));
-  if (energy) KACC_HIP(ctx, hipMemcpy(energy, t->d_set_e[cur], 8 * n * Z, hipMemcpyDeviceToHost));
-  if (power) KACC_HIP(ctx, hipMemcpy(power, t->d_set_p[cur], 8 * n * Z, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> sizes(t->nodes);
+  KACC_HIP(ctx, hipMemcpy(sizes.data(), t->d_size, 4ull * t->nodes, hipMemcpyDeviceToHost));
+  std::vector<uint64_t> off(t->nodes + 1, 0);
+  for (uint32_t n = 0; n < t->nodes; ++n) off[n + 1] = off[n] + std::min(sizes[n], t->cap);
+  const uint64_t total = off[t->nodes];
+  if (total > 0xffffffffull) return kacc_fail(ctx, KACC_ERANGE, "tracked items exceed 2^32");
+  *count = static_cast<uint32_t>(total);
+  if (total == 0 || (!key && !node && !energy && !power)) return KACC_OK;
+  const size_t Z = t->Z;
+  void *d_off = nullptr, *d_key = nullptr, *d_node = nullptr, *d_e = nullptr, *d_p = nullptr;
+  hipError_t e = hipMalloc(&d_off, 8 * off.size());
+  if (e == hipSuccess) e = hipMalloc(&d_key, 8 * total);
+  if (e == hipSuccess) e = hipMalloc(&d_node, 4 * total);
+  if (e == hipSuccess) e = hipMalloc(&d_e, 8 * total * Z);
+  if (e == hipSuccess) e = hipMalloc(&d_p, 8 * total * Z);
+  if (e == hipSuccess) e = hipMemcpy(d_off, off.data(), 8 * off.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(kacc::trk::pack_kernel, dim3(t->nodes), dim3(kacc::trk::kThreads), 0, nullptr,
+                       tracker_args(t), static_cast<const uint64_t *>(d_off), static_cast<uint64_t *>(d_key),
+                       static_cast<uint32_t *>(d_node), static_cast<uint64_t *>(d_e), static_cast<double *>(d_p));
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && key) e = hipMemcpy(key, d_key, 8 * total, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && node) e = hipMemcpy(node, d_node, 4 * total, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && energy) e = hipMemcpy(energy, d_e, 8 * total * Z, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && power) e = hipMemcpy(power, d_p, 8 * total * Z, hipMemcpyDeviceToHost);
+  for (void *p : {d_off, d_key, d_node, d_e, d_p})
+    if (p) (void)hipFree(p);
+  if (e != hipSuccess) return kacc_fail(ctx, KACC_EHIP, "tracker items: %s", hipGetErrorString(e));
   return KACC_OK;
 }
 

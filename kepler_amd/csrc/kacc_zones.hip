@@ -11,10 +11,10 @@
 // MaxUint64 (:55-67).  The monitor reads every zone of a node even after one
 // fails and then fails the node's interval (monitor/node.go:37-44).
 //
-// One thread per (node, zone); S sub-zones each, stored [node][zone][socket]
-// so a thread's readings are contiguous.  The outputs are the interval
-// batch's zone_energy / zone_max; failures OR KACC_NODE_READ_ERROR into the
-// batch's node_status.
+// One thread per node, its zones in order; S sub-zones each, stored
+// [node][zone][socket].  The outputs are the interval batch's zone_energy /
+// zone_max and the KACC_NODE_READ_ERROR bit of the batch's node_status, set
+// when one of the node's zones failed and cleared otherwise (other bits kept).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,34 +41,49 @@ struct Args {
   uint32_t *node_status;
 };
 
+// One thread per node: its Z aggregated zones in order; the node's read-error
+// bit is written (set or cleared) every call, so a node fails only the
+// intervals whose reads failed (monitor/node.go:37-44: every zone is read,
+// then the interval fails).
 __global__ __launch_bounds__(kThreads) void zone_agg_kernel(const Args a) {
-  const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
-  if (i >= a.n) return;
-  const uint64_t base = static_cast<uint64_t>(i) * a.S;
-  const uint64_t amax = a.agg_max[i];
-  a.out_max[i] = amax;
-  uint64_t total = 0;
-  for (uint32_t s = 0; s < a.S; ++s) {
-    const uint64_t k = base + s;
-    if (a.sub_status && a.sub_status[k]) {  // energy_zone.go:104-108
+  const uint32_t node = blockIdx.x * kThreads + threadIdx.x;
+  if (node >= a.n / a.Z) return;
+  bool failed = false;
+  for (uint32_t z = 0; z < a.Z; ++z) {
+    const uint32_t i = node * a.Z + z;
+    const uint64_t base = static_cast<uint64_t>(i) * a.S;
+    const uint64_t amax = a.agg_max[i];
+    a.out_max[i] = amax;
+    uint64_t total = 0;
+    bool ok = true;
+    for (uint32_t s = 0; s < a.S && ok; ++s) {
+      const uint64_t k = base + s;
+      if (a.sub_status && a.sub_status[k]) {  // energy_zone.go:104-108: return at once
+        ok = false;
+        break;
+      }
+      const uint64_t r = a.readings[k];
+      if (a.seen[k]) {
+        const uint64_t prev = a.last[k], mx = a.sub_max[k];
+        total += r >= prev ? r - prev : mx > 0 ? (mx - prev) + r : r - prev;  // :115-128
+      } else {
+        total += r;  // :130-131 first reading
+      }
+      a.last[k] = r;
+      a.seen[k] = 1u;
+    }
+    if (!ok) {
       a.out_energy[i] = 0;
-      atomicOr(a.node_status + i / a.Z, KACC_NODE_READ_ERROR);
-      return;
+      failed = true;
+      continue;
     }
-    const uint64_t r = a.readings[k];
-    if (a.seen[k]) {
-      const uint64_t prev = a.last[k], mx = a.sub_max[k];
-      total += r >= prev ? r - prev : mx > 0 ? (mx - prev) + r : r - prev;  // :115-128
-    } else {
-      total += r;  // :130-131 first reading
-    }
-    a.last[k] = r;
-    a.seen[k] = 1u;
+    uint64_t cur = a.current[i] + total;  // :136
+    if (amax > 0) cur %= amax;            // :139-145
+    a.current[i] = cur;
+    a.out_energy[i] = cur;
   }
-  uint64_t cur = a.current[i] + total;  // :136
-  if (amax > 0) cur %= amax;            // :139-145
-  a.current[i] = cur;
-  a.out_energy[i] = cur;
+  const uint32_t st = a.node_status[node];
+  a.node_status[node] = failed ? (st | KACC_NODE_READ_ERROR) : (st & ~KACC_NODE_READ_ERROR);
 }
 
 }  // namespace zagg
@@ -168,7 +183,7 @@ int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_
   a.out_max = out_max;
   a.node_status = node_status;
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  const uint32_t grid = (a.n + kacc::zagg::kThreads - 1) / kacc::zagg::kThreads;
+  const uint32_t grid = (z->n_nodes + kacc::zagg::kThreads - 1) / kacc::zagg::kThreads;
   hipLaunchKernelGGL(kacc::zagg::zone_agg_kernel, dim3(grid), dim3(kacc::zagg::kThreads), 0, st, a);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;

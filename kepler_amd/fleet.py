@@ -324,8 +324,25 @@ class FleetSim:
     zero_ratio_frac: float = 0.01
     churn: float = 0.02
     read_error_frac: float = 0.0
+    # fraction of nodes per interval given one adversarial-but-reachable input (see
+    # ADVERSARIAL): zero / backward clock steps, unchanged counters, usage ratio 1 / > 1 /
+    # < 0, negative CPU deltas (PID reuse in a cached entry), huge cancelling deltas
+    adversarial: float = 0.0
     interval: int = 0
     _rng: np.random.Generator = field(init=False, repr=False)
+
+    # adversarial scenarios: (name, reference line the input exercises)
+    ADVERSARIAL = (
+        ("dt_zero", "node.go:34 now.Sub(prev).Seconds() == 0 -> p = ΔE/0 = +Inf or NaN"),
+        ("clock_backward", "node.go:34 negative Seconds() -> negative / -Inf power"),
+        ("energy_unchanged", "node.go:50-56 ΔE = 0 with a nonzero ratio -> activeEnergy 0, zones skipped"),
+        ("energy_unchanged_one_zone", "node.go:50-56 one zone's ΔE = 0"),
+        ("ratio_one", "node.go:56 usage ratio exactly 1: idle = 0"),
+        ("ratio_above_one", "procfs_reader.go:137-139 (dIdle+dIowait < 0) -> ratio > 1: u64 idle wraps"),
+        ("ratio_negative", "ratio < 0 -> Energy(negative) wraps, negative ActivePower"),
+        ("negative_cpu_delta", "informer.go:518 a reused PID in a cached entry: Δ = total - prev < 0"),
+        ("huge_cancelling_deltas", "process.go:130 ratio = Δ/ΔcpuNode huge -> Energy() out of range"),
+    )
 
     def __post_init__(self):
         L = self.layout
@@ -336,6 +353,12 @@ class FleetSim:
         self.ts = (1_000_000_000_000 + self._rng.integers(0, 10**9, size=N)).astype(np.int64)
         self.cum_ticks = self._rng.integers(0, 10_000, size=L.n_procs).astype(np.int64)
         self.prev_total = np.zeros(L.n_procs, dtype=np.float64)  # informer cache starts empty
+        # a process born while its node's reads fail is first seen (NEW) at the node's next
+        # good interval: Refresh is skipped when calculateNodePower fails (monitor.go:399-408)
+        self.pending_new = np.zeros(L.n_procs, dtype=bool)
+        self.node_of_proc = np.repeat(np.arange(N), np.diff(L.proc_off.astype(np.int64)))
+        self.last_status = np.zeros(N, dtype=np.uint32)
+        self.last_scenario = np.full(N, -1, dtype=np.int64)
         pkg = self._rng.uniform(50.0, 400.0, size=N)
         dram = self._rng.uniform(5.0, 40.0, size=N)
         watts = {"package": pkg, "core": 0.6 * pkg, "uncore": 0.1 * pkg, "dram": dram,
@@ -347,16 +370,37 @@ class FleetSim:
         L, rng = self.layout, self._rng
         N, Z = L.n_nodes, L.zones
         dt = self.dt_ns + rng.integers(-self.jitter_ns, self.jitter_ns + 1, size=N)
-        self.ts = self.ts + dt
         dts = np.repeat(dt, Z).astype(np.float64) / 1e9
         watts = self.zone_watts * rng.uniform(0.8, 1.2, size=N * Z)
         de = np.round(watts * dts * 1e6).astype(np.uint64)
-        self.counters = (self.counters + de) % self.zone_max
         ratio = rng.uniform(0.05, 0.95, size=N)
         ratio[rng.random(N) < self.zero_ratio_frac] = 0.0
+        scen = np.full(N, -1, dtype=np.int64)
+        if self.adversarial > 0 and self.interval > 0:
+            # a separate stream: the ordinary inputs stay those of a non-adversarial sim
+            arng = np.random.default_rng([self.seed, 0xAD, self.interval])
+            hit = arng.random(N) < self.adversarial
+            scen[hit] = arng.integers(0, len(self.ADVERSARIAL), size=int(hit.sum()))
+            names = [s[0] for s in self.ADVERSARIAL]
+            is_ = lambda name: scen == names.index(name)  # noqa: E731
+            # the counters advance with real time; only the clock reading is off
+            dt = np.where(is_("dt_zero"), 0, dt)
+            dt = np.where(is_("clock_backward"), -arng.integers(1, 5 * 10**9, size=N), dt)
+            de = de.reshape(N, Z)
+            de[is_("energy_unchanged")] = 0
+            one = np.flatnonzero(is_("energy_unchanged_one_zone"))
+            de[one, arng.integers(0, Z, size=one.size)] = 0
+            de = de.reshape(-1)
+            ratio = np.where(is_("ratio_one"), 1.0, ratio)
+            ratio = np.where(is_("ratio_above_one"), 1.0 + arng.uniform(0.01, 1.0, size=N), ratio)
+            ratio = np.where(is_("ratio_negative"), -arng.uniform(0.01, 0.5, size=N), ratio)
+        self.ts = self.ts + dt
+        self.counters = (self.counters + de) % self.zone_max
         status = np.zeros(N, dtype=np.uint32)
         if self.read_error_frac > 0 and self.interval > 0:
             status[rng.random(N) < self.read_error_frac] = KACC_NODE_READ_ERROR
+        self.last_status = status
+        self.last_scenario = scen
         return dict(node_ts_ns=self.ts.astype(np.int64), node_usage_ratio=ratio, node_status=status,
                     zone_energy=self.counters.copy(), zone_max=self.zone_max)
 
@@ -369,17 +413,41 @@ class FleetSim:
         dticks = np.where(rng.random(P) < 0.3, 0,
                           np.minimum(rng.lognormal(3.0, 1.5, size=P), 50_000.0)).astype(np.int64)
         proc_slot = L.proc_slot.copy()
+        # rows of nodes whose read fails this interval: the reference skips Refresh
+        # (monitor.go:399-408), so their informer cache (prev totals) stays and a process
+        # born meanwhile is first seen at the node's next good interval
+        skipped = (self.last_status[self.node_of_proc] & KACC_NODE_READ_ERROR) != 0
         if first:
             proc_slot |= np.uint32(KACC_SLOT_NEW)
         elif self.churn > 0:
             born = rng.random(P) < self.churn  # PID reuse of the slot by a new process
             self.cum_ticks[born] = 0
             self.prev_total[born] = 0.0
-            proc_slot[born] |= np.uint32(KACC_SLOT_NEW)
+            self.pending_new |= born
+        if not first:
+            show = self.pending_new & ~skipped
+            proc_slot[show] |= np.uint32(KACC_SLOT_NEW)
+            self.pending_new &= skipped
         self.cum_ticks += dticks
+        if self.adversarial > 0 and not first:
+            arng = np.random.default_rng([self.seed, 0xAE, self.interval])
+            scen = self.last_scenario[self.node_of_proc]
+            names = [s[0] for s in self.ADVERSARIAL]
+            # a reused PID in a cached entry: the new process's cumulative time is below the
+            # old one's, and the entry is not new (informer.go:512-520) -> Δ < 0
+            reuse = (scen == names.index("negative_cpu_delta")) & (arng.random(P) < 0.3)
+            self.cum_ticks[reuse] = arng.integers(0, 50, size=int(reuse.sum()))
+            # long-lived processes with huge cumulative times whose deltas cancel: ΔcpuNode is
+            # tiny next to single deltas, ratios are huge, Energy() goes out of range
+            cached = (proc_slot & np.uint32(KACC_SLOT_NEW)) == 0  # entries the informer already had
+            huge = np.flatnonzero((scen == names.index("huge_cancelling_deltas")) & (arng.random(P) < 0.05) & cached)
+            if huge.size:  # alternately +M (a long runner) and -M (a reused PID of one), M = 1e13 s
+                up, down = huge[0::2], huge[1::2]
+                self.cum_ticks[up] += 10**15
+                self.prev_total[down] += 1e13
         total = self.cum_ticks.astype(np.float64) / 100.0
         cpu_delta = total - self.prev_total
-        self.prev_total = total
+        self.prev_total = np.where(skipped, self.prev_total, total)
         flag = np.uint32(KACC_SLOT_NEW) if first else np.uint32(0)
         self.interval += 1
         out.update(

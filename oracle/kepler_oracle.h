@@ -106,6 +106,7 @@ typedef struct kor_tracker kor_tracker;
 kor_tracker *kor_tracker_create(int64_t max_size, uint64_t min_energy, uint32_t zones, uint32_t zone);
 void kor_tracker_destroy(kor_tracker *t);
 void kor_tracker_clear(kor_tracker *t);
+void kor_tracker_clear_node(kor_tracker *t, uint32_t node);
 void kor_tracker_add_one(kor_tracker *t, uint32_t node, uint64_t key, const uint64_t *energy,
                          const double *power);
 void kor_tracker_add_batch(kor_tracker *t, uint32_t n, const uint32_t *node, const uint64_t *key,

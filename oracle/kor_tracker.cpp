@@ -3,7 +3,8 @@
 // CPU restatement of TerminatedResourceTracker
 // (internal/monitor/terminated_resource_tracker.go) with Go's container/heap
 // algorithms (Push = append + up, Pop = swap(0, n-1) + down + remove last;
-// Less = EnergyTotal <, :188-191), item by item as Add() does it.
+// Less = EnergyTotal <, :188-191), item by item as Add() does it — one tracker
+// per node, as every node's PowerMonitor owns its own (monitor.go:123-144).
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -25,10 +26,10 @@ struct Item {
 
 }  // namespace
 
-struct kor_tracker {
+// One node's TerminatedResourceTracker.
+struct NodeTracker {
   int64_t max_size;
   uint64_t min_energy;
-  uint32_t zones, zone;
   std::vector<Item> heap;                                       // Heap[T]
   std::map<std::pair<uint32_t, uint64_t>, size_t> resources;   // ID -> present (index unused)
 
@@ -85,6 +86,18 @@ struct kor_tracker {
   }
 };
 
+struct kor_tracker {
+  int64_t max_size;
+  uint64_t min_energy;
+  uint32_t zones, zone;
+  std::map<uint32_t, NodeTracker> nodes;  // node -> its own tracker
+  void add(Item it) {
+    auto f = nodes.find(it.node);
+    if (f == nodes.end()) f = nodes.emplace(it.node, NodeTracker{max_size, min_energy, {}, {}}).first;
+    f->second.add(std::move(it));
+  }
+};
+
 extern "C" {
 
 kor_tracker *kor_tracker_create(int64_t max_size, uint64_t min_energy, uint32_t zones, uint32_t zone) {
@@ -98,10 +111,11 @@ kor_tracker *kor_tracker_create(int64_t max_size, uint64_t min_energy, uint32_t 
 
 void kor_tracker_destroy(kor_tracker *t) { delete t; }
 
-void kor_tracker_clear(kor_tracker *t) {  // :156-160
-  t->heap.clear();
-  t->resources.clear();
+void kor_tracker_clear(kor_tracker *t) {  // :156-160, every node
+  t->nodes.clear();
 }
+
+void kor_tracker_clear_node(kor_tracker *t, uint32_t node) { t->nodes.erase(node); }
 
 void kor_tracker_add_one(kor_tracker *t, uint32_t node, uint64_t key, const uint64_t *energy,
                          const double *power) {
@@ -136,7 +150,8 @@ uint32_t kor_tracker_items(const kor_tracker *t, uint64_t *key, uint32_t *node, 
                            double *power) {
   // Items() is a map: returned here sorted by (node, key)
   std::vector<const Item *> v;
-  for (const auto &it : t->heap) v.push_back(&it);
+  for (const auto &nt : t->nodes)
+    for (const auto &it : nt.second.heap) v.push_back(&it);
   std::sort(v.begin(), v.end(), [](const Item *a, const Item *b) {
     return a->node != b->node ? a->node < b->node : a->key < b->key;
   });

@@ -69,6 +69,8 @@ def load():
     lib.kor_tracker_destroy.restype = None
     lib.kor_tracker_clear.argtypes = [c_void_p]
     lib.kor_tracker_clear.restype = None
+    lib.kor_tracker_clear_node.argtypes = [c_void_p, c_uint32]
+    lib.kor_tracker_clear_node.restype = None
     lib.kor_tracker_add_one.argtypes = [c_void_p, c_uint32, c_uint64, c_void_p, c_void_p]
     lib.kor_tracker_add_one.restype = None
     lib.kor_tracker_add_batch.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
@@ -272,8 +274,13 @@ class OracleTracker:
         self.zones = zones
         self.h = self.lib.kor_tracker_create(max_size, min_energy, zones, zone)
 
-    def clear(self):
-        self.lib.kor_tracker_clear(self.h)
+    def clear(self, nodes=None):
+        """Clear every node's tracker, or those of `nodes`."""
+        if nodes is None:
+            self.lib.kor_tracker_clear(self.h)
+        else:
+            for n in nodes:
+                self.lib.kor_tracker_clear_node(self.h, int(n))
 
     def add_one(self, node: int, key: int, energy, power=None):
         e = np.ascontiguousarray(energy, dtype=np.uint64)

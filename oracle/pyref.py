@@ -40,6 +40,12 @@ def go_float64_to_uint64(x: float) -> int:
     return (cvttsd2sq(x - TWO63) | (1 << 63)) & U64
 
 
+def go_fdiv(a: float, b: float) -> float:
+    """Go float64 division: IEEE, x/0 = ±Inf, 0/0 = NaN (no panic, unlike Python's `/`)."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return float(np.float64(a) / np.float64(b))
+
+
 def go_trunc_divmod(d: int, m: int):
     """Go integer division and remainder (truncated toward zero)."""
     q = abs(d) // m
@@ -102,7 +108,7 @@ class PyRef:
             delta = energy_delta(e, pz["EnergyTotal"], int(a["zone_max"][n * Z + z]))
             active = go_float64_to_uint64(float(delta) * ratio)
             idle = (delta - active) & U64
-            p = float(delta) / dt
+            p = go_fdiv(float(delta), dt)
             ap = p * ratio
             zones.append(dict(EnergyTotal=e, ActiveEnergyTotal=(pz["ActiveEnergyTotal"] + active) & U64,
                               IdleEnergyTotal=(pz["IdleEnergyTotal"] + idle) & U64, activeEnergy=active,

@@ -156,3 +156,56 @@ def test_format_lines_byte_exact(table, metric):
     offs = d_line_off.cpu().numpy()
     assert offs[-1] == total and np.all(np.diff(offs) > 0)
     acc.close()
+
+
+def test_format_lines_hipcub_fault_regression_multi_tile_past_4gib():
+    """Regression guard for the round-1 fault (DESIGN §4.7: hipcub's scan faulted at 80M lines;
+    the scan is now the library's own reduce-then-scan): 16M lines = 3,907 scan tiles of
+    4,096 (> 256 tiles: the multi-level scan_tile_prefix path) and 5.0 GB of text, so line
+    offsets cross 4 GiB.  line_off is strictly increasing, its last entry is the sizing pass's
+    total, and sampled lines (tile edges, the 4 GiB crossing, random) match
+    oracle/gofmt.sample_line byte for byte."""
+    from kepler_amd.torch_batch import current_stream_handle
+    from oracle.gofmt import sample_line
+
+    Z, count, L = 4, 4_000_000, 260
+    metric = "kepler_process_cpu_joules_total"
+    zone_names = ["package", "core", "uncore", "dram"]
+    rng = np.random.default_rng(23)
+    acc = accel.Accel(Z, nodes=1, proc_slots=count, ctr_slots=1, vm_slots=1, pod_slots=1)
+    vals = (rng.lognormal(20, 5, size=count * Z)).astype(np.uint64)
+    acc.upload("proc_energy", vals)
+    # fixed-width label pairs: pid="00001234",comm="xxxx...x" (L bytes per row)
+    head = b'comm="'
+    body = np.frombuffer((head + b"w" * (L - len(head) - len(b'",pid="00000000"')) + b'",pid="00000000"'), np.uint8)
+    labels = np.tile(body, (count, 1))
+    digits = np.array([(np.arange(count) // 10 ** k) % 10 for k in range(7, -1, -1)], dtype=np.uint8).T + ord("0")
+    labels[:, L - 9:L - 1] = digits
+    d_labels = torch.from_numpy(labels.reshape(-1)).cuda()
+    label_off = (np.arange(count + 1, dtype=np.int64) * L)
+    d_loff = torch.from_numpy(label_off).cuda()
+    n_lines = count * Z
+    d_line_off = torch.zeros(n_lines + 1, dtype=torch.int64, device="cuda")
+    s = current_stream_handle()
+    args = ("proc_energy", metric, 0, count, zone_names, d_labels.data_ptr(), d_loff.data_ptr(),
+            d_line_off.data_ptr())
+    total = acc.format_lines(*args, stream=s)
+    assert total > 2**32 and n_lines > 256 * 4096
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    assert acc.format_lines(*args, out_ptr=out.data_ptr(), out_cap=total, stream=s) == total
+    acc.sync(s)
+    offs = d_line_off.cpu().numpy()
+    assert offs[0] == 0 and offs[-1] == total
+    assert np.all(np.diff(offs) > 0)
+    cross = int(np.searchsorted(offs, 2**32, side="right")) - 1  # the line holding byte 2^32
+    picks = {0, 1, n_lines - 1, cross - 1, cross, cross + 1}
+    for t in (4096, 4096 * 256, 4096 * 257, 4096 * 1000):  # scan tile edges
+        picks |= {t - 1, t, t + 1}
+    picks |= set(rng.integers(0, n_lines, size=400).tolist())
+    for i in sorted(p for p in picks if 0 <= p < n_lines):
+        r, z = divmod(i, Z)
+        got = bytes(out[int(offs[i]):int(offs[i + 1])].cpu().numpy())
+        want = sample_line(metric, bytes(labels[r]).decode(), zone_names[z], joules(int(vals[r * Z + z]))).encode()
+        assert got == want, (i, got[:120], want[:120])
+    del out
+    acc.close()

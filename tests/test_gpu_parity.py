@@ -407,3 +407,61 @@ def test_recreated_aggregates_bit_exact():
         ora.interval(a, layout.sizes())
         for name, _ in accel.TABLES:
             np.testing.assert_array_equal(eng.table(name), ora.state[name], err_msg=f"interval {k} {name}")
+
+
+def assert_table_equal(got, want, msg):
+    """Bit-exact, except that any NaN equals any NaN: Go formats every NaN alike ("NaN" in
+    strconv and the Prometheus text format) and the NaN bits are not an observable of the
+    reference; x86 SSE2 (Go on amd64, the oracle) produces the default NaN with the sign
+    bit set where gfx950 produces it without."""
+    if want.dtype == np.float64:
+        gb, wb = got.view(np.uint64), want.view(np.uint64)
+        both_nan = np.isnan(got) & np.isnan(want)
+        bad = (gb != wb) & ~both_nan
+        assert not bad.any(), f"{msg}: {int(bad.sum())} differ, first at {int(np.flatnonzero(bad)[0])}: " \
+                              f"{got[bad][0]!r} vs {want[bad][0]!r}"
+    else:
+        np.testing.assert_array_equal(got, want, err_msg=msg)
+
+
+ADV_FLEETS = [
+    ("z4-fast-shuffled", dict(n_nodes=40, procs_per_node=[2000, 300, 1, 0, 1500] * 8, zones=4,
+                              shuffle_slots=True)),
+    ("z2-small-kernel", dict(n_nodes=64, procs_per_node=[500, 64, 3, 0] * 16, zones=2)),
+    ("z4-small-kernel", dict(n_nodes=32, procs_per_node=[512, 200, 1, 77] * 8, zones=4)),
+    ("z4-big-nodes", dict(n_nodes=6, procs_per_node=[10000, 3000, 12, 0, 2049, 700], zones=4, vm_frac=0.02,
+                          procs_per_vm=2)),
+    ("z3-odd", dict(n_nodes=30, procs_per_node=257, zones=3, vm_frac=0.05, procs_per_vm=3)),
+    ("z4-fragmented-span", dict(n_nodes=24, procs_per_node=[2000, 1200, 64, 5] * 6, zones=4, fragment_slots=0.05)),
+]
+
+
+@pytest.mark.parametrize("name,kw", ADV_FLEETS, ids=[f[0] for f in ADV_FLEETS])
+def test_adversarial_inputs_bit_exact(name, kw):
+    """Reachable edge inputs (fleet.FleetSim.ADVERSARIAL), every table against the oracle:
+    Δt = 0 / backward clock (node.go:34 -> ±Inf / NaN node and workload power), unchanged
+    counters (ΔE = 0 with a nonzero ratio), usage ratio 1 / > 1 / < 0 (u64 idle wrap,
+    negative ActivePower), negative CPU deltas (informer.go:518, PID reuse in a cached
+    entry: Energy() of negatives, u64 EnergyTotal wrap, process.go:136) and huge cancelling
+    deltas (Energy() out of range, process.go:130), with churn and read errors, on every
+    kernel path (fast, small, chunked big nodes, odd Z, slot sweep)."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(seed=19, **kw)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=19, churn=0.04, read_error_frac=0.05, adversarial=0.5)
+    eng = EngineBackend(layout.zones, caps)
+    ora = Oracle(layout.zones, **caps)
+    edges = 0
+    for k in range(6):
+        a = sim.next_interval()
+        if kw.get("fragment_slots"):
+            a["node_proc_span"] = layout.proc_span()
+        eng.interval(a, layout.sizes(), layout.fast_flag())
+        ora.interval(a, layout.sizes())
+        for tname, _ in accel.TABLES:
+            assert_table_equal(eng.table(tname), ora.state[tname], f"interval {k} {tname}")
+        st = ora.state
+        edges += int((~np.isfinite(st["node_power"])).sum() + (st["node_active_power"] < 0).sum()
+                     + (st["proc_energy"] >= np.uint64(1 << 63)).sum() + (a["proc_cpu_delta"] < 0).sum())
+    assert edges > 0  # the edges were exercised

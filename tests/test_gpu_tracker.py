@@ -63,6 +63,7 @@ def test_tracker_kat_on_device(case):
 
 FLEETS = [
     ("small", [40, 0, 300, 7, 1000, 64], 2, 0.1, 25),
+    ("many-nodes-top3", [60, 200, 5, 0, 90, 400] * 6, 2, 0.1, 3),
     ("config3-like", [2000] * 16, 4, 0.02, 500),
     ("unlimited", [500, 200, 1500], 2, 0.05, -1),
     ("big-node", [12000, 300, 2500], 4, 0.03, 200),
@@ -72,8 +73,10 @@ FLEETS = [
 @pytest.mark.parametrize("concurrent", [False, True], ids=["one-stream", "tracker-beside-interval"])
 @pytest.mark.parametrize("name,sizes,Z,churn,max_size", FLEETS, ids=[f[0] for f in FLEETS])
 def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurrent):
-    """concurrent: the tracker runs on a second stream beside the interval kernel
-    (it reads only terminated slots, which the interval never writes)."""
+    """One tracker per node (every node's PowerMonitor owns one): each node keeps its own top
+    max_size, against one Go heap per node.  concurrent: the tracker runs on a second stream
+    beside the interval kernel (it reads only terminated slots, which the interval never
+    writes) and clears only the odd nodes (a per-node export); otherwise every node."""
     layout = fleet.make_layout(len(sizes), sizes, Z, seed=31)
     sizes_d = layout.sizes()
     rows = np.diff(layout.proc_off.astype(np.int64))
@@ -114,8 +117,14 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
             s2.wait_event(joined)
         acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         if it == 3:  # an export happened: Clear() before this interval's adds (process.go:80-84)
-            tr.clear(ts2)
-            otr.clear()
+            if concurrent:  # only the odd nodes exported
+                mask = (np.arange(layout.n_nodes) % 2).astype(np.int32)
+                d_mask = torch.from_numpy(mask).cuda()
+                tr.clear(ts2, d_mask.data_ptr())
+                otr.clear(np.flatnonzero(mask))
+            else:
+                tr.clear(ts2)
+                otr.clear()
         tr.add(sm, tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), ts2)
         if concurrent:  # the next join rewrites the terminated lists the tracker reads
             torch.cuda.current_stream().wait_stream(s2)

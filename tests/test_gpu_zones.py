@@ -38,10 +38,11 @@ class GpuAgg:
         self.m = torch.zeros(n_nodes * self.Z, dtype=torch.int64, device="cuda")
         self.st = torch.zeros(n_nodes, dtype=torch.int32, device="cuda")
 
-    def read(self, readings, sub_status=None, sync=True):
+    def read(self, readings, sub_status=None, sync=True, zero_status=True):
         r = dev(readings, np.uint64)
         s = None if sub_status is None else dev(sub_status, np.uint32)
-        self.st.zero_()
+        if zero_status:
+            self.st.zero_()
         h = current_stream_handle()
         self.z.read(r.data_ptr(), 0 if s is None else s.data_ptr(), self.e.data_ptr(), self.m.data_ptr(),
                     self.st.data_ptr(), h)
@@ -115,3 +116,26 @@ def test_aggregated_zones_feed_interval():
         ora.interval(a_ora, layout.sizes())
         for name, _ in accel.TABLES:
             np.testing.assert_array_equal(acc.download(name), ora.state[name], err_msg=f"interval {it} {name}")
+
+
+def test_read_error_bit_set_and_cleared_every_read():
+    """node_status passed unchanged every interval (INTEGRATION.md's loop): the read-error
+    bit follows each read — a node fails only the intervals whose reads failed (monitor.go:
+    328-335) — and the caller's other status bits are kept."""
+    N, Z, S = 6, 2, 2
+    sub_max = np.full(N * Z * S, 10**9, dtype=np.uint64)
+    acc = accel.Accel(Z, nodes=N, proc_slots=1, ctr_slots=1, vm_slots=1, pod_slots=1)
+    g, o = GpuAgg(acc, N, S, sub_max), OracleZoneAgg(N, Z, S, sub_max)
+    g.st.copy_(torch.tensor([0, 4, 0, 4, 0, 0], dtype=torch.int32))  # an unrelated caller bit
+    cnt = np.arange(N * Z * S, dtype=np.uint64) * 1000
+    for it, bad_nodes in enumerate([[], [1, 2], [2], [], [5]]):
+        cnt = cnt + np.uint64(777)
+        st = np.zeros(N * Z * S, np.uint32)
+        for n in bad_nodes:
+            st[n * Z * S + S] = 1  # node n, zone 1, socket 0
+        ge, _, gs = g.read(cnt, st, zero_status=False)
+        oe, _, os_ = o.read(cnt, st)
+        want = np.array([4 if n in (1, 3) else 0 for n in range(N)], np.uint32) | os_
+        np.testing.assert_array_equal(gs, want, err_msg=f"read {it}")
+        good = np.repeat(os_ == 0, Z)
+        np.testing.assert_array_equal(ge[good], oe[good], err_msg=f"read {it}")

@@ -71,3 +71,58 @@ def test_threaded_oracle_matches_serial(oracle_lib):
         a_mt.interval_mt(a, layout.sizes(), threads=5)
     for tname, _ in accel.TABLES:
         np.testing.assert_array_equal(a_mt.state[tname], a_ser.state[tname], err_msg=tname)
+
+
+def bits(a: np.ndarray) -> np.ndarray:
+    return a.view(np.uint64) if a.dtype == np.float64 else a
+
+
+@pytest.mark.parametrize("name,kw", FLEETS + [("z4-big", dict(n_nodes=4, procs_per_node=[2500, 40, 700, 9],
+                                                              zones=4))], ids=[f[0] for f in FLEETS] + ["z4-big"])
+def test_adversarial_inputs_oracle_matches_python_restatement(name, kw, oracle_lib):
+    """Reachable edge inputs (fleet.FleetSim.ADVERSARIAL: Δt = 0 and backward clock -> ±Inf / NaN
+    power, unchanged counters, usage ratio 1 / > 1 / < 0 -> u64 idle wrap, negative CPU deltas
+    -> Energy() of negatives and u64 total wrap, huge cancelling deltas -> Energy() out of
+    range): the C++ oracle and the Python restatement agree bit for bit, NaN bits included
+    (both evaluate on x86 SSE2, as Go on amd64 does)."""
+    from oracle.oracle import KOR_SUM_LISTING, Oracle
+
+    layout = fleet.make_layout(seed=7, **kw)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=7, churn=0.05, read_error_frac=0.1, adversarial=0.6)
+    ora = Oracle(layout.zones, **caps, sum_mode=KOR_SUM_LISTING)
+    ref = PyRef(layout.zones)
+    for k in range(6):
+        a = sim.next_interval()
+        ora.interval(a, layout.sizes())
+        ref.interval(a)
+        got = ref.tables(layout.n_nodes, caps)
+        for tname, _ in accel.TABLES:
+            np.testing.assert_array_equal(bits(ora.state[tname]), bits(got[tname]), err_msg=f"interval {k} {tname}")
+
+
+def test_adversarial_scenarios_reach_their_edges(oracle_lib):
+    """The adversarial mode really produces the edge values it is for."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(40, [300, 64, 1000, 5] * 10, 4, seed=3)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=3, adversarial=0.9)
+    ora = Oracle(layout.zones, **caps)
+    seen = dict(inf=False, nan=False, neg_power=False, idle_wrap=False, out_of_range=False, neg_delta=False)
+    prev_idle = None
+    for k in range(8):
+        a = sim.next_interval()
+        seen["neg_delta"] |= bool((a["proc_cpu_delta"] < 0).any())
+        ora.interval(a, layout.sizes())
+        st = ora.state
+        npow = np.concatenate([st["node_power"], st["proc_power"]])
+        seen["inf"] |= bool(np.isinf(npow).any())
+        seen["nan"] |= bool(np.isnan(np.concatenate([st["node_idle_power"], st["proc_power"]])).any())
+        seen["neg_power"] |= bool((st["node_active_power"] < 0).any())
+        seen["out_of_range"] |= bool((st["proc_energy"] == np.uint64(1 << 63)).any())
+        idle = st["node_idle_total"].copy()
+        if prev_idle is not None:
+            seen["idle_wrap"] |= bool((idle < prev_idle).any())  # u64 modular add wrapped
+        prev_idle = idle
+    assert all(seen.values()), seen

@@ -14,7 +14,8 @@ def test_tracker_oracle_kat(case):
 
 
 def test_batch_order_is_a_go_order():
-    """add_batch == add_one in descending-energy order (one of Go's map orders)."""
+    """add_batch == add_one in descending-energy order (one of Go's map orders); one tracker
+    per node."""
     from oracle.oracle import OracleTracker
 
     rng = np.random.default_rng(5)
@@ -31,8 +32,11 @@ def test_batch_order_is_a_go_order():
         b.add_one(int(node[i]), int(key[i]), tab_e[slot[i] * Z: slot[i] * Z + Z], tab_p[slot[i] * Z: slot[i] * Z + Z])
     for x, y in zip(a.items(), b.items()):
         np.testing.assert_array_equal(x, y)
-    k, _, e, _ = a.items()
-    assert k.size == 50
-    # top-50 by energy (distinct values): exactly the 50 largest eligible
-    eligible = sorted((int(tab_e[s * Z]) for s in slot if int(tab_e[s * Z]) >= 10**6), reverse=True)[:50]
-    assert sorted(int(x) for x in e[:, 0]) == sorted(eligible)
+    k, nd, e, _ = a.items()
+    # one tracker per node (monitor.go:123-144): each node keeps its own top 50 (distinct values)
+    for n in range(4):
+        elig = sorted((int(tab_e[slot[i] * Z]) for i in range(len(slot))
+                       if node[i] == n and int(tab_e[slot[i] * Z]) >= 10**6), reverse=True)[:50]
+        got = sorted(int(x) for x in e[nd == n, 0])
+        assert got == sorted(elig), n
+    assert k.size == sum(min(50, int(((node == n) & (tab_e[slot * Z] >= 10**6)).sum())) for n in range(4)) > 50
