@@ -412,6 +412,62 @@ int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, co
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                    uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream);
 
+/* ---- host packer: informer records -> interval CSR -----
+ * The step before the path: what resource.Informer.Refresh
+ * (internal/resource/informer.go:167-326) leaves per node — the running
+ * processes in /proc listing order with PID, CPUTimeDelta, Type and their
+ * container / VM / pod — packed into kacc_interval's layout, on host threads:
+ * container processes grouped by container (containers grouped by pod, pods
+ * in order of their containers' first appearance, ContainersNoPod last; a
+ * container's rows in listing order: its CPU-time sum order, :229-233), then
+ * VM processes grouped by VM (listing order: the last row is the writer,
+ * :445), then the others.  Container / VM / pod IDs are the caller's 64-bit
+ * keys of the ID strings (KACC_KEY_EMPTY / KACC_KEY_TOMB reserved).  The
+ * packer emits the keys kacc_slot_join takes (PIDs per row, IDs per
+ * aggregate) and row_record (the input record of every row) for kacc_unpack.
+ * Outputs may point into a pinned batch view (kacc_batch_alloc).             */
+#define KACC_PROC_REGULAR 0u   /* resource.RegularProcess   */
+#define KACC_PROC_CONTAINER 1u /* resource.ContainerProcess */
+#define KACC_PROC_VM 2u        /* resource.VMProcess        */
+typedef struct kacc_records {
+  uint32_t n_nodes;
+  uint32_t reserved0;
+  const uint32_t *rec_off;   /* [n_nodes + 1] node n's records [rec_off[n], rec_off[n+1])   */
+  const uint32_t *pid;       /* [R] Process.PID                                              */
+  const double *cpu_delta;   /* [R] Process.CPUTimeDelta (informer.go:518)                   */
+  const uint8_t *type;       /* [R] KACC_PROC_*  (Process.Type)                              */
+  const uint64_t *ctr_key;   /* [R] key of Process.Container.ID (type CONTAINER)             */
+  const uint64_t *vm_key;    /* [R] key of Process.VirtualMachine.ID (type VM)               */
+  const uint64_t *pod_key;   /* [R] key of the container's Pod.ID per LookupByContainerID
+                                    (pod.go:209-239), KACC_KEY_EMPTY = not found; or NULL     */
+  const uint32_t *pod_ns;    /* [R] the pod's namespace index (namespace totals); or NULL    */
+} kacc_records;
+typedef struct kacc_packed {
+  /* in: array capacities; out: the counts (also on KACC_ERANGE: the sizes needed) */
+  uint32_t n_procs, n_ctrs, n_vms, n_pods;
+  uint32_t *proc_off, *ctr_off, *vm_off, *pod_off; /* [n_nodes + 1]                    */
+  double *proc_cpu_delta;                          /* [P] rows                          */
+  uint32_t *proc_key;                              /* [P] PID of each row               */
+  uint32_t *row_record;                            /* [P] input record of each row, or NULL */
+  uint32_t *ctr_proc_end;                          /* [C]                               */
+  uint64_t *ctr_key;                               /* [C]                               */
+  uint32_t *vm_proc_end;                           /* [V]                               */
+  uint64_t *vm_key;                                /* [V]                               */
+  uint32_t *pod_ctr_end;                           /* [Q]                               */
+  uint64_t *pod_key;                               /* [Q]                               */
+  uint32_t *pod_ns;                                /* [Q]                               */
+} kacc_packed;
+/* HOST arrays; `threads` host threads (0 = 1).  KACC_ERANGE when a capacity
+ * is short (out->n_* then hold the sizes needed; nothing was written).     */
+int kacc_pack(const kacc_records *in, kacc_packed *out, uint32_t threads);
+/* The unpack (device, async on `stream`): for i < n, the kind's state-table
+ * row of slot word slot_words[i] (energy u64 / power f64, Z each) goes to
+ * out row dest[i] (dest = the packer's row_record: results in input-record
+ * order) or row i (dest NULL: in batch order, the order of the packer's
+ * keys) — what the cgo shim turns into Snapshot entries (types.go:75-193). */
+int kacc_unpack(kacc_ctx *ctx, kacc_kind kind, uint32_t n, const uint32_t *slot_words, const uint32_t *dest,
+                uint64_t *out_energy, double *out_power, void *stream);
+
 /* ---- terminated-workload trackers ---------------------
  * TerminatedResourceTracker (internal/monitor/terminated_resource_tracker.go)
  * for one workload kind, on the device — ONE TRACKER PER NODE, as every

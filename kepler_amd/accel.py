@@ -45,6 +45,8 @@ KACC_F_SMALL_NODES = 0x8
 KACC_SMALL_MAX_PROCS = 512
 KACC_SMALL_MAX_AGGREGATES = 128
 KACC_UNIQUE_ID_BYTES = 128
+KACC_PROC_REGULAR, KACC_PROC_CONTAINER, KACC_PROC_VM = 0, 1, 2
+KACC_KEY_TOMB = 0xFFFFFFFFFFFFFFFE
 
 # kacc_table enum, in header order: (name, numpy dtype)
 TABLES = [
@@ -88,6 +90,8 @@ EXPORTS = [
     "kacc_tracker_clear",
     "kacc_tracker_add",
     "kacc_tracker_items",
+    "kacc_pack",
+    "kacc_unpack",
     "kacc_slotmap_create",
     "kacc_slotmap_destroy",
     "kacc_slotmap_reset",
@@ -184,6 +188,22 @@ ARRAY_DTYPES = {
 }
 
 
+class KaccRecords(ctypes.Structure):
+    _fields_ = [("n_nodes", c_uint32), ("reserved0", c_uint32)] + [
+        (n, c_void_p) for n in ("rec_off", "pid", "cpu_delta", "type", "ctr_key", "vm_key", "pod_key", "pod_ns")]
+
+
+PACKED_ARRAYS = [("proc_off", np.uint32), ("ctr_off", np.uint32), ("vm_off", np.uint32), ("pod_off", np.uint32),
+                 ("proc_cpu_delta", np.float64), ("proc_key", np.uint32), ("row_record", np.uint32),
+                 ("ctr_proc_end", np.uint32), ("ctr_key", np.uint64), ("vm_proc_end", np.uint32),
+                 ("vm_key", np.uint64), ("pod_ctr_end", np.uint32), ("pod_key", np.uint64), ("pod_ns", np.uint32)]
+
+
+class KaccPacked(ctypes.Structure):
+    _fields_ = [(n, c_uint32) for n in ("n_procs", "n_ctrs", "n_vms", "n_pods")] + [
+        (n, c_void_p) for n, _ in PACKED_ARRAYS]
+
+
 class KaccShape(ctypes.Structure):
     _fields_ = [(n, c_uint32) for n in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods", "intervals")]
 
@@ -236,6 +256,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_sync.argtypes = [c_void_p, c_void_p]
     lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
     lib.kacc_batch_alloc.argtypes = [c_void_p, POINTER(KaccShape), POINTER(c_void_p), POINTER(POINTER(KaccInterval))]
+    lib.kacc_pack.argtypes = [POINTER(KaccRecords), POINTER(KaccPacked), c_uint32]
+    lib.kacc_unpack.argtypes = [c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.kacc_last_error_copy.argtypes = [c_void_p, c_char_p, ctypes.c_size_t]
     lib.kacc_last_error_copy.restype = ctypes.c_size_t
     lib.kacc_create_multi.argtypes = [POINTER(c_int), c_int, POINTER(KaccConfig), POINTER(c_void_p),
@@ -292,6 +314,50 @@ def last_error(ctx=None) -> str:
     buf = ctypes.create_string_buffer(1024)
     lib.kacc_last_error_copy(ctx, buf, len(buf))
     return buf.value.decode()
+
+
+def pack(rec_off, pid, cpu_delta, ptype, ctr_key, vm_key, pod_key=None, pod_ns=None, threads: int = 1,
+         out: Optional[dict] = None) -> dict:
+    """kacc_pack over host arrays: informer records (per node, /proc listing order) -> the
+    interval CSR + slot-join keys + row_record.  ``out``: preallocated arrays (e.g. views of a
+    pinned batch) to write into; by default arrays sized for the worst case are allocated and
+    trimmed to the counts.  Returns the arrays and the counts (n_procs, ...)."""
+    lib = load()
+    rec_off = np.ascontiguousarray(rec_off, dtype=np.uint32)
+    n_nodes = rec_off.size - 1
+    R = int(rec_off[-1])
+    arrs = dict(pid=np.ascontiguousarray(pid, dtype=np.uint32), cpu_delta=np.ascontiguousarray(cpu_delta, np.float64),
+                type=np.ascontiguousarray(ptype, dtype=np.uint8), ctr_key=np.ascontiguousarray(ctr_key, np.uint64),
+                vm_key=np.ascontiguousarray(vm_key, np.uint64))
+    if pod_key is not None:
+        arrs["pod_key"] = np.ascontiguousarray(pod_key, np.uint64)
+    if pod_ns is not None:
+        arrs["pod_ns"] = np.ascontiguousarray(pod_ns, np.uint32)
+    for k, a in arrs.items():
+        if a.size != R:
+            raise ValueError(f"{k}: {a.size} records, rec_off says {R}")
+    rec = KaccRecords(n_nodes, 0, rec_off.ctypes.data,
+                      *[arrs[k].ctypes.data if k in arrs else None
+                        for k in ("pid", "cpu_delta", "type", "ctr_key", "vm_key", "pod_key", "pod_ns")])
+    if out is None:
+        sizes = dict(proc_off=n_nodes + 1, ctr_off=n_nodes + 1, vm_off=n_nodes + 1, pod_off=n_nodes + 1)
+        out = {n: np.zeros(max(sizes.get(n, R), 1), dtype=dt) for n, dt in PACKED_ARRAYS}
+        caps = (R, R, R, R)
+    else:
+        caps = (out["proc_cpu_delta"].size, out["ctr_key"].size, out["vm_key"].size, out["pod_key"].size)
+    pk = KaccPacked(*caps, *[out[n].ctypes.data if out.get(n) is not None else None for n, _ in PACKED_ARRAYS])
+    rc = lib.kacc_pack(ctypes.byref(rec), ctypes.byref(pk), threads)
+    if rc != KACC_OK:
+        raise AccelError(rc, last_error(None))
+    counts = dict(n_nodes=n_nodes, n_procs=pk.n_procs, n_ctrs=pk.n_ctrs, n_vms=pk.n_vms, n_pods=pk.n_pods)
+    per = dict(proc=pk.n_procs, row=pk.n_procs, ctr=pk.n_ctrs, vm=pk.n_vms, pod=pk.n_pods)
+    res = {}
+    for n, _ in PACKED_ARRAYS:
+        if out.get(n) is None:
+            continue
+        res[n] = out[n] if n.endswith("_off") else out[n][:per[n.split("_")[0]]]
+    res.update(counts)
+    return res
 
 
 def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int) -> int:
@@ -447,6 +513,12 @@ class Accel:
                                                c_void_p(out_ptr or None), out_cap, ctypes.byref(total),
                                                c_void_p(stream or None)))
         return total.value
+
+    def unpack(self, kind: int, n: int, slot_words_ptr: int, dest_ptr: int, out_energy_ptr: int,
+               out_power_ptr: int, stream: int = 0) -> None:
+        """kacc_unpack: per-workload energy / power rows out of the state tables (device pointers)."""
+        self._check(self.lib.kacc_unpack(self.ctx, kind, n, c_void_p(slot_words_ptr), c_void_p(dest_ptr or None),
+                                         c_void_p(out_energy_ptr), c_void_p(out_power_ptr), c_void_p(stream or None)))
 
     def namespace_totals(self, n_ns: int, ns_pod_off_ptr: int, ns_pod_slot_ptr: int,
                          out_energy_ptr: int, out_power_ptr: int, stream: int = 0) -> None:
