@@ -235,7 +235,9 @@ def main():
         return t
 
     iv_tensors = [make(k) for k in range(n_ivs)]
-    ivs = [interval_from_tensors(t, sizes, layout.fast_flag()) for t in iv_tensors]
+    # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
+    # runs K > 1 fast-node intervals as one launch
+    ivs = [interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES) for t in iv_tensors]
     prime_t = to_device(prime)
     acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
     acc.sync(stream)
@@ -314,8 +316,11 @@ def main():
     wall_max = float(wall_t.item())
     total_procs, total_nodes_done = (float(x) for x in procs_t.tolist())
 
-    bytes_per_launch = accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
-                                            sizes["n_vms"], sizes["n_pods"])
+    # roofline numerator per interval: the K-interval one-launch path reads the engine state
+    # once and carries it on chip, so its algorithmic bytes are fewer (kacc_intervals_bytes)
+    fused = accel.fused_intervals(layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES, K, args.node_order, Z)
+    bytes_per_launch = accel.intervals_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"], sizes["n_vms"],
+                                             sizes["n_pods"], K, fused) / K
     k_avg_ms = float(np.mean(kernel_ms))
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
 
@@ -368,8 +373,13 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
-            "bytes_per_launch": bytes_per_launch,
-            "kernel": (f"kacc::small_kernel<{Z}> (one launch per step, one wavefront per node: every node "
+            "bytes_per_interval": bytes_per_launch,
+            "bytes_per_interval_unfused": accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
+                                                               sizes["n_vms"], sizes["n_pods"]),
+            "kernel": (f"kacc::intervals_carry_kernel<{Z},0,{256 if layout.fast_flag() & accel.KACC_F_MEDIUM_NODES else 512}>"
+                       f" ({K} intervals in one launch, state carried on chip; "
+                       f"achieved = kacc_intervals_bytes(carried) / K per interval)" if fused else
+                       f"kacc::small_kernel<{Z}> (one launch per step, one wavefront per node: every node "
                        f"fits KACC_F_SMALL_NODES)" if layout.fast_flag() & accel.KACC_F_SMALL_NODES else
                        f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, "
                        f"KACC_F_FAST_NODES)" if layout.fast_flag() else

@@ -96,10 +96,31 @@ extern "C" {
                                     KACC_F_FAST_NODES.  A node that does not fit
                                     is not computed and raises KACC_ERANGE (bit
                                     32).  kacc_batch_submit sets it by itself. */
+#define KACC_F_NODE_SLOT_RANGES 0x10u /* caller guarantees every workload slot the
+                                          batch's rows and aggregates use belongs to
+                                          one node only for the whole call (the
+                                          per-node slot ranges of kacc_slot_join).
+                                          With KACC_F_FAST_NODES on every batch of a
+                                          kacc_run_intervals call, the K intervals
+                                          run as ONE launch (each node carried
+                                          through K intervals by one workgroup);
+                                          results are bit-identical.            */
+#define KACC_F_MEDIUM_NODES 0x20u /* caller guarantees every node has at most
+                                     KACC_MEDIUM_MAX_PROCS process rows and at
+                                     most KACC_MEDIUM_MAX_AGGREGATES containers+
+                                     VMs+pods; implies KACC_F_FAST_NODES.  The
+                                     one-launch K-interval path then runs 256-
+                                     thread workgroups (four per CU: a 1k-node
+                                     shard resident at once).  A node that does
+                                     not fit is not computed and raises
+                                     KACC_ERANGE (bit 32).  kacc_batch_submit
+                                     sets it by itself.                      */
 #define KACC_FAST_MAX_PROCS 2048u
 #define KACC_FAST_MAX_AGGREGATES 512u
 #define KACC_SMALL_MAX_PROCS 512u
 #define KACC_SMALL_MAX_AGGREGATES 128u
+#define KACC_MEDIUM_MAX_PROCS 1024u
+#define KACC_MEDIUM_MAX_AGGREGATES 256u
 
 typedef struct kacc_ctx kacc_ctx;
 
@@ -231,7 +252,10 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *dev_batch, void *strea
  * order on `stream`: interval k+1 sees the state interval k wrote, exactly as
  * `count` kacc_run_interval calls, but issued back to back from C (fleet
  * replay; BASELINE config 5: 60 batched intervals with counter wraparound).
- * Every descriptor's shape is checked before the first launch.               */
+ * Every descriptor's shape is checked before the first launch.  When every
+ * descriptor has KACC_F_FAST_NODES | KACC_F_NODE_SLOT_RANGES (not
+ * KACC_F_SMALL_NODES), the same n_nodes and no node_order, the K intervals
+ * are one kernel launch (bit-identical to K launches).                      */
 int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t count, void *stream);
 int kacc_sync(kacc_ctx *ctx, void *stream);
 
@@ -570,6 +594,12 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
                       const char *labels, const uint64_t *label_off, const uint32_t *row_order,
                       uint64_t *line_off, char *out, uint64_t out_cap, uint64_t *total, void *stream);
 
+/* Algorithmic HBM bytes of K consecutive intervals of these sizes: K times
+ * kacc_interval_bytes, or (carried != 0: kacc_run_intervals' one-launch path,
+ * which reads the engine state a node / row / aggregate needs once and carries
+ * it on chip while the slots stay put) that minus K-1 state reads.          */
+uint64_t kacc_intervals_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,
+                              uint64_t n_vms, uint64_t n_pods, uint32_t intervals, int carried);
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
  * sizes (the roofline numerator).                  */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,

@@ -42,8 +42,12 @@ KACC_F_TRUSTED_LAYOUT = 0x4
 KACC_FAST_MAX_PROCS = 2048
 KACC_FAST_MAX_AGGREGATES = 512
 KACC_F_SMALL_NODES = 0x8
+KACC_F_NODE_SLOT_RANGES = 0x10
 KACC_SMALL_MAX_PROCS = 512
 KACC_SMALL_MAX_AGGREGATES = 128
+KACC_F_MEDIUM_NODES = 0x20
+KACC_MEDIUM_MAX_PROCS = 1024
+KACC_MEDIUM_MAX_AGGREGATES = 256
 KACC_UNIQUE_ID_BYTES = 128
 KACC_PROC_REGULAR, KACC_PROC_CONTAINER, KACC_PROC_VM = 0, 1, 2
 KACC_KEY_TOMB = 0xFFFFFFFFFFFFFFFE
@@ -123,6 +127,7 @@ EXPORTS = [
     "kacc_allreduce_namespaces",
     "kacc_gather_pods",
     "kacc_last_error_copy",
+    "kacc_intervals_bytes",
     "kacc_interval_bytes",
 ]
 
@@ -283,7 +288,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     ]
     lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
     lib.kacc_interval_bytes.restype = c_uint64
+    lib.kacc_intervals_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_int]
+    lib.kacc_intervals_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
+    lib.kacc_debug_run_intervals_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_uint32, c_void_p, c_int]
+    lib.kacc_debug_carry_stamps.argtypes = [c_void_p, POINTER(KaccInterval), c_uint32, c_void_p, c_int, c_void_p]
     lib.kacc_format_values.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p]
     lib.kacc_zone_agg_create.argtypes = [c_void_p, c_uint32, c_uint32, c_void_p, POINTER(c_void_p)]
     lib.kacc_zone_agg_destroy.argtypes = [c_void_p]
@@ -362,6 +371,20 @@ def pack(rec_off, pid, cpu_delta, ptype, ctr_key, vm_key, pod_key=None, pod_ns=N
 
 def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int) -> int:
     return int(load().kacc_interval_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods))
+
+
+def intervals_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int, intervals: int,
+                    carried: bool) -> int:
+    return int(load().kacc_intervals_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods, intervals, int(carried)))
+
+
+KACC_CARRY_MAX_ZONES = 2
+
+
+def fused_intervals(flags: int, intervals: int, node_order: bool = False, zones: int = 2) -> bool:
+    """Whether kacc_run_intervals runs these K intervals as one carried-state launch."""
+    return (intervals > 1 and zones <= KACC_CARRY_MAX_ZONES and bool(flags & KACC_F_FAST_NODES)
+            and bool(flags & KACC_F_NODE_SLOT_RANGES) and not flags & KACC_F_SMALL_NODES and not node_order)
 
 
 def make_interval(arrays: dict, sizes: dict, flags: int = 0, ptr=None) -> KaccInterval:
@@ -458,6 +481,19 @@ class Accel:
         """Timing ablation (kacc_debug.h); variant != 0 is not the reference semantics."""
         self._check(self.lib.kacc_debug_run_variant(self.ctx, ctypes.byref(dev_interval),
                                                     c_void_p(stream or None), variant))
+
+    def run_intervals_variant(self, dev_intervals, stream: int, variant: int) -> None:
+        """Timing ablation of the one-launch K-interval kernel (kacc_debug.h); variant != 0 is not
+        the reference semantics."""
+        arr = (KaccInterval * len(dev_intervals))(*dev_intervals)
+        self._check(self.lib.kacc_debug_run_intervals_variant(self.ctx, arr, len(dev_intervals),
+                                                              c_void_p(stream or None), variant))
+
+    def carry_stamps(self, dev_intervals, stream: int, variant: int, d_out: int) -> None:
+        """Per-wave phase cycle totals of the carry kernel into d_out (kacc_debug.h; diagnostic)."""
+        arr = (KaccInterval * len(dev_intervals))(*dev_intervals)
+        self._check(self.lib.kacc_debug_carry_stamps(self.ctx, arr, len(dev_intervals), c_void_p(stream or None),
+                                                     variant, c_void_p(d_out)))
 
     def sync(self, stream: int = 0) -> None:
         self._check(self.lib.kacc_sync(self.ctx, c_void_p(stream or None)))

@@ -35,50 +35,6 @@ namespace cluster {
 
 constexpr int kThreads = 256;
 
-// Cluster node totals of one context: block b reduces table b / Z, zone b % Z
-// over the context's nodes.  Lane l sums nodes l, l+256, ... in order, then a
-// halving tree (l += l+s, s = 128..1): a fixed order, so the f64 sums are
-// reproducible run to run; u64 sums are modular and order independent.
-//   out_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal
-//   out_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower
-template <int Z>
-__global__ __launch_bounds__(kThreads) void node_totals_kernel(uint64_t n_nodes, const uint64_t *active_total,
-                                                               const uint64_t *idle_total, const double *power,
-                                                               const double *active_power,
-                                                               const double *idle_power, uint64_t *out_e,
-                                                               double *out_p) {
-  __shared__ double red_p[kThreads];
-  __shared__ unsigned long long red_e[kThreads];
-  const uint32_t tab = blockIdx.x / Z, z = blockIdx.x % Z, t = threadIdx.x;
-  if (tab < 2) {
-    const uint64_t *src = tab == 0 ? active_total : idle_total;
-    unsigned long long s = 0;
-    for (uint64_t n = t; n < n_nodes; n += kThreads) s += src[n * Z + z];
-    red_e[t] = s;
-  } else {
-    const double *src = tab == 2 ? power : tab == 3 ? active_power : idle_power;
-    double s = 0.0;
-    for (uint64_t n = t; n < n_nodes; n += kThreads) s = s + src[n * Z + z];
-    red_p[t] = s;
-  }
-  __syncthreads();
-  for (uint32_t s = kThreads / 2; s >= 1; s >>= 1) {
-    if (t < s) {
-      if (tab < 2)
-        red_e[t] += red_e[t + s];
-      else
-        red_p[t] = red_p[t] + red_p[t + s];
-    }
-    __syncthreads();
-  }
-  if (t == 0) {
-    if (tab < 2)
-      out_e[tab * Z + z] = red_e[0];
-    else
-      out_p[(tab - 2) * Z + z] = red_p[0];
-  }
-}
-
 // acc += add, element-wise (u64 modular, f64 one rounding per element).
 __global__ __launch_bounds__(kThreads) void accumulate_kernel(uint64_t n_e, uint64_t *acc_e, const uint64_t *add_e,
                                                               uint64_t n_p, double *acc_p, const double *add_p) {
@@ -159,28 +115,6 @@ int cluster_scratch(kacc_cluster *c) {
 
 hipStream_t shard_stream(const kacc_cluster *c, void *const *streams, size_t s) {
   return (streams && streams[s]) ? static_cast<hipStream_t>(streams[s]) : c->shards[s]->stream;
-}
-
-template <int Z>
-void launch_node_totals(kacc_ctx *x, uint64_t *oe, double *op, hipStream_t st) {
-  hipLaunchKernelGGL((kacc::cluster::node_totals_kernel<Z>), dim3(5 * Z), dim3(kacc::cluster::kThreads), 0, st,
-                     x->cfg.nodes, (const uint64_t *)x->tables[KACC_T_NODE_ACTIVE_TOTAL],
-                     (const uint64_t *)x->tables[KACC_T_NODE_IDLE_TOTAL], (const double *)x->tables[KACC_T_NODE_POWER],
-                     (const double *)x->tables[KACC_T_NODE_ACTIVE_POWER],
-                     (const double *)x->tables[KACC_T_NODE_IDLE_POWER], oe, op);
-}
-
-void node_totals(kacc_ctx *x, uint64_t *oe, double *op, hipStream_t st) {
-  switch (x->cfg.zones) {
-    case 1: launch_node_totals<1>(x, oe, op, st); break;
-    case 2: launch_node_totals<2>(x, oe, op, st); break;
-    case 3: launch_node_totals<3>(x, oe, op, st); break;
-    case 4: launch_node_totals<4>(x, oe, op, st); break;
-    case 5: launch_node_totals<5>(x, oe, op, st); break;
-    case 6: launch_node_totals<6>(x, oe, op, st); break;
-    case 7: launch_node_totals<7>(x, oe, op, st); break;
-    default: launch_node_totals<8>(x, oe, op, st); break;
-  }
 }
 
 template <int Z>
@@ -432,20 +366,15 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
     if (nodes && (!out_node_energy[s] || !out_node_power[s]))
       return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL node-total array", s);
   }
-  // 1. partial vectors of every shard, on its stream
+  // 1. partial vectors of every shard, on its stream: namespace sums and node
+  //    totals in one launch per shard
   for (size_t s = 0; s < ns; ++s) {
     kacc_ctx *x = c->shards[s];
     hipStream_t st = shard_stream(c, streams, s);
-    if (n_ns) {
-      const int rc = kacc_namespace_totals(x, n_ns, ns_pod_off[s], ns_pod_slot[s], out_energy[s], out_power[s], st);
-      if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
-    }
-    if (nodes) {
-      KACC_HIP(c0, hipSetDevice(x->device));
-      (void)hipGetLastError();
-      node_totals(x, out_node_energy[s], out_node_power[s], st);
-      KACC_HIP(c0, hipGetLastError());
-    }
+    const int rc = kacc_internal_cluster_partials(
+        x, n_ns, n_ns ? ns_pod_off[s] : nullptr, n_ns ? ns_pod_slot[s] : nullptr, n_ns ? out_energy[s] : nullptr,
+        n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr, st);
+    if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
   }
   // 2. shards of one GPU (on the compute streams)
   int rc = KACC_OK;

@@ -12,6 +12,17 @@ extern "C" {
  * 9 = 1|8.  Variants != 0 do not compute the reference semantics.          */
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream, int variant);
 
+/* Per-wave s_memtime phase totals of the carry kernel (Z = 2; variant 0 or 2) into
+ * d_out[n_nodes][8][8] (diagnostic; results are the reference's).             */
+int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *batches, uint32_t count, void *stream,
+                            int variant, uint64_t *d_out);
+/* One-launch K-interval kernel ablation (Z = 2; the FAST or MEDIUM shape from the
+ * flags): 0 = production, 1 = no process-row stores, 2 = rows prefetched an interval
+ * ahead into registers, 4 = no aggregates, 5 = 1|4, 8 = never take the moved path.
+ * Variants 1, 4, 5, 8 do not compute the reference results.                   */
+int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *batches, uint32_t count, void *stream,
+                                     int variant);
+
 /* Slot join timing ablation: stop_after = k returns after phase k (1 load,
  * 2 lookups, 3 terminated, 4 allocation, 5 inserts); 0 = the full join.    */
 int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,

@@ -22,7 +22,11 @@ __device__ __forceinline__ int64_t cvttsd2sq(double x) {
 
 // Go float64 -> uint64 conversion on amd64 (cmd/compile ssagen
 // float64ToUint64): x < 2^63 ? int64(x) : int64(x - 2^63) | 1<<63.
+// Energies of one interval fit 32 bits (4.29e9 µJ) almost always: for x in
+// (-1, 2^32) truncation is one v_cvt_u32_f64 (the same value as CVTTSD2SQ), and
+// the general expansion runs only when some lane of the wave needs it.
 __device__ __forceinline__ uint64_t go_f64_to_u64(double x) {
+  if (__builtin_expect(x > -1.0 && x < 4294967296.0, 1)) return static_cast<uint32_t>(x);
   if (x < kTwo63) return static_cast<uint64_t>(cvttsd2sq(x));
   return static_cast<uint64_t>(cvttsd2sq(x - kTwo63)) | 0x8000000000000000ull;
 }

@@ -427,9 +427,9 @@ __device__ __forceinline__ bool fits_fast(const NodeRanges &r) {
          (r.c1 - r.c0) + (r.v1 - r.v0) + (r.q1 - r.q0) <= static_cast<uint32_t>(kTpb<V>);
 }
 
+// One node snapshot of one interval on workgroup `blk` (interval_kernel).
 template <int Z, int V>
-__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : 6)
-void interval_kernel(const kacc_interval b, const DevState st) {
+__device__ __forceinline__ void interval_node(const kacc_interval &b, const DevState &st, const uint32_t blk) {
   constexpr int kThreads = kTpb<V>;
   constexpr int kRowsPerThread = kRpt<V>;
   // non-temporal hints on the row streams (read once / written once per
@@ -448,9 +448,9 @@ void interval_kernel(const kacc_interval b, const DevState st) {
   const int tid = threadIdx.x;
   // the previous interval's pod_kernel has drained the deferred list; this
   // interval's chunk_kernel refills it after this kernel
-  if (blockIdx.x == 0 && tid == 0) st.defer_ctr[0] = 0u;
-  uint32_t n = blockIdx.x;
-  if (b.node_order) n = b.node_order[blockIdx.x];
+  if (blk == 0 && tid == 0) st.defer_ctr[0] = 0u;
+  uint32_t n = blk;
+  if (b.node_order) n = b.node_order[blk];
   if (n >= b.n_nodes) {
     if (tid == 0) raise_err(st.err, kErrNode);
     return;
@@ -638,9 +638,13 @@ void interval_kernel(const kacc_interval b, const DevState st) {
     if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
   } else {
     // lane l < 256 sums rows l, l+256, l+512, ... in order; then the halving tree
-    if (tid < kTree) {
+    if (tid < kTree) {  // all reads in flight; +0.0 past the node's end is an identity
+      double v[kRowsLds / kTree];
+#pragma unroll
+      for (int u = 0; u < kRowsLds / kTree; ++u) v[u] = s_d[tid + kTree * u];
       double s = 0.0;
-      for (uint32_t r = tid; r < rows; r += kTree) s = s + s_d[r];
+#pragma unroll
+      for (int u = 0; u < kRowsLds / kTree; ++u) s = s + (tid + kTree * u < rows ? v[u] : 0.0);
       red[tid] = s;
     }
     __syncthreads();
@@ -760,6 +764,561 @@ void interval_kernel(const kacc_interval b, const DevState st) {
     }
   }
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
+}
+
+template <int Z, int V>
+__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : 6)
+void interval_kernel(const kacc_interval b, const DevState st) {
+  interval_node<Z, V>(b, st, blockIdx.x);
+}
+
+// ============ K intervals in one launch, state carried on chip ====================
+// intervals_carry_kernel: the same node snapshot (fast path, per-row slot
+// accesses) for K consecutive intervals, one workgroup per node, with
+//   * the node's state (has_prev, last timestamp, zone counters and active /
+//     idle totals) carried in registers;
+//   * every row's last written totals carried in LDS (s_cw / s_cE, keyed by
+//     the row position and its slot word) and every aggregate's in registers:
+//     when interval k+1 gives a position the slot it had in interval k (the
+//     steady state: the slot join keeps a running workload's slot), its
+//     previous total is on chip — no 8Z-byte reload per row;
+//   * interval k+1's inputs (offsets, Δ, slot words, aggregate descriptors,
+//     node readings) loaded into registers during interval k (staged into LDS
+//     at the top of k+1), and LDS-only barriers inside an interval, so neither
+//     the prefetch nor interval k's stores are waited on before use.
+// A position whose slot changed (churn moved rows, aggregates appeared)
+// makes the workgroup take one full barrier (its earlier stores complete and
+// become visible) and reload those previous totals from the tables.
+// Arithmetic, order and outputs are interval_node's, bit for bit.  Z <= 2 (the
+// carried totals take 16Z KiB of LDS: two workgroups per CU at Z = 2).
+constexpr int kCarryMaxZ = 2;
+
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Descriptors read from memory hold generic pointers: flat loads, which also
+// count on lgkmcnt, so every LDS wait would drain the prefetch.  Every array of
+// a batch is global memory: say so.
+#define KACC_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const T KACC_GLOBAL *gbl(const T *p) {
+  return (const T KACC_GLOBAL *)p;
+}
+
+// An index the compiler must treat as per-lane: loads through it are vector
+// loads (vmcnt, waited for at the first use of the value) rather than scalar
+// loads (lgkmcnt, which every LDS wait drains).
+__device__ __forceinline__ uint32_t lane_index(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+// The wait for a prefetched register happens here (ahead of the interval's
+// stores, so that it never waits on them).
+template <typename T>
+__device__ __forceinline__ void land(const T &x) {
+  asm volatile("" ::"v"(x));
+}
+// What an empty array or an absent optional input reads (never written).
+__device__ const uint64_t kacc_zero_words[2] = {0ull, 0ull};
+__device__ __forceinline__ const uint32_t *zero_u32() { return reinterpret_cast<const uint32_t *>(kacc_zero_words); }
+__device__ __forceinline__ const double *zero_f64() { return reinterpret_cast<const double *>(kacc_zero_words); }
+
+// Node inputs of up to kCarryChunk + 1 consecutive intervals, staged in LDS
+// once per chunk (one memory round trip per kCarryChunk intervals): the row
+// offsets, readings and status of node n.  Entry e is interval c + e (the last
+// interval repeated past K).
+// Two shapes: T = 512 threads for KACC_F_FAST_NODES (2048 rows, 512 aggregates)
+// and T = 256 for KACC_F_MEDIUM_NODES (1024 rows, 256 aggregates: four
+// workgroups per CU, so a 1k-node shard is resident in one round).
+constexpr int kCarryRpt = 4;  // row positions per lane
+template <int T>
+constexpr int kCarryEntries = T / 8;  // one offset word per lane
+template <int T>
+constexpr int kCarryChunk = kCarryEntries<T> - 1;  // + the lookahead entry the row prefetch reads
+template <int Z, int T>
+struct CarryTables {
+  uint32_t off[kCarryEntries<T> * 8];
+  uint32_t status[kCarryEntries<T>];
+  int64_t ts[kCarryEntries<T>];
+  double ratio[kCarryEntries<T>], nd_given[kCarryEntries<T>];
+  uint64_t ze[kCarryEntries<T> * Z], zm[kCarryEntries<T> * Z];
+};
+// A node's rows and this lane's aggregate descriptor (raw; loaded an interval
+// ahead): resolved at use, so that no instruction reads them right after the load.
+template <int Z>
+struct CarryRows {
+  double d[kCarryRpt];
+  uint32_t w[kCarryRpt];
+  uint32_t ce, cb, cw, ve, vb, vw, qe, qb, qw, cre;
+};
+
+template <int Z, int T>
+__device__ __forceinline__ void fill_tables(const kacc_interval *bs, uint32_t K, uint32_t c, uint32_t n,
+                                            CarryTables<Z, T> &t) {
+  const uint32_t tid = threadIdx.x;
+  {
+    const uint32_t e = tid >> 3, f = tid & 7u;
+    const kacc_interval &b = bs[lane_index(min(c + e, K - 1))];
+    const uint32_t *arr = f < 2 ? b.proc_off : f < 4 ? b.ctr_off : f < 6 ? b.vm_off : b.pod_off;
+    t.off[tid] = gbl(arr)[n + (f & 1u)];
+  }
+  if (tid < static_cast<uint32_t>(kCarryEntries<T>)) {
+    const kacc_interval &b = bs[lane_index(min(c + tid, K - 1))];
+    t.status[tid] = b.node_status ? gbl(b.node_status)[n] : 0u;
+    t.ts[tid] = gbl(b.node_ts_ns)[n];
+    t.ratio[tid] = gbl(b.node_usage_ratio)[n];
+    t.nd_given[tid] = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) ? gbl(b.node_cpu_delta)[n] : 0.0;
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      t.ze[tid * Z + z] = gbl(b.zone_energy)[static_cast<uint64_t>(n) * Z + z];
+      t.zm[tid * Z + z] = gbl(b.zone_max)[static_cast<uint64_t>(n) * Z + z];
+    }
+  }
+}
+
+// Row ranges from raw offsets (uniform), clamped as node_ranges() does; a
+// malformed batch is reported at use.
+__device__ __forceinline__ NodeRanges carry_ranges(const kacc_interval &b, const uint32_t *o, uint32_t &bad) {
+  NodeRanges r{uniform_u32(o[0]), uniform_u32(o[1]), uniform_u32(o[2]), uniform_u32(o[3]),
+               uniform_u32(o[4]), uniform_u32(o[5]), uniform_u32(o[6]), uniform_u32(o[7])};
+  bad = 0u;
+  if (r.p1 > b.n_procs || r.p0 > r.p1 || r.c1 > b.n_ctrs || r.c0 > r.c1 || r.v1 > b.n_vms || r.v0 > r.v1 ||
+      r.q1 > b.n_pods || r.q0 > r.q1) {
+    bad = 1u;
+    r.p1 = min(r.p1, b.n_procs);
+    r.p0 = min(r.p0, r.p1);
+    r.c1 = min(r.c1, b.n_ctrs);
+    r.c0 = min(r.c0, r.c1);
+    r.v1 = min(r.v1, b.n_vms);
+    r.v0 = min(r.v0, r.v1);
+    r.q1 = min(r.q1, b.n_pods);
+    r.q0 = min(r.q0, r.q1);
+  }
+  return r;
+}
+
+// Every load unconditional from a clamped index into the node's own rows (lanes
+// past the node's end re-read its last row: one cache line), empty arrays read
+// the zero words: no branch, and no instruction touches a loaded value here.
+template <int Z, int T>
+__device__ __forceinline__ void load_rows(const kacc_interval &b, const NodeRanges &r, CarryRows<Z> &o) {
+  constexpr int kThreads = T, kR = kCarryRpt;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t rows = r.p1 - r.p0, nc = r.c1 - r.c0, nv = r.v1 - r.v0, nq = r.q1 - r.q0;
+  {
+    const bool has = b.n_procs != 0;
+    const double *pd = has ? b.proc_cpu_delta : zero_f64();
+    const uint32_t *pw = has ? b.proc_slot : zero_u32();
+    const uint32_t hi = !has ? 0u : rows ? r.p1 - 1 : min(r.p0, b.n_procs - 1);
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const uint32_t at = lane_index(min(r.p0 + tid + k * kThreads, hi));
+      o.d[k] = __builtin_nontemporal_load(gbl(pd) + at);
+      o.w[k] = __builtin_nontemporal_load(gbl(pw) + at);
+    }
+  }
+  {  // containers: lanes [0, nc)
+    const bool has = b.n_ctrs != 0;
+    const uint32_t *pe = has ? b.ctr_proc_end : zero_u32();
+    const uint32_t *ps = has ? b.ctr_slot : zero_u32();
+    const uint32_t last = has ? b.n_ctrs - 1 : 0u;
+    const uint32_t at = lane_index(min(r.c0 + min(tid, nc ? nc - 1 : 0u), last));
+    o.ce = gbl(pe)[at];
+    o.cb = gbl(pe)[at ? at - 1 : 0u];
+    o.cw = gbl(ps)[at];
+    o.cre = gbl(pe)[lane_index(nc ? min(r.c1 - 1, last) : 0u)];  // the VM rows' start when nc > 0
+  }
+  {  // VMs: lanes [nc, nc + nv)
+    const bool has = b.n_vms != 0;
+    const uint32_t *pe = has ? b.vm_proc_end : zero_u32();
+    const uint32_t *ps = has ? b.vm_slot : zero_u32();
+    const uint32_t last = has ? b.n_vms - 1 : 0u;
+    const uint32_t j = tid >= nc ? min(tid - nc, nv ? nv - 1 : 0u) : 0u;
+    const uint32_t at = lane_index(min(r.v0 + j, last));
+    o.ve = gbl(pe)[at];
+    o.vb = gbl(pe)[at ? at - 1 : 0u];
+    o.vw = gbl(ps)[at];
+  }
+  {  // pods: lanes [nc + nv, nc + nv + nq)
+    const bool has = b.n_pods != 0;
+    const uint32_t *pe = has ? b.pod_ctr_end : zero_u32();
+    const uint32_t *ps = has ? b.pod_slot : zero_u32();
+    const uint32_t last = has ? b.n_pods - 1 : 0u;
+    const uint32_t j = tid >= nc + nv ? min(tid - nc - nv, nq ? nq - 1 : 0u) : 0u;
+    const uint32_t at = lane_index(min(r.q0 + j, last));
+    o.qe = gbl(pe)[at];
+    o.qb = gbl(pe)[at ? at - 1 : 0u];
+    o.qw = gbl(ps)[at];
+  }
+}
+
+template <int Z>
+__device__ __forceinline__ void land_rows(const CarryRows<Z> &o) {
+#pragma unroll
+  for (int k = 0; k < kCarryRpt; ++k) {
+    land(o.d[k]);
+    land(o.w[k]);
+  }
+  land(o.ce), land(o.cb), land(o.cw), land(o.ve), land(o.vb), land(o.vw), land(o.qe), land(o.qb), land(o.qw);
+  land(o.cre);
+}
+
+// Timing ablations of intervals_carry_kernel (kacc_debug_run_intervals_variant; a
+// variant != 0 does NOT compute the reference results).
+constexpr int kCarryNoRowStores = 1;   // no process-row stores
+constexpr int kCarryPrefetch = 2;      // rows loaded an interval ahead into registers (measured
+                                       // slower at four workgroups per CU: profiles/r02/carry_*)
+constexpr int kCarryNoAggregates = 4;  // containers / VMs / pods skipped
+constexpr int kCarryNeverMoved = 8;    // never take the moved path (no barrier, no reload)
+constexpr int kCarryStamps = 16;       // per-wave s_memtime phase totals into st.items (diagnostic)
+constexpr int kCarryPhases = 8;
+
+template <int Z, int V = 0, int T = 512>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void intervals_carry_kernel(const kacc_interval *__restrict__ bs,
+                                                                        const uint32_t K, const DevState st) {
+  static_assert(Z <= kCarryMaxZ, "carried totals are sized for Z <= kCarryMaxZ");
+  static_assert(T == 512 || T == 256, "carry shapes: FAST (512) and MEDIUM (256)");
+  constexpr int kThreads = T, kR = kCarryRpt, kRows = kR * T;
+  constexpr bool kPrefetch = (V & kCarryPrefetch) != 0;
+  __shared__ double s_d[kRows];        // this interval's Δ
+  __shared__ uint32_t s_w[kRows];      // and slot words
+  __shared__ uint32_t s_cw[kRows];     // carried: the slot word last written at each position
+  __shared__ uint64_t s_cE[kRows * Z]; // carried: the totals written there
+  __shared__ double s_cd[kThreads];
+  __shared__ double s_ct[kThreads];
+  __shared__ NodeShared sh;
+  __shared__ uint32_t s_moved;
+  const uint32_t tid = threadIdx.x, n = blockIdx.x;
+  if (n == 0 && tid == 0) st.defer_ctr[0] = 0u;
+  uint64_t t_acc[kCarryPhases] = {};
+  uint64_t t_last = (V & kCarryStamps) ? __builtin_amdgcn_s_memtime() : 0;
+  auto mark = [&](int ph) {
+    if constexpr ((V & kCarryStamps) != 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      t_acc[ph] += t - t_last;
+      t_last = t;
+    }
+  };
+  // carried node state: zone tid (< Z) and the node scalars (every lane)
+  const uint64_t zi = static_cast<uint64_t>(n) * Z + (tid < static_cast<uint32_t>(Z) ? tid : 0u);
+  uint32_t c_has_prev = st.node_has_prev[n];
+  int64_t c_ts = st.node_ts[n];
+  uint64_t c_etot = st.node_energy_total[zi], c_atot = st.node_active_total[zi], c_itot = st.node_idle_total[zi];
+  // carried aggregate (one per lane)
+  uint32_t c_role = 0, c_aw = 0xffffffffu;
+  uint64_t c_aE[Z];
+  double c_atotal = 0.0;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) c_aE[z] = 0;
+#pragma unroll
+  for (int j = 0; j < kR; ++j) s_cw[tid + j * kThreads] = 0xffffffffu;
+  if (tid == 0) s_moved = 0;
+
+  // node inputs staged in LDS per chunk of intervals; the rows one interval ahead
+  __shared__ CarryTables<Z, T> tab;
+  CarryRows<Z> rw;
+  fill_tables<Z, T>(bs, K, 0u, n, tab);
+  lds_barrier();
+  {
+    uint32_t bad;
+    load_rows<Z, T>(bs[0], carry_ranges(bs[0], tab.off, bad), rw);
+  }
+  for (uint32_t k = 0, c = 0; k < K; ++k) {
+    if (k - c == static_cast<uint32_t>(kCarryChunk<T>)) {  // block-uniform: the next chunk's inputs
+      c = k;
+      fill_tables<Z, T>(bs, K, c, n, tab);
+      lds_barrier();
+    }
+    mark(7);
+    const uint32_t e = k - c;
+    const kacc_interval &b = bs[k];
+    if constexpr (!kPrefetch) {
+      if (k > 0) {
+        uint32_t bad;
+        load_rows<Z, T>(b, carry_ranges(b, tab.off + e * 8, bad), rw);
+      }
+    }
+    uint32_t bad_offsets;
+    const NodeRanges rg = carry_ranges(b, tab.off + e * 8, bad_offsets);
+    const uint32_t p0 = rg.p0, p1 = rg.p1, c0 = rg.c0, c1 = rg.c1, q0 = rg.q0, q1 = rg.q1;
+    const uint32_t rows = p1 - p0, nc = c1 - c0, nv = rg.v1 - rg.v0, nq = q1 - q0;
+    const bool fits = rows <= static_cast<uint32_t>(kRows) && nc + nv + nq <= static_cast<uint32_t>(kThreads);
+    // this interval's node inputs (uniform ones to SGPRs) and this lane's aggregate
+    const uint32_t status = uniform_u32(tab.status[e]);
+    const int64_t ts = static_cast<int64_t>(uniform_u64(static_cast<uint64_t>(tab.ts[e])));
+    const double ratio = uniform_f64(tab.ratio[e]), nd_given = uniform_f64(tab.nd_given[e]);
+    const uint32_t zl = tid < static_cast<uint32_t>(Z) ? tid : 0u;
+    const uint64_t ze = tab.ze[e * Z + zl], zm = tab.zm[e * Z + zl];
+    const bool is_c = tid < nc, is_v = !is_c && tid < nc + nv, is_q = !is_c && !is_v && tid < nc + nv + nq;
+    const uint32_t a_beg0 = is_c   ? (tid == 0 ? p0 : rw.cb)
+                            : is_v ? (tid == nc ? (nc ? rw.cre : p0) : rw.vb)
+                            : is_q ? (tid == nc + nv ? c0 : rw.qb)
+                                   : 0u;
+    const uint32_t a_end0 = is_c ? rw.ce : is_v ? rw.ve : is_q ? rw.qe : 0u;
+    const uint32_t a_w = is_c ? rw.cw : is_v ? rw.vw : is_q ? rw.qw : 0xffffffffu;
+    bool moved = false;
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {  // stage the rows (LDS of interval k-1 is free: barrier at its end)
+      const uint32_t r = tid + j * kThreads;
+      if (r < rows && fits) {
+        s_d[r] = rw.d[j];
+        s_w[r] = rw.w[j];
+        moved |= (rw.w[j] & KACC_SLOT_MASK) != (s_cw[r] & KACC_SLOT_MASK);
+      }
+    }
+    const uint32_t flags = b.flags;
+    // in flight during interval k: rows and node inputs of k+1, offsets of k+2
+    // (a past-the-end interval re-reads the last one: no branch)
+    if constexpr (kPrefetch) {
+      const uint32_t k1 = min(k + 1, K - 1);
+      uint32_t bad;
+      load_rows<Z, T>(bs[k1], carry_ranges(bs[k1], tab.off + (k1 - c) * 8, bad), rw);
+    }
+    if (bad_offsets) {
+      if (tid == 0) raise_err(st.err, kErrOffsets);
+    }
+    if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44: previous snapshot kept
+      if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+    } else if (!fits) {  // the caller's KACC_F_FAST_NODES promise was wrong
+      if (tid == 0) raise_err(st.err, kErrBigNode);
+    } else {
+      // ---- this lane's aggregate; did any position move? ---------------------------------
+      const uint32_t role = (V & kCarryNoAggregates) ? 0u : is_c ? 1u : is_v ? 2u : is_q ? 3u : 0u;
+      const uint32_t a_s = a_w & KACC_SLOT_MASK;
+      const uint64_t a_cap = role == 1 ? st.ctr_slots : role == 2 ? st.vm_slots : role == 3 ? st.pod_slots : 0;
+      const bool a_ok = role != 0 && a_s < a_cap;
+      if (role != 0 && !a_ok) raise_err(st.err, kErrSlot);
+      const bool a_moved = a_ok && (role != c_role || a_s != (c_aw & KACC_SLOT_MASK));
+      moved |= a_moved;
+      if (__any(moved) && (tid & 63) == 0) s_moved = 1u;
+      mark(0);
+      lds_barrier();  // s_d / s_w staged, s_moved set
+      mark(1);
+      if ((V & kCarryNeverMoved) == 0 && s_moved) {  // block-uniform: the rare path
+        __syncthreads();  // this workgroup's earlier stores complete and visible (and ordered)
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+          const uint32_t r = tid + j * kThreads;
+          if (r >= rows) continue;
+          const uint32_t sw = s_w[r];
+          const uint64_t sl = sw & KACC_SLOT_MASK;
+          if (sl == (s_cw[r] & KACC_SLOT_MASK)) continue;
+          uint64_t pv[Z];
+          if (sl < st.proc_slots) {
+            load_row<Z>(st.proc_energy, sl, pv);
+          } else {
+#pragma unroll
+            for (int z = 0; z < Z; ++z) pv[z] = 0;
+          }
+#pragma unroll
+          for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = pv[z];
+        }
+        if (a_moved) {
+          load_row<Z>(role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy, a_s, c_aE);
+          c_atotal = role == 1 ? st.ctr_cpu_total[a_s] : role == 3 ? st.pod_cpu_total[a_s] : 0.0;
+        }
+        lds_barrier();
+        if (tid == 0) s_moved = 0;
+      }
+      double a_total = (role != 2 && a_ok && !(a_w & KACC_SLOT_NEW)) ? c_atotal : 0.0;
+
+      // ---- A: node zones (node.go:10-84 / 101-131) from the carried state ------------------
+      const bool first = c_has_prev == 0u;
+      uint64_t z_active = 0;
+      double z_p = 0.0, z_ap = 0.0, z_ip = 0.0;
+      if (tid < static_cast<uint32_t>(Z)) {
+        if (first) {
+          z_active = go_f64_to_u64(u2f(ze) * ratio);
+          c_atot = z_active;
+          c_itot = ze - z_active;
+        } else {
+          const double dt = go_duration_seconds(go_sub_mono(ts, c_ts));
+          const uint64_t delta = energy_delta(ze, c_etot, zm);
+          z_active = go_f64_to_u64(u2f(delta) * ratio);
+          c_atot = c_atot + z_active;
+          c_itot = c_itot + (delta - z_active);
+          z_p = u2f(delta) / dt;
+          z_ap = z_p * ratio;
+          z_ip = z_p - z_ap;
+        }
+        c_etot = ze;
+        sh.active_energy[tid] = z_active;
+        sh.power[tid] = z_p;
+        sh.active_power[tid] = z_ap;
+        if (tid == 0) sh.first = first ? 1u : 0u;
+      }
+      // ---- B: ProcessTotalCPUTimeDelta (informer.go:330-333) by the last wave, while the
+      //      others sum containers: interval_kernel's canonical 256-leaf tree evaluated by
+      //      64 lanes as small_kernel does (lane t: leaves t, t+64, t+128, t+192, each the
+      //      in-order sum of rows l, l+256, ...) — the same additions in the same order
+      if (flags & KACC_F_NODE_CPU_DELTA_GIVEN) {
+        if (tid == 0) sh.node_delta = nd_given;
+      } else if (tid >= static_cast<uint32_t>(kThreads - 64)) {
+        const uint32_t t = tid - (kThreads - 64);
+        // a leaf's LDS reads issued together (r < kRows: in bounds); a row past the
+        // node's end adds +0.0, an identity on a sum that starts at +0.0
+        constexpr int kU = kRows / kTree, kB = kU < 4 ? kU : 4;  // reads in flight
+        double leaf[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          double sum = 0.0;
+#pragma unroll
+          for (int u0 = 0; u0 < kU; u0 += kB) {
+            double v[kB];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) v[u] = s_d[t + 64u * q + static_cast<uint32_t>(kTree) * (u0 + u)];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+              const uint32_t r = t + 64u * q + static_cast<uint32_t>(kTree) * (u0 + u);
+              sum = sum + (r < rows ? v[u] : 0.0);
+            }
+          }
+          leaf[q] = sum;
+        }
+        double x = (leaf[0] + leaf[2]) + (leaf[1] + leaf[3]);
+#pragma unroll
+        for (int s2 = 32; s2 >= 1; s2 >>= 1) x = x + __shfl_down(x, s2, 64);
+        if (t == 0) sh.node_delta = x;
+      }
+      // ---- C: containers and VMs (one lane per segment, listing order) -------------------
+      double a_delta = 0.0;
+      if (role == 1 || role == 2) {
+        uint32_t beg = a_beg0, end = a_end0;
+        if (beg < p0 || end < beg || end > p1) {
+          raise_err(st.err, kErrOffsets);
+          beg = max(min(beg, p1), p0);
+          end = max(min(end, p1), beg);
+        }
+        if (role == 1) {  // informer.go:229-233, 481-486: in order, 4 LDS reads in flight
+          uint32_t i = beg - p0;
+          const uint32_t e = end - p0;
+          for (; i + 4 <= e; i += 4) {
+            const double x0 = s_d[i], x1 = s_d[i + 1], x2 = s_d[i + 2], x3 = s_d[i + 3];
+            a_delta = a_delta + x0;
+            a_total = a_total + x0;
+            a_delta = a_delta + x1;
+            a_total = a_total + x1;
+            a_delta = a_delta + x2;
+            a_total = a_total + x2;
+            a_delta = a_delta + x3;
+            a_total = a_total + x3;
+          }
+          for (; i < e; ++i) {
+            const double di = s_d[i];
+            a_delta = a_delta + di;
+            a_total = a_total + di;
+          }
+          s_cd[tid] = a_ok ? a_delta : 0.0;
+          s_ct[tid] = a_ok ? a_total : 0.0;
+        } else {  // informer.go:445: the last process in listing order wins
+          a_delta = end > beg ? s_d[end - 1 - p0] : 0.0;
+        }
+      }
+      mark(2);
+      lds_barrier();
+      mark(3);
+      // ---- D: pods (informer.go:305-309, 502-507) -----------------------------------------
+      if (role == 3) {
+        uint32_t beg = a_beg0, end = a_end0;
+        if (beg < c0 || end < beg || end > c1) {
+          raise_err(st.err, kErrOffsets);
+          beg = max(min(beg, c1), c0);
+          end = max(min(end, c1), beg);
+        }
+        for (uint32_t c = beg - c0; c < end - c0; ++c) {
+          a_delta = a_delta + s_cd[c];
+          a_total = a_total + s_ct[c];  // quirk: the container's running total
+        }
+      }
+      // ---- E: attribution; the prefetch lands before the first store -----------------------
+      if constexpr (kPrefetch) {
+        land_rows<Z>(rw);
+      }
+      mark(4);
+      if (tid < static_cast<uint32_t>(Z)) {
+        st.node_active_total[zi] = c_atot;
+        st.node_idle_total[zi] = c_itot;
+        st.node_energy_total[zi] = ze;
+        st.node_active_energy[zi] = z_active;
+        st.node_power[zi] = z_p;
+        st.node_active_power[zi] = z_ap;
+        st.node_idle_power[zi] = z_ip;
+      }
+      const Attr<Z> a = make_attr<Z>(sh);
+      if (tid == 0) {
+        st.node_ts[n] = ts;
+        st.node_has_prev[n] = 1u;
+        st.node_usage_ratio[n] = a.first ? 0.0 : ratio;
+        st.node_cpu_delta[n] = a.nd;
+        st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
+      }
+      if (a_ok) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+        if (role == 1) {
+          st.ctr_cpu_delta[a_s] = a_delta;
+          st.ctr_cpu_total[a_s] = a_total;
+        } else if (role == 2) {
+          st.vm_cpu_delta[a_s] = a_delta;
+        } else {
+          st.pod_cpu_delta[a_s] = a_delta;
+          st.pod_cpu_total[a_s] = a_total;
+        }
+        uint64_t E[Z];
+        double P[Z];
+        attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, c_aE, E, P);
+        uint64_t *ae = role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy;
+        double *ap = role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
+        store_row<Z, true, uint64_t>(ae, a_s, E);
+        store_row<Z, true, double>(ap, a_s, P);
+#pragma unroll
+        for (int z = 0; z < Z; ++z) c_aE[z] = E[z];
+        c_atotal = a_total;
+      }
+      c_role = a_ok ? role : 0u;
+      c_aw = a_ok ? a_w : 0xffffffffu;
+#pragma unroll
+      for (int j = 0; j < kR; ++j) {  // process.go:118-148
+        const uint32_t r = tid + j * kThreads;
+        if (r >= rows) {
+          s_cw[r] = 0xffffffffu;
+          continue;
+        }
+        const uint32_t wk = s_w[r];
+        const uint64_t sl = wk & KACC_SLOT_MASK;
+        if (sl >= st.proc_slots) {
+          raise_err(st.err, kErrSlot);
+          s_cw[r] = 0xffffffffu;
+          continue;
+        }
+        uint64_t pv[Z], E[Z];
+        double P[Z];
+#pragma unroll
+        for (int z = 0; z < Z; ++z) pv[z] = s_cE[r * Z + z];
+        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E, P);
+        if constexpr ((V & kCarryNoRowStores) == 0) {
+          store_row<Z, true, uint64_t>(st.proc_energy, sl, E);
+          store_row<Z, true, double>(st.proc_power, sl, P);
+        }
+#pragma unroll
+        for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = E[z];
+        s_cw[r] = wk;  // read back only by this lane (same position) next interval
+      }
+      c_has_prev = 1u;
+      c_ts = ts;
+    }
+    mark(5);
+    lds_barrier();  // LDS of interval k read by every wave before interval k+1 writes it
+    mark(6);
+  }
+  if constexpr ((V & kCarryStamps) != 0) {
+    if ((tid & 63u) == 0) {
+      uint64_t *out = reinterpret_cast<uint64_t *>(st.items) + (static_cast<uint64_t>(n) * 8 + tid / 64) * kCarryPhases;
+#pragma unroll
+      for (int ph = 0; ph < kCarryPhases; ++ph) out[ph] = t_acc[ph];
+    }
+  }
 }
 
 // ======================= small nodes: one wavefront per node ======================
@@ -986,8 +1545,11 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     double leaf[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      const uint32_t r0 = lane + 64u * q, r1 = r0 + kTree;  // both < kSmallRows: in bounds
+      const double v0 = s_d[r0], v1 = s_d[r1];
       double s = 0.0;
-      for (uint32_t r = lane + 64u * q; r < rows; r += kTree) s = s + s_d[r];
+      s = s + (r0 < rows ? v0 : 0.0);  // +0.0 past the node's end: an identity
+      s = s + (r1 < rows ? v1 : 0.0);
       leaf[q] = s;
     }
     const double t0 = leaf[0] + leaf[2];
@@ -1677,14 +2239,11 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
 // pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
 // f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
 template <int Z>
-__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
-                                                           const uint32_t *__restrict__ off,
-                                                           const uint32_t *__restrict__ slots,
-                                                           const uint64_t *__restrict__ pe,
-                                                           const double *__restrict__ pp,
-                                                           uint64_t pod_slots, uint64_t *out_e,
-                                                           double *out_p, uint32_t *err) {
-  const uint32_t k = (blockIdx.x * blockDim.x + threadIdx.x) / kNsLanes;
+__device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
+                                                const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
+                                                const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
+                                                double *out_p, uint32_t *err) {
+  const uint32_t k = (blk * kBlock + threadIdx.x) / kNsLanes;
   const uint32_t lane = threadIdx.x % kNsLanes;
   const bool active = k < n_ns;  // inactive lanes still join the shuffles
   unsigned long long e[Z];
@@ -1738,6 +2297,106 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns,
     store_row<Z, false, unsigned long long>(reinterpret_cast<unsigned long long *>(out_e), k, e);
     store_row<Z, false, double>(out_p, k, p);
   }
+}
+
+template <int Z>
+__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const uint32_t *__restrict__ off,
+                                                           const uint32_t *__restrict__ slots,
+                                                           const uint64_t *__restrict__ pe,
+                                                           const double *__restrict__ pp, uint64_t pod_slots,
+                                                           uint64_t *out_e, double *out_p, uint32_t *err) {
+  namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+}
+
+// Cluster partial sums of one context in ONE launch (kacc_allreduce_namespaces):
+// blocks [0, ns_blocks) are namespace_kernel's; the others reduce the node
+// tables — block b sums nodes [256b, 256b + 256), lane order then a halving
+// tree, into partials[b]; the last block to finish adds the partials in block
+// order (a fixed order whichever block is last: reproducible f64 sums) into
+//   node_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal   (u64, modular)
+//   node_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower       (f64)
+struct NodeTotalsArgs {
+  uint64_t n_nodes;
+  const uint64_t *active_total, *idle_total;
+  const double *power, *active_power, *idle_power;
+  uint64_t *part_e;   // [blocks][2Z]
+  double *part_p;     // [blocks][3Z]
+  uint32_t *done;     // block counter, re-armed by the last block
+  uint64_t *out_e;
+  double *out_p;
+};
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T *s_wave) {  // kBlock lanes, fixed order
+#pragma unroll
+  for (int sft = 32; sft >= 1; sft >>= 1) v = v + __shfl_down(v, sft, 64);
+  if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T t = s_wave[0];
+#pragma unroll
+  for (int w = 1; w < kBlock / 64; ++w) t = t + s_wave[w];
+  __syncthreads();
+  return t;
+}
+
+template <int Z>
+__global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
+                                                                  const uint32_t *__restrict__ off,
+                                                                  const uint32_t *__restrict__ slots,
+                                                                  const uint64_t *__restrict__ pe,
+                                                                  const double *__restrict__ pp, uint64_t pod_slots,
+                                                                  uint64_t *out_e, double *out_p, uint32_t *err,
+                                                                  const NodeTotalsArgs na) {
+  if (blockIdx.x < ns_blocks) {
+    namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+    return;
+  }
+  __shared__ unsigned long long s_we[kBlock / 64];
+  __shared__ double s_wp[kBlock / 64];
+  __shared__ uint32_t s_last;
+  const uint32_t b = blockIdx.x - ns_blocks, nb = gridDim.x - ns_blocks;
+  const uint64_t n = static_cast<uint64_t>(b) * kBlock + threadIdx.x;
+  const bool in = n < na.n_nodes;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    const unsigned long long a = in ? na.active_total[n * Z + z] : 0ull;
+    const unsigned long long i = in ? na.idle_total[n * Z + z] : 0ull;
+    const double pw = in ? na.power[n * Z + z] : 0.0;
+    const double ap = in ? na.active_power[n * Z + z] : 0.0;
+    const double ip = in ? na.idle_power[n * Z + z] : 0.0;
+    const unsigned long long sa = block_sum(a, s_we), si = block_sum(i, s_we);
+    const double sp = block_sum(pw, s_wp), sap = block_sum(ap, s_wp), sip = block_sum(ip, s_wp);
+    if (threadIdx.x == 0) {
+      na.part_e[b * 2 * Z + z] = sa;
+      na.part_e[b * 2 * Z + Z + z] = si;
+      na.part_p[b * 3 * Z + z] = sp;
+      na.part_p[b * 3 * Z + Z + z] = sap;
+      na.part_p[b * 3 * Z + 2 * Z + z] = sip;
+    }
+  }
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(na.done, 1u) == nb - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x < 5 * Z) {  // one lane per output, partials in block order
+    const uint32_t j = threadIdx.x;
+    if (j < 2 * Z) {
+      unsigned long long t = 0;
+      for (uint32_t k = 0; k < nb; ++k) t += __hip_atomic_load(na.part_e + k * 2 * Z + j, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT);
+      na.out_e[j] = t;
+    } else {
+      const uint32_t q = j - 2 * Z;
+      double t = 0.0;
+      for (uint32_t k = 0; k < nb; ++k)
+        t = t + __hip_atomic_load(na.part_p + k * 3 * Z + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      na.out_p[q] = t;
+    }
+  }
+  if (threadIdx.x == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
 }
 
 }  // namespace kacc
@@ -1915,6 +2574,17 @@ void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const 
                      ctx->d_err);
 }
 
+template <int Z>
+void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, kacc_ctx *ctx,
+                             uint64_t *out_e, double *out_p, const kacc::NodeTotalsArgs &na, uint32_t node_blocks,
+                             hipStream_t st) {
+  const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
+  const uint32_t ns_blocks = (n_ns + per_block - 1) / per_block;
+  hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
+                     ns_blocks, n_ns, off, slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
+                     (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p, ctx->d_err, na);
+}
+
 // Chunk-item list sized for the worst case of a batch (every node oversized,
 // plus one partial chunk per node) and the deferred-pod list for every pod.
 // Grown (synchronously, between intervals) only when a batch is larger than
@@ -1959,7 +2629,7 @@ int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
   if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
     return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
   if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES | KACC_F_TRUSTED_LAYOUT |
-                   KACC_F_SMALL_NODES))
+                   KACC_F_SMALL_NODES | KACC_F_NODE_SLOT_RANGES | KACC_F_MEDIUM_NODES))
     return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
   return KACC_OK;
 }
@@ -2065,19 +2735,71 @@ int check_slots(kacc_ctx *ctx, const char *name, const uint32_t *w, uint32_t n, 
   return KACC_OK;
 }
 
-// KACC_F_SMALL_NODES when every node fits one wavefront, else KACC_F_FAST_NODES
-// when every node fits the fast workgroup, else 0 (host batch, offsets already
-// validated).
+// KACC_F_FAST_NODES when every node fits the fast workgroup (| KACC_F_MEDIUM_NODES
+// / KACC_F_SMALL_NODES when every node also fits those shapes), else 0 (host
+// batch, offsets already validated).
 uint32_t node_size_flags(const kacc_interval &b) {
-  bool small = true;
+  bool small = true, medium = true;
   for (uint32_t n = 0; n < b.n_nodes; ++n) {
     const uint32_t rows = b.proc_off[n + 1] - b.proc_off[n];
     const uint32_t agg = (b.ctr_off[n + 1] - b.ctr_off[n]) + (b.vm_off[n + 1] - b.vm_off[n]) +
                          (b.pod_off[n + 1] - b.pod_off[n]);
     if (rows > KACC_FAST_MAX_PROCS || agg > KACC_FAST_MAX_AGGREGATES) return 0u;
     small = small && rows <= KACC_SMALL_MAX_PROCS && agg <= KACC_SMALL_MAX_AGGREGATES;
+    medium = medium && rows <= KACC_MEDIUM_MAX_PROCS && agg <= KACC_MEDIUM_MAX_AGGREGATES;
   }
-  return small ? (KACC_F_SMALL_NODES | KACC_F_FAST_NODES) : KACC_F_FAST_NODES;
+  return KACC_F_FAST_NODES | (small ? KACC_F_SMALL_NODES : 0u) | (medium ? KACC_F_MEDIUM_NODES : 0u);
+}
+
+// The K descriptors of a fused kacc_run_intervals, copied to the device on
+// `st` through a pinned staging buffer (reused once its last copy is done).
+int stage_batches(kacc_ctx *ctx, const kacc_interval *b, uint32_t K, hipStream_t st) {
+  if (K > ctx->batch_cap) {
+    if (ctx->batch_copied) KACC_HIP(ctx, hipEventSynchronize(ctx->batch_copied));
+    if (ctx->d_batches) KACC_HIP(ctx, hipFree(ctx->d_batches));
+    if (ctx->h_batches) KACC_HIP(ctx, hipHostFree(ctx->h_batches));
+    ctx->d_batches = nullptr;
+    ctx->h_batches = nullptr;
+    ctx->batch_cap = 0;
+    KACC_HIP(ctx, hipMalloc(&ctx->d_batches, sizeof(kacc_interval) * K));
+    KACC_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->h_batches), sizeof(kacc_interval) * K,
+                                hipHostMallocDefault));
+    ctx->batch_cap = K;
+  }
+  if (!ctx->batch_copied) KACC_HIP(ctx, hipEventCreateWithFlags(&ctx->batch_copied, hipEventDisableTiming));
+  KACC_HIP(ctx, hipEventSynchronize(ctx->batch_copied));  // the previous copy has read the staging buffer
+  std::memcpy(ctx->h_batches, b, sizeof(kacc_interval) * K);
+  KACC_HIP(ctx, hipMemcpyAsync(ctx->d_batches, ctx->h_batches, sizeof(kacc_interval) * K, hipMemcpyHostToDevice, st));
+  KACC_HIP(ctx, hipEventRecord(ctx->batch_copied, st));
+  return KACC_OK;
+}
+
+template <int V>
+void launch_carry(uint32_t Z, bool medium, const kacc_interval *d_b, uint32_t K, uint32_t n_nodes,
+                  const kacc::DevState &s, hipStream_t st) {
+  if (medium) {
+    if (Z == 1)
+      hipLaunchKernelGGL((kacc::intervals_carry_kernel<1, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
+    else
+      hipLaunchKernelGGL((kacc::intervals_carry_kernel<2, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
+  } else {
+    if (Z == 1)
+      hipLaunchKernelGGL((kacc::intervals_carry_kernel<1, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
+    else
+      hipLaunchKernelGGL((kacc::intervals_carry_kernel<2, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
+  }
+}
+
+void launch_intervals(uint32_t Z, bool medium, const kacc_interval *d_b, uint32_t K, uint32_t n_nodes,
+                      const kacc::DevState &s, hipStream_t st) {
+  launch_carry<0>(Z, medium, d_b, K, n_nodes, s, st);
+}
+
+// every descriptor promises KACC_F_MEDIUM_NODES
+bool all_medium(const kacc_interval *b, uint32_t count) {
+  for (uint32_t k = 0; k < count; ++k)
+    if (!(b[k].flags & KACC_F_MEDIUM_NODES)) return false;
+  return true;
 }
 
 }  // namespace
@@ -2164,6 +2886,13 @@ void kacc_destroy(kacc_ctx *ctx) {
   if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
   if (ctx->d_items) (void)hipFree(ctx->d_items);
   if (ctx->d_defer) (void)hipFree(ctx->d_defer);
+  if (ctx->d_node_part) (void)hipFree(ctx->d_node_part);
+  if (ctx->batch_copied) {
+    (void)hipEventSynchronize(ctx->batch_copied);
+    (void)hipEventDestroy(ctx->batch_copied);
+  }
+  if (ctx->d_batches) (void)hipFree(ctx->d_batches);
+  if (ctx->h_batches) (void)hipHostFree(ctx->h_batches);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) {
     (void)hipStreamSynchronize(ctx->copy_stream);
@@ -2225,6 +2954,22 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
   if (rc != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
   const kacc::DevState ds = dev_state(ctx);
+  // one launch for all K intervals when every node stays in one workgroup's
+  // hands: fast nodes, node-private slots, one node set, launch order = node id
+  bool fused = count > 1 && ctx->cfg.zones <= static_cast<uint32_t>(kacc::kCarryMaxZ);
+  for (uint32_t k = 0; k < count && fused; ++k) {
+    const kacc_interval &b = dev_batches[k];
+    fused = (b.flags & KACC_F_FAST_NODES) && (b.flags & KACC_F_NODE_SLOT_RANGES) &&
+            !(b.flags & KACC_F_SMALL_NODES) && !b.node_order && b.n_nodes == dev_batches[0].n_nodes &&
+            b.n_nodes > 0;
+  }
+  if (fused) {
+    if ((rc = stage_batches(ctx, dev_batches, count, st)) != KACC_OK) return rc;
+    launch_intervals(ctx->cfg.zones, all_medium(dev_batches, count), ctx->d_batches, count, dev_batches[0].n_nodes,
+                     ds, st);
+    KACC_HIP(ctx, hipGetLastError());
+    return KACC_OK;
+  }
   for (uint32_t k = 0; k < count; ++k)
     if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
   KACC_HIP(ctx, hipGetLastError());
@@ -2577,6 +3322,67 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, con
   return KACC_OK;
 }
 
+int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
+                                   uint64_t *out_energy, double *out_power, uint64_t *node_energy, double *node_power,
+                                   void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (n_ns && (!off || !slots || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const uint64_t Z = ctx->cfg.zones;
+  const uint32_t node_blocks =
+      node_energy ? static_cast<uint32_t>((ctx->cfg.nodes + kacc::kBlock - 1) / kacc::kBlock) : 0u;
+  if (node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
+    KACC_HIP(ctx, hipStreamSynchronize(st));
+    if (ctx->d_node_part) KACC_HIP(ctx, hipFree(ctx->d_node_part));
+    ctx->d_node_part = nullptr;
+    ctx->node_part_cap = 0;
+    KACC_HIP(ctx, hipMalloc(&ctx->d_node_part, 8 * 5 * Z * node_blocks + 16));
+    KACC_HIP(ctx, hipMemsetAsync(ctx->d_node_part, 0, 8 * 5 * Z * node_blocks + 16, st));
+    ctx->node_part_cap = node_blocks;
+  }
+  kacc::NodeTotalsArgs na{};
+  na.n_nodes = ctx->cfg.nodes;
+  na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
+  na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];
+  na.power = (const double *)ctx->tables[KACC_T_NODE_POWER];
+  na.active_power = (const double *)ctx->tables[KACC_T_NODE_ACTIVE_POWER];
+  na.idle_power = (const double *)ctx->tables[KACC_T_NODE_IDLE_POWER];
+  na.done = static_cast<uint32_t *>(ctx->d_node_part);  // [0]; partials after 16 B
+  na.part_e = reinterpret_cast<uint64_t *>(static_cast<char *>(ctx->d_node_part) + 16);
+  na.part_p = reinterpret_cast<double *>(na.part_e + 2 * Z * std::max<uint32_t>(ctx->node_part_cap, 1));
+  na.out_e = node_energy;
+  na.out_p = node_power;
+  if (!n_ns && !node_blocks) return KACC_OK;
+  (void)hipGetLastError();
+  switch (ctx->cfg.zones) {
+    case 1: launch_cluster_partials<1>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 2: launch_cluster_partials<2>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 3: launch_cluster_partials<3>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 4: launch_cluster_partials<4>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 5: launch_cluster_partials<5>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 6: launch_cluster_partials<6>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 7: launch_cluster_partials<7>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    default: launch_cluster_partials<8>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+  }
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+uint64_t kacc_intervals_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V, uint64_t Q, uint32_t K,
+                              int carried) {
+  // K intervals of these sizes.  Carried (intervals_carry_kernel,
+  // steady state): the engine state a node / row / aggregate reads back — zone
+  // counters and totals, has_prev / ts, previous workload totals and CPU totals —
+  // is read once, then carried on chip.
+  if (!carried) return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q);
+  if (K == 0) return 0;
+  const uint64_t state_once = N * (12 + 24ull * Z) + P * 8ull * Z + C * (8 + 8ull * Z) + V * 8ull * Z +
+                              Q * (8 + 8ull * Z);
+  return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q) -
+         static_cast<uint64_t>(K - 1) * state_once;
+}
+
 uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V,
                              uint64_t Q) {
   // minimal HBM bytes of one interval_kernel launch.
@@ -2586,6 +3392,54 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
   const uint64_t vm = 16 + 24ull * Z;
   const uint64_t pod = 32 + 24ull * Z;
   return N * node + P * proc + C * ctr + V * vm + Q * pod;
+}
+
+// Internal (kacc_debug.h): timing ablations of the one-launch K-interval kernel.
+int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream, int variant,
+                            uint64_t *d_out) {
+  if (!ctx || !b || count == 0 || !d_out) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  int rc = stage_batches(ctx, b, count, st);
+  if (rc != KACC_OK) return rc;
+  kacc::DevState ds = dev_state(ctx);
+  ds.items = reinterpret_cast<kacc::ChunkItem *>(d_out);  // [n_nodes][8 waves][8 phases] u64
+  const bool medium = all_medium(b, count);
+  (void)hipGetLastError();
+  if (variant == 0)
+    launch_carry<16>(2, medium, ctx->d_batches, count, b[0].n_nodes, ds, st);
+  else if (variant == 2)
+    launch_carry<18>(2, medium, ctx->d_batches, count, b[0].n_nodes, ds, st);
+  else
+    return fail(ctx, KACC_EINVAL, "stamp variant %d not built", variant);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream,
+                                     int variant) {
+  if (!ctx || !b || count == 0) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  int rc = stage_batches(ctx, b, count, st);
+  if (rc != KACC_OK) return rc;
+  const kacc::DevState ds = dev_state(ctx);
+  const bool medium = all_medium(b, count);
+  const uint32_t nn = b[0].n_nodes;
+  (void)hipGetLastError();
+  switch (variant) {
+    case 0: launch_carry<0>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 1: launch_carry<1>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 2: launch_carry<2>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 4: launch_carry<4>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 5: launch_carry<5>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 8: launch_carry<8>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    default: return fail(ctx, KACC_EINVAL, "variant %d not built", variant);
+  }
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
 }
 
 // Internal (kacc_debug.h): timing ablations of the interval kernel.  A variant

@@ -28,6 +28,12 @@ struct kacc_ctx {
   uint32_t item_cap = 0;
   uint2 *d_defer = nullptr;
   uint32_t defer_cap = 0;
+  void *d_node_part = nullptr;  // cluster node-total partial sums (+ block counter)
+  uint32_t node_part_cap = 0;   // blocks
+  kacc_interval *d_batches = nullptr;  // fused kacc_run_intervals: descriptors on the device
+  kacc_interval *h_batches = nullptr;  //   and their pinned staging copy
+  uint32_t batch_cap = 0;
+  hipEvent_t batch_copied = nullptr;
   std::string err;
 };
 
@@ -58,6 +64,13 @@ struct kacc_slotmap {
   uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
   uint32_t *d_slots = nullptr;  // 64-bit IDs only
 };
+
+// Namespace partial sums (kacc_namespace_totals' order) and, when node_energy
+// is non-NULL, the context's cluster node totals (node_energy [2Z], node_power
+// [3Z]), in ONE launch on `stream` (kacc_engine.hip; used by kacc_cluster.hip).
+extern "C" int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off,
+                                              const uint32_t *slots, uint64_t *out_energy, double *out_power,
+                                              uint64_t *node_energy, double *node_power, void *stream);
 
 // Records the message on ctx (or the thread's create error when ctx is NULL)
 // and returns code.

@@ -103,10 +103,11 @@ class FleetLayout:
         return out
 
     def fast_flag(self) -> int:
-        """KACC_F_FAST_NODES when every node fits the fast path (| KACC_F_SMALL_NODES
-        when every node fits one wavefront), else 0."""
-        from .accel import (KACC_F_FAST_NODES, KACC_F_SMALL_NODES, KACC_FAST_MAX_AGGREGATES,
-                            KACC_FAST_MAX_PROCS, KACC_SMALL_MAX_AGGREGATES, KACC_SMALL_MAX_PROCS)
+        """KACC_F_FAST_NODES when every node fits the fast path (| KACC_F_MEDIUM_NODES /
+        KACC_F_SMALL_NODES when every node also fits those shapes), else 0."""
+        from .accel import (KACC_F_FAST_NODES, KACC_F_MEDIUM_NODES, KACC_F_SMALL_NODES, KACC_FAST_MAX_AGGREGATES,
+                            KACC_FAST_MAX_PROCS, KACC_MEDIUM_MAX_AGGREGATES, KACC_MEDIUM_MAX_PROCS,
+                            KACC_SMALL_MAX_AGGREGATES, KACC_SMALL_MAX_PROCS)
 
         rows = np.diff(self.proc_off.astype(np.int64))
         agg = (np.diff(self.ctr_off.astype(np.int64)) + np.diff(self.vm_off.astype(np.int64))
@@ -114,7 +115,8 @@ class FleetLayout:
         if not (np.all(rows <= KACC_FAST_MAX_PROCS) and np.all(agg <= KACC_FAST_MAX_AGGREGATES)):
             return 0
         small = bool(np.all(rows <= KACC_SMALL_MAX_PROCS) and np.all(agg <= KACC_SMALL_MAX_AGGREGATES))
-        return KACC_F_FAST_NODES | (KACC_F_SMALL_NODES if small else 0)
+        medium = bool(np.all(rows <= KACC_MEDIUM_MAX_PROCS) and np.all(agg <= KACC_MEDIUM_MAX_AGGREGATES))
+        return KACC_F_FAST_NODES | (KACC_F_SMALL_NODES if small else 0) | (KACC_F_MEDIUM_NODES if medium else 0)
 
     def static_arrays(self) -> Dict[str, np.ndarray]:
         return dict(proc_off=self.proc_off, ctr_off=self.ctr_off, vm_off=self.vm_off,

@@ -387,6 +387,72 @@ def test_run_intervals_matches_sequential(name, kw):
     acc.close()
 
 
+@pytest.mark.parametrize("name,kw,K", [
+    ("z2-config2-like", dict(n_nodes=64, procs_per_node=[1000, 700, 1, 0, 2048, 513] * 10 + [9] * 4, zones=2), 12),
+    ("z2-fragmented", dict(n_nodes=16, procs_per_node=[2000, 900, 64, 3] * 4, zones=2, fragment_slots=0.05), 9),
+    ("z1-shuffled", dict(n_nodes=20, procs_per_node=[1500, 600, 0, 77] * 5, zones=1, shuffle_slots=True), 7),
+    ("z4-not-fused", dict(n_nodes=12, procs_per_node=[2000, 600, 0, 77] * 3, zones=4), 5),
+    # more intervals than one LDS chunk of node inputs (kCarryChunk = 63): two refills
+    ("z2-long", dict(n_nodes=6, procs_per_node=[300, 1200, 5, 0, 64, 2048], zones=2), 140),
+    ("z1-long-fragmented", dict(n_nodes=4, procs_per_node=[700, 90, 1, 2000], zones=1, fragment_slots=0.1), 66),
+    # KACC_F_MEDIUM_NODES (every node <= 1024 rows, <= 256 aggregates): 256-thread workgroups,
+    # 31 intervals per LDS chunk of node inputs
+    ("z2-medium", dict(n_nodes=48, procs_per_node=[1000, 700, 1, 0, 1024, 513] * 8, zones=2), 12),
+    ("z2-medium-long", dict(n_nodes=5, procs_per_node=[1024, 300, 7, 0, 999], zones=2), 70),
+    ("z1-medium-fragmented", dict(n_nodes=8, procs_per_node=[900, 64, 3, 1024] * 2, zones=1, fragment_slots=0.05), 33),
+])
+def test_fused_run_intervals_bit_exact(name, kw, K):
+    """kacc_run_intervals as ONE launch (KACC_F_FAST_NODES | KACC_F_NODE_SLOT_RANGES: every
+    workgroup carries its node through K intervals) == the oracle interval by interval, with
+    churn, read errors, zero ratios, counter wraparound and adversarial inputs."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(seed=23, **kw)
+    flags = layout.fast_flag() & ~accel.KACC_F_SMALL_NODES
+    assert flags & accel.KACC_F_FAST_NODES
+    assert bool(flags & accel.KACC_F_MEDIUM_NODES) == ("medium" in name), name
+    flags |= accel.KACC_F_NODE_SLOT_RANGES
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=23, churn=0.03, read_error_frac=0.05, max_energy=fleet.MAX_ENERGY_FAKE,
+                         adversarial=0.1)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    ivs = [sim.next_interval() for _ in range(K)]
+    if kw.get("fragment_slots"):
+        for a in ivs:
+            a["node_proc_span"] = layout.proc_span()
+    dev = [to_device(a) for a in ivs]
+    descs = [interval_from_tensors(t, sizes, flags) for t in dev]
+    s = current_stream_handle()
+    acc.run_intervals(descs[:1], s)  # first read alone, then K-1 in one launch
+    acc.run_intervals(descs[1:], s)
+    acc.sync(s)
+    for a in ivs:
+        ora.interval(a, sizes)
+    for tname, _ in accel.TABLES:
+        assert_table_equal(acc.download(tname), ora.state[tname], tname)
+    acc.close()
+
+
+@pytest.mark.parametrize("procs", [[1000, 1025, 3], [200, 220, 3]])
+def test_medium_flag_rejects_oversized_node(procs):
+    """KACC_F_MEDIUM_NODES is a promise: under the one-launch path a node over 1024 rows
+    (or over 256 aggregates) raises KACC_ERANGE and nothing faults."""
+    kw = {} if max(procs) > 1024 else dict(procs_per_ctr=1, ctr_frac=0.95, ctrs_per_pod=1.0)
+    layout = fleet.make_layout(3, procs, 2, seed=6, **kw)
+    assert layout.fast_flag() & accel.KACC_F_FAST_NODES and not layout.fast_flag() & accel.KACC_F_MEDIUM_NODES
+    flags = accel.KACC_F_FAST_NODES | accel.KACC_F_MEDIUM_NODES | accel.KACC_F_NODE_SLOT_RANGES
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    sim = fleet.FleetSim(layout, seed=6)
+    dev = [to_device(sim.next_interval()) for _ in range(3)]
+    s = current_stream_handle()
+    with pytest.raises(accel.AccelError) as ei:
+        acc.run_intervals([interval_from_tensors(t, layout.sizes(), flags) for t in dev], s)
+        acc.sync(s)
+    assert ei.value.code == accel.KACC_ERANGE
+    acc.close()
+
+
 def test_recreated_aggregates_bit_exact():
     """Containers / VMs / pods recreated in their slots (NEW on aggregate slot
     words after the first interval): totals restart, CPU caches reset."""
