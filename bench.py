@@ -62,6 +62,9 @@ def parse():
                     help="process slots on a random subset of each node's slot range of (1+F) x rows, "
                          "with node_proc_span (the slot join's steady state under churn)")
     ap.add_argument("--cpu-runs", type=int, default=0, help="CPU baseline: timed runs (0 = as many as fit)")
+    ap.add_argument("--frag-line", type=float, default=0.02,
+                    help="N = 1, pristine slots: also time the same workload with F fragmented slots "
+                         "(the slot join's steady state) and report it as `fragmented` (0 = off)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -165,6 +168,57 @@ def exchange_unique_id(rank, world, make_id):
     return uid
 
 
+def fragmented_line(args, frag, K, steps, pristine_ms, bytes_per_interval):
+    """The same config with process slots fragmented as the slot join leaves them under churn
+    (each node's rows on a random subset of (1+frag) x rows slots, node_proc_span given):
+    interval-kernel time per interval with HIP events on the launch stream (median of `steps`)."""
+    import torch
+
+    from kepler_amd import accel, fleet
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes),
+                                      fragment_slots=frag)
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=fleet.SEED)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    stream = current_stream_handle()
+    statics = to_device(layout.static_arrays())
+    statics.update(to_device({"node_proc_span": layout.proc_span()}))
+    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+    prime = to_device(sim.next_interval())
+    acc.run_interval(interval_from_tensors(prime, sizes), stream)
+    del prime
+    full = [to_device(sim.next_interval()) for _ in range(2)]
+    ivs = []
+    for k in range((steps + 1) * K):
+        t = dict(statics)
+        t.update(full[k % 2])
+        t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
+                            if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
+        ivs.append(interval_from_tensors(t, sizes, flags))
+    ms = []
+    for i in range(steps + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        if K == 1:
+            acc.run_interval(ivs[i], stream)
+        else:
+            acc.run_intervals(ivs[i * K:(i + 1) * K], stream)
+        b.record()
+        b.synchronize()
+        if i:
+            ms.append(a.elapsed_time(b) / K)
+    acc.sync(stream)
+    acc.close()
+    k_ms = float(np.median(ms))
+    achieved = bytes_per_interval / (k_ms * 1e-3) / 1e9
+    return {"fragment_slots": frag, "kernel_ms": k_ms, "achieved_GBps": achieved, "frac": achieved / HBM_PEAK_GBPS,
+            "pristine_over_fragmented": pristine_ms / k_ms,
+            "note": "same rows / algorithmic bytes as the pristine line; slots are a random subset of "
+                    "(1+F) x rows per node in random row order, moved in slot order (node_proc_span)"}
+
+
 def bench_nodes(config, world, nodes=None):
     """Fleet size of a config at `world` GPUs: weak scaling (a fixed shard per GPU) except
     config 4, whose 100k-node fleet is split over the GPUs (strong scaling)."""
@@ -265,7 +319,7 @@ def main():
         if ev is not None:
             ev[1].record()
         b = k % 2
-        if done[b] is not None:  # stream-level wait (no host sync)
+        if done[b] is not None and not done[b].query():  # stream-level wait (no host sync) unless done
             torch.cuda.current_stream().wait_event(done[b])
         cluster.allreduce_namespaces(n_ns, [ns_t["off"].data_ptr()], [ns_t["slot"].data_ptr()],
                                      [ns_e[b].data_ptr()], [ns_p[b].data_ptr()], [nd_e[b].data_ptr()],
@@ -329,9 +383,10 @@ def main():
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
-        ent = pmc.get(f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else ""))
-        if ent and ent.get("n_procs") == sizes["n_procs"]:
-            traffic = ent.get("hbm_bytes_per_launch")
+        ent = pmc.get(f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else "")
+                      + (f"_k{K}" if fused else ""))
+        if ent and ent.get("n_procs") == sizes["n_procs"]:  # per interval, like `achieved`
+            traffic = ent.get("hbm_bytes_per_interval", ent.get("hbm_bytes_per_launch"))
 
     result = {
         "metric": METRIC,
@@ -417,6 +472,13 @@ def main():
                                            f"{res['soa_mt']['runs']} runs"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
+
+    if world == 1 and args.frag_line > 0 and args.fragment == 0 and args.config in (1, 2, 3):
+        try:
+            result["fragmented"] = fragmented_line(args, args.frag_line, K, min(args.steps, 10), k_avg_ms,
+                                                   bytes_per_launch)
+        except Exception as e:  # a secondary line: report, never lose the headline
+            result["fragmented"] = {"error": repr(e)}
 
     if rank == 0:
         line = json.dumps(result)

@@ -376,6 +376,9 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
         n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr, st);
     if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
   }
+  // one rank, one shard: the partial sums are the cluster totals (no combine, no
+  // collective, and no cross-stream packets between the caller's intervals)
+  if (c->nranks == 1 && ns == 1) return KACC_OK;
   // 2. shards of one GPU (on the compute streams)
   int rc = KACC_OK;
   if (n_ns && (rc = local_combine(c, streams, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;

@@ -2254,34 +2254,29 @@ __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, con
     p[z] = 0.0;
   }
   const uint32_t beg = active ? off[k] : 0u, end = active ? off[k + 1] : 0u;
+  // loads unconditional from clamped indices (a predicated load makes the
+  // compiler branch around it and wait per element); the adds are masked
   for (uint32_t j0 = beg + lane; j0 < end; j0 += kNsLanes * kNsUnroll) {
     uint32_t sl[kNsUnroll];
 #pragma unroll
-    for (int u = 0; u < kNsUnroll; ++u) {
-      const uint32_t j = j0 + u * kNsLanes;
-      sl[u] = j < end ? (slots[j] & KACC_SLOT_MASK) : 0xffffffffu;
-    }
+    for (int u = 0; u < kNsUnroll; ++u) sl[u] = slots[min(j0 + u * kNsLanes, end - 1)] & KACC_SLOT_MASK;
     uint64_t er[kNsUnroll][Z];
     double pr[kNsUnroll][Z];
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
-      if (sl[u] < pod_slots) {
-        load_row<Z>(pe, sl[u], er[u]);
-        load_row_f64<Z>(pp, sl[u], pr[u]);
-      }
+      const uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
+      load_row<Z>(pe, at, er[u]);
+      load_row_f64<Z>(pp, at, pr[u]);
     }
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
-      const uint32_t j = j0 + u * kNsLanes;
-      if (j >= end) continue;
-      if (sl[u] >= pod_slots) {
-        raise_err(err, kErrNs);
-        continue;
-      }
+      const bool in = j0 + u * kNsLanes < end;
+      if (in && sl[u] >= pod_slots) raise_err(err, kErrNs);
+      const bool use = in && sl[u] < pod_slots;
 #pragma unroll
       for (int z = 0; z < Z; ++z) {
-        e[z] += er[u][z];
-        p[z] = p[z] + pr[u][z];
+        e[z] += use ? er[u][z] : 0ull;
+        if (use) p[z] = p[z] + pr[u][z];
       }
     }
   }
@@ -2310,34 +2305,23 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 
 // Cluster partial sums of one context in ONE launch (kacc_allreduce_namespaces):
 // blocks [0, ns_blocks) are namespace_kernel's; the others reduce the node
-// tables — block b sums nodes [256b, 256b + 256), lane order then a halving
-// tree, into partials[b]; the last block to finish adds the partials in block
-// order (a fixed order whichever block is last: reproducible f64 sums) into
+// tables — block b sums nodes [b·npb, (b+1)·npb) (lane l: nodes l, l+256, …,
+// then the wave trees and the four waves in order) into partials[b]; the last
+// block to finish adds the ≤ kNodeBlocksMax partials in block order (a fixed
+// order whichever block is last: reproducible f64 sums) into
 //   node_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal   (u64, modular)
 //   node_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower       (f64)
+constexpr uint32_t kNodeBlocksMax = 64;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
+  uint32_t npb;       // nodes per block (a multiple of kBlock)
   const uint64_t *active_total, *idle_total;
   const double *power, *active_power, *idle_power;
-  uint64_t *part_e;   // [blocks][2Z]
-  double *part_p;     // [blocks][3Z]
+  uint64_t *part;     // [blocks][5Z] raw 8-byte words: 2Z u64 then 3Z f64
   uint32_t *done;     // block counter, re-armed by the last block
   uint64_t *out_e;
   double *out_p;
 };
-
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T *s_wave) {  // kBlock lanes, fixed order
-#pragma unroll
-  for (int sft = 32; sft >= 1; sft >>= 1) v = v + __shfl_down(v, sft, 64);
-  if ((threadIdx.x & 63) == 0) s_wave[threadIdx.x >> 6] = v;
-  __syncthreads();
-  T t = s_wave[0];
-#pragma unroll
-  for (int w = 1; w < kBlock / 64; ++w) t = t + s_wave[w];
-  __syncthreads();
-  return t;
-}
 
 template <int Z>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
@@ -2351,52 +2335,82 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
     namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
     return;
   }
-  __shared__ unsigned long long s_we[kBlock / 64];
-  __shared__ double s_wp[kBlock / 64];
+  constexpr int kV = 5 * Z;
+  __shared__ uint64_t s_w[kBlock / 64][kV];
+  __shared__ uint64_t s_part[kNodeBlocksMax * kV];
   __shared__ uint32_t s_last;
-  const uint32_t b = blockIdx.x - ns_blocks, nb = gridDim.x - ns_blocks;
-  const uint64_t n = static_cast<uint64_t>(b) * kBlock + threadIdx.x;
-  const bool in = n < na.n_nodes;
+  const uint32_t tid = threadIdx.x, b = blockIdx.x - ns_blocks, nb = gridDim.x - ns_blocks;
+  unsigned long long ve[2 * Z];
+  double vp[3 * Z];
 #pragma unroll
-  for (int z = 0; z < Z; ++z) {
-    const unsigned long long a = in ? na.active_total[n * Z + z] : 0ull;
-    const unsigned long long i = in ? na.idle_total[n * Z + z] : 0ull;
-    const double pw = in ? na.power[n * Z + z] : 0.0;
-    const double ap = in ? na.active_power[n * Z + z] : 0.0;
-    const double ip = in ? na.idle_power[n * Z + z] : 0.0;
-    const unsigned long long sa = block_sum(a, s_we), si = block_sum(i, s_we);
-    const double sp = block_sum(pw, s_wp), sap = block_sum(ap, s_wp), sip = block_sum(ip, s_wp);
-    if (threadIdx.x == 0) {
-      na.part_e[b * 2 * Z + z] = sa;
-      na.part_e[b * 2 * Z + Z + z] = si;
-      na.part_p[b * 3 * Z + z] = sp;
-      na.part_p[b * 3 * Z + Z + z] = sap;
-      na.part_p[b * 3 * Z + 2 * Z + z] = sip;
+  for (int q = 0; q < 2 * Z; ++q) ve[q] = 0;
+#pragma unroll
+  for (int q = 0; q < 3 * Z; ++q) vp[q] = 0.0;
+  const uint64_t n_end = min(static_cast<uint64_t>(b + 1) * na.npb, na.n_nodes);
+  for (uint64_t n = static_cast<uint64_t>(b) * na.npb + tid; n < n_end; n += kBlock) {
+    uint64_t a[Z], i[Z];
+    double pw[Z], ap[Z], ip[Z];
+    load_row<Z>(na.active_total, n, a);
+    load_row<Z>(na.idle_total, n, i);
+    load_row_f64<Z>(na.power, n, pw);
+    load_row_f64<Z>(na.active_power, n, ap);
+    load_row_f64<Z>(na.idle_power, n, ip);
+#pragma unroll
+    for (int z = 0; z < Z; ++z) {
+      ve[z] += a[z];
+      ve[Z + z] += i[z];
+      vp[z] = vp[z] + pw[z];
+      vp[Z + z] = vp[Z + z] + ap[z];
+      vp[2 * Z + z] = vp[2 * Z + z] + ip[z];
     }
   }
-  if (threadIdx.x == 0) {
+#pragma unroll
+  for (int sft = 32; sft >= 1; sft >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 2 * Z; ++q) ve[q] += __shfl_down(ve[q], sft, 64);
+#pragma unroll
+    for (int q = 0; q < 3 * Z; ++q) vp[q] = vp[q] + __shfl_down(vp[q], sft, 64);
+  }
+  if ((tid & 63u) == 0) {
+#pragma unroll
+    for (int q = 0; q < 2 * Z; ++q) s_w[tid >> 6][q] = ve[q];
+#pragma unroll
+    for (int q = 0; q < 3 * Z; ++q) s_w[tid >> 6][2 * Z + q] = static_cast<uint64_t>(__double_as_longlong(vp[q]));
+  }
+  __syncthreads();
+  if (tid < static_cast<uint32_t>(kV)) {  // the four waves in order
+    uint64_t r;
+    if (tid < 2u * Z) {
+      r = s_w[0][tid];
+      for (int w = 1; w < kBlock / 64; ++w) r += s_w[w][tid];
+    } else {
+      double t = __longlong_as_double(static_cast<long long>(s_w[0][tid]));
+      for (int w = 1; w < kBlock / 64; ++w) t = t + __longlong_as_double(static_cast<long long>(s_w[w][tid]));
+      r = static_cast<uint64_t>(__double_as_longlong(t));
+    }
+    na.part[static_cast<uint64_t>(b) * kV + tid] = r;
+  }
+  __syncthreads();
+  if (tid == 0) {
     __threadfence();
     s_last = atomicAdd(na.done, 1u) == nb - 1 ? 1u : 0u;
   }
   __syncthreads();
   if (!s_last) return;
   __threadfence();
-  if (threadIdx.x < 5 * Z) {  // one lane per output, partials in block order
-    const uint32_t j = threadIdx.x;
-    if (j < 2 * Z) {
-      unsigned long long t = 0;
-      for (uint32_t k = 0; k < nb; ++k) t += __hip_atomic_load(na.part_e + k * 2 * Z + j, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-      na.out_e[j] = t;
-    } else {
-      const uint32_t q = j - 2 * Z;
-      double t = 0.0;
-      for (uint32_t k = 0; k < nb; ++k)
-        t = t + __hip_atomic_load(na.part_p + k * 3 * Z + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      na.out_p[q] = t;
-    }
+  for (uint32_t x = tid; x < nb * kV; x += kBlock)  // every partial in flight at once
+    s_part[x] = __hip_atomic_load(na.part + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (tid < 2u * Z) {
+    unsigned long long t = 0;
+    for (uint32_t k = 0; k < nb; ++k) t += s_part[k * kV + tid];
+    na.out_e[tid] = t;
+  } else if (tid < static_cast<uint32_t>(kV)) {
+    double t = 0.0;
+    for (uint32_t k = 0; k < nb; ++k) t = t + __longlong_as_double(static_cast<long long>(s_part[k * kV + tid]));
+    na.out_p[tid - 2 * Z] = t;
   }
-  if (threadIdx.x == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
+  if (tid == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
 }
 
 }  // namespace kacc
@@ -3330,8 +3344,11 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint64_t Z = ctx->cfg.zones;
+  // at most kNodeBlocksMax blocks of a multiple of kBlock nodes each
+  const uint64_t groups = (ctx->cfg.nodes + kacc::kBlock - 1) / kacc::kBlock;
+  const uint32_t npb = static_cast<uint32_t>(kacc::kBlock * ((groups + kacc::kNodeBlocksMax - 1) / kacc::kNodeBlocksMax));
   const uint32_t node_blocks =
-      node_energy ? static_cast<uint32_t>((ctx->cfg.nodes + kacc::kBlock - 1) / kacc::kBlock) : 0u;
+      node_energy && ctx->cfg.nodes ? static_cast<uint32_t>((ctx->cfg.nodes + npb - 1) / npb) : 0u;
   if (node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
     KACC_HIP(ctx, hipStreamSynchronize(st));
     if (ctx->d_node_part) KACC_HIP(ctx, hipFree(ctx->d_node_part));
@@ -3343,14 +3360,14 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
   }
   kacc::NodeTotalsArgs na{};
   na.n_nodes = ctx->cfg.nodes;
+  na.npb = npb;
   na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
   na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];
   na.power = (const double *)ctx->tables[KACC_T_NODE_POWER];
   na.active_power = (const double *)ctx->tables[KACC_T_NODE_ACTIVE_POWER];
   na.idle_power = (const double *)ctx->tables[KACC_T_NODE_IDLE_POWER];
   na.done = static_cast<uint32_t *>(ctx->d_node_part);  // [0]; partials after 16 B
-  na.part_e = reinterpret_cast<uint64_t *>(static_cast<char *>(ctx->d_node_part) + 16);
-  na.part_p = reinterpret_cast<double *>(na.part_e + 2 * Z * std::max<uint32_t>(ctx->node_part_cap, 1));
+  na.part = reinterpret_cast<uint64_t *>(static_cast<char *>(ctx->d_node_part) + 16);
   na.out_e = node_energy;
   na.out_p = node_power;
   if (!n_ns && !node_blocks) return KACC_OK;

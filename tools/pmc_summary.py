@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into pmc_traffic.json.
 
-usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR SOURCE_LABEL OUT.json [CONFIG [KERNEL]]
+usage: python tools/pmc_summary.py FETCH_DIR WRITE_DIR SOURCE_LABEL OUT.json [CONFIG [KERNEL [K]]]
 
 KERNEL is a substring of the profiled kernel name (default "interval_kernel<4, 0>");
-an existing OUT.json keeps its other configs' entries.
+K > 1: the kernel is the one-launch K-interval carry kernel (entry "config<C>_k<K>",
+algorithmic bytes kacc_intervals_bytes(carried), per-interval figures = per launch / K).
+An existing OUT.json keeps its other configs' entries.
 
 FETCH_SIZE is doubled (MI355X_MICROARCH.md §HBM: gfx950 tallies 128-B streaming
 reads at 64 B); both counters are KiB.  Per launch of kacc::interval_kernel<Z,0>.
@@ -32,11 +34,13 @@ def main():
     fdir, wdir, label, out = sys.argv[1:5]
     cfg = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     kernel = sys.argv[6] if len(sys.argv) > 6 else "interval_kernel<4, 0>"
+    K = int(sys.argv[7]) if len(sys.argv) > 7 else 1
     from kepler_amd import accel, fleet
 
     layout = fleet.config_layout(cfg, nodes=40000 if cfg == 1 else None)  # bench.py --config 1 fleet
     s = layout.sizes()
-    alg = accel.interval_bytes(layout.zones, *[s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
+    dims = [s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")]
+    alg = accel.interval_bytes(layout.zones, *dims) if K == 1 else accel.intervals_bytes(layout.zones, *dims, K, True)
     fv, wv = values(fdir, "FETCH_SIZE", kernel), values(wdir, "WRITE_SIZE", kernel)
     if not fv or not wv:
         raise SystemExit(f"no {kernel} counter rows found")
@@ -45,8 +49,9 @@ def main():
     if os.path.exists(out):
         with open(out) as f:
             res = json.load(f)
+    key = f"config{cfg}" + (f"_k{K}" if K > 1 else "")
     res.update({
-        f"config{cfg}": {
+        key: {
             "n_procs": s["n_procs"],
             "kernel": "kacc::" + kernel.replace(" ", ""),
             "fetch_size_kib_median": fm,
@@ -56,13 +61,16 @@ def main():
             "tools/bench_variants.py (VARIANTS=0 ROUNDS=3); FETCH_SIZE doubled per "
             "MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B streaming reads at 64 B); values in KiB",
             "algorithmic_bytes_per_launch": alg,
+            "intervals_per_launch": K,
+            "hbm_bytes_per_interval": (2.0 * fm + wm) * 1024.0 / K,
+            "algorithmic_bytes_per_interval": alg / K,
             "source": label,
             "raw_kib": {"FETCH_SIZE": fv, "WRITE_SIZE": wv},
         }
     })
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
-    r = res[f"config{cfg}"]
+    r = res[key]
     print(f"traffic {r['hbm_bytes_per_launch']/1e9:.3f} GB/launch vs algorithmic {alg/1e9:.3f} GB")
 
 
