@@ -63,8 +63,8 @@ def parse():
                          "with node_proc_span (the slot join's steady state under churn)")
     ap.add_argument("--cpu-runs", type=int, default=0, help="CPU baseline: timed runs (0 = as many as fit)")
     ap.add_argument("--frag-line", type=float, default=0.02,
-                    help="N = 1, pristine slots: also time the same workload with F fragmented slots "
-                         "(the slot join's steady state) and report it as `fragmented` (0 = off)")
+                    help="N = 1: also time this workload under three slot layouts on the same box (pristine "
+                         "without / with node_proc_span, F fragmented) and report them as `slot_layouts` (0 = off)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -168,55 +168,63 @@ def exchange_unique_id(rank, world, make_id):
     return uid
 
 
-def fragmented_line(args, frag, K, steps, pristine_ms, bytes_per_interval):
-    """The same config with process slots fragmented as the slot join leaves them under churn
-    (each node's rows on a random subset of (1+frag) x rows slots, node_proc_span given):
-    interval-kernel time per interval with HIP events on the launch stream (median of `steps`)."""
+def slot_layout_lines(args, frag, K, steps, bytes_per_interval):
+    """Same-box kernel time per interval (HIP events on the launch stream, median of `steps`)
+    of this config under three slot layouts: pristine slots without node_proc_span (row
+    order), pristine with it, and slots fragmented as the slot join leaves them under churn
+    (each node's rows on a random subset of (1+frag) x rows slots, in random row order,
+    node_proc_span given).  Same rows, same algorithmic bytes."""
     import torch
 
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
-    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes),
-                                      fragment_slots=frag)
-    sizes = layout.sizes()
-    sim = fleet.FleetSim(layout, seed=fleet.SEED)
-    acc = accel.Accel(layout.zones, **layout.capacities())
-    stream = current_stream_handle()
-    statics = to_device(layout.static_arrays())
-    statics.update(to_device({"node_proc_span": layout.proc_span()}))
-    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
-    prime = to_device(sim.next_interval())
-    acc.run_interval(interval_from_tensors(prime, sizes), stream)
-    del prime
-    full = [to_device(sim.next_interval()) for _ in range(2)]
-    ivs = []
-    for k in range((steps + 1) * K):
-        t = dict(statics)
-        t.update(full[k % 2])
-        t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
-                            if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
-        ivs.append(interval_from_tensors(t, sizes, flags))
-    ms = []
-    for i in range(steps + 1):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        if K == 1:
-            acc.run_interval(ivs[i], stream)
-        else:
-            acc.run_intervals(ivs[i * K:(i + 1) * K], stream)
-        b.record()
-        b.synchronize()
-        if i:
-            ms.append(a.elapsed_time(b) / K)
-    acc.sync(stream)
-    acc.close()
-    k_ms = float(np.median(ms))
-    achieved = bytes_per_interval / (k_ms * 1e-3) / 1e9
-    return {"fragment_slots": frag, "kernel_ms": k_ms, "achieved_GBps": achieved, "frac": achieved / HBM_PEAK_GBPS,
-            "pristine_over_fragmented": pristine_ms / k_ms,
-            "note": "same rows / algorithmic bytes as the pristine line; slots are a random subset of "
-                    "(1+F) x rows per node in random row order, moved in slot order (node_proc_span)"}
+    def one(fr, span):
+        _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes),
+                                          fragment_slots=fr)
+        sizes = layout.sizes()
+        sim = fleet.FleetSim(layout, seed=fleet.SEED)
+        acc = accel.Accel(layout.zones, **layout.capacities())
+        stream = current_stream_handle()
+        statics = to_device(layout.static_arrays())
+        if span:
+            statics.update(to_device({"node_proc_span": layout.proc_span()}))
+        flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+        prime = to_device(sim.next_interval())
+        acc.run_interval(interval_from_tensors(prime, sizes), stream)
+        del prime
+        full = [to_device(sim.next_interval()) for _ in range(2)]
+        ivs = []
+        for k in range((steps + 1) * K):
+            t = dict(statics)
+            t.update(full[k % 2])
+            t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
+                                if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
+            ivs.append(interval_from_tensors(t, sizes, flags))
+        ms = []
+        for i in range(steps + 1):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            if K == 1:
+                acc.run_interval(ivs[i], stream)
+            else:
+                acc.run_intervals(ivs[i * K:(i + 1) * K], stream)
+            b.record()
+            b.synchronize()
+            if i:
+                ms.append(a.elapsed_time(b) / K)
+        acc.sync(stream)
+        acc.close()
+        k_ms = float(np.median(ms))
+        achieved = bytes_per_interval / (k_ms * 1e-3) / 1e9
+        return {"kernel_ms": k_ms, "achieved_GBps": achieved, "frac": achieved / HBM_PEAK_GBPS}
+
+    out = {"pristine_no_span": one(0.0, False), "pristine_span": one(0.0, True),
+           f"fragmented_{frag:g}_span": one(frag, True)}
+    out["fragmented_over_pristine"] = out[f"fragmented_{frag:g}_span"]["kernel_ms"] / out["pristine_span"]["kernel_ms"]
+    out["note"] = ("same box, same method, same rows / algorithmic bytes; fragmented = each node's rows on a "
+                   "random subset of (1+F) x rows slots in random row order (the slot join's steady state)")
+    return out
 
 
 def bench_nodes(config, world, nodes=None):
@@ -272,8 +280,9 @@ def main():
     stream = current_stream_handle()
     assert stream != 0
     statics = to_device(layout.static_arrays())
-    if args.fragment > 0:  # the slot join's per-node spans: rows moved in slot order
-        statics.update(to_device({"node_proc_span": layout.proc_span()}))
+    # the slot join's per-node spans (kacc_slot_join reports them every interval): nodes whose
+    # slots fit the kernels' windows are moved in slot order
+    statics.update(to_device({"node_proc_span": layout.proc_span()}))
     dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
                 for a in full]
     node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")
@@ -475,10 +484,10 @@ def main():
 
     if world == 1 and args.frag_line > 0 and args.fragment == 0 and args.config in (1, 2, 3):
         try:
-            result["fragmented"] = fragmented_line(args, args.frag_line, K, min(args.steps, 10), k_avg_ms,
-                                                   bytes_per_launch)
+            result["slot_layouts"] = slot_layout_lines(args, args.frag_line, K, min(args.steps, 10),
+                                                       bytes_per_launch)
         except Exception as e:  # a secondary line: report, never lose the headline
-            result["fragmented"] = {"error": repr(e)}
+            result["slot_layouts"] = {"error": repr(e)}
 
     if rank == 0:
         line = json.dumps(result)

@@ -845,6 +845,7 @@ struct CarryTables {
   int64_t ts[kCarryEntries<T>];
   double ratio[kCarryEntries<T>], nd_given[kCarryEntries<T>];
   uint64_t ze[kCarryEntries<T> * Z], zm[kCarryEntries<T> * Z];
+  uint32_t span_lo[kCarryEntries<T>], span_hi[kCarryEntries<T>];  // node_proc_span (lo > hi: none)
 };
 // A node's rows and this lane's aggregate descriptor (raw; loaded an interval
 // ahead): resolved at use, so that no instruction reads them right after the load.
@@ -871,6 +872,8 @@ __device__ __forceinline__ void fill_tables(const kacc_interval *bs, uint32_t K,
     t.ts[tid] = gbl(b.node_ts_ns)[n];
     t.ratio[tid] = gbl(b.node_usage_ratio)[n];
     t.nd_given[tid] = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) ? gbl(b.node_cpu_delta)[n] : 0.0;
+    t.span_lo[tid] = b.node_proc_span ? gbl(b.node_proc_span)[2 * static_cast<uint64_t>(n)] : 1u;
+    t.span_hi[tid] = b.node_proc_span ? gbl(b.node_proc_span)[2 * static_cast<uint64_t>(n) + 1] : 0u;
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
       t.ze[tid * Z + z] = gbl(b.zone_energy)[static_cast<uint64_t>(n) * Z + z];
@@ -1016,6 +1019,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
 #pragma unroll
   for (int j = 0; j < kR; ++j) s_cw[tid + j * kThreads] = 0xffffffffu;
   if (tid == 0) s_moved = 0;
+  // Process-row totals are carried either by ROW position (s_cw: the slot word
+  // last written there; a changed slot means "moved") or, when the interval
+  // gives the node's slot span (node_proc_span, hi - lo < kRows), by SLOT
+  // position in a window [c_sbase, c_sbase + kRows) of the node's own slots:
+  // rows are then attributed in slot order through an LDS inverse map (s_inv,
+  // in s_cw's memory), so every wave instruction writes contiguous slots even
+  // when the join left the node's slots in random row order.  The window is
+  // loaded once (the node's slots are private for the whole call) and stays
+  // valid across intervals while lo is unchanged.
+  constexpr uint32_t kNoWindow = 0xffffffffu, kWindowPending = 0xfffffffeu;
+  uint32_t c_sbase = kNoWindow;
+  uint16_t *s_inv = reinterpret_cast<uint16_t *>(s_cw);
 
   // node inputs staged in LDS per chunk of intervals; the rows one interval ahead
   __shared__ CarryTables<Z, T> tab;
@@ -1059,16 +1074,36 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
                                    : 0u;
     const uint32_t a_end0 = is_c ? rw.ce : is_v ? rw.ve : is_q ? rw.qe : 0u;
     const uint32_t a_w = is_c ? rw.cw : is_v ? rw.vw : is_q ? rw.qw : 0xffffffffu;
-    bool moved = false;
+    // slot sweep this interval? (block-uniform)
+    const uint32_t s_lo = uniform_u32(tab.span_lo[e]), s_hi = uniform_u32(tab.span_hi[e]);
+    const bool sweep = rows > 0 && s_hi >= s_lo && s_hi - s_lo < static_cast<uint32_t>(kRows) && s_hi < st.proc_slots;
+    const uint32_t span = sweep ? s_hi - s_lo + 1 : 0u;
+    if (sweep != (c_sbase != kNoWindow)) {  // layout change: drop the row keys / start an empty map
+#pragma unroll
+      for (int j = 0; j < kR; ++j) s_cw[tid + j * kThreads] = 0xffffffffu;  // s_inv: all 0xffff
+      c_sbase = sweep ? kWindowPending : kNoWindow;
+      lds_barrier();
+    }
+    const bool process = !(status & KACC_NODE_READ_ERROR) && fits;
+    bool moved = false, outside = false;
 #pragma unroll
     for (int j = 0; j < kR; ++j) {  // stage the rows (LDS of interval k-1 is free: barrier at its end)
       const uint32_t r = tid + j * kThreads;
       if (r < rows && fits) {
         s_d[r] = rw.d[j];
         s_w[r] = rw.w[j];
-        moved |= (rw.w[j] & KACC_SLOT_MASK) != (s_cw[r] & KACC_SLOT_MASK);
+        if (sweep) {
+          const uint32_t pos = (rw.w[j] & KACC_SLOT_MASK) - s_lo;
+          if (process && pos < span)
+            s_inv[pos] = static_cast<uint16_t>(r);
+          else
+            outside = process;  // a row outside its node's span: not computed
+        } else {
+          moved |= (rw.w[j] & KACC_SLOT_MASK) != (s_cw[r] & KACC_SLOT_MASK);
+        }
       }
     }
+    if (outside) raise_err(st.err, kErrSlot);
     const uint32_t flags = b.flags;
     // in flight during interval k: rows and node inputs of k+1, offsets of k+2
     // (a past-the-end interval re-reads the last one: no branch)
@@ -1094,27 +1129,43 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
       const bool a_moved = a_ok && (role != c_role || a_s != (c_aw & KACC_SLOT_MASK));
       moved |= a_moved;
       if (__any(moved) && (tid & 63) == 0) s_moved = 1u;
+      const bool load_window = sweep && c_sbase != s_lo;  // block-uniform
       mark(0);
-      lds_barrier();  // s_d / s_w staged, s_moved set
+      lds_barrier();  // s_d / s_w / s_inv staged, s_moved set
       mark(1);
-      if ((V & kCarryNeverMoved) == 0 && s_moved) {  // block-uniform: the rare path
+      if (((V & kCarryNeverMoved) == 0 && s_moved) || load_window) {  // block-uniform: the rare path
         __syncthreads();  // this workgroup's earlier stores complete and visible (and ordered)
+        if (load_window) {  // the table rows of slots [lo, lo + kRows) (those in the table)
 #pragma unroll
-        for (int j = 0; j < kR; ++j) {
-          const uint32_t r = tid + j * kThreads;
-          if (r >= rows) continue;
-          const uint32_t sw = s_w[r];
-          const uint64_t sl = sw & KACC_SLOT_MASK;
-          if (sl == (s_cw[r] & KACC_SLOT_MASK)) continue;
-          uint64_t pv[Z];
-          if (sl < st.proc_slots) {
-            load_row<Z>(st.proc_energy, sl, pv);
-          } else {
+          for (int j = 0; j < kR; ++j) {
+            const uint32_t pos = tid + j * kThreads;
+            const uint64_t sl = static_cast<uint64_t>(s_lo) + pos;
+            uint64_t pv[Z];
+            if (sl < st.proc_slots) {
+              load_row<Z>(st.proc_energy, sl, pv);
 #pragma unroll
-            for (int z = 0; z < Z; ++z) pv[z] = 0;
+              for (int z = 0; z < Z; ++z) s_cE[pos * Z + z] = pv[z];
+            }
           }
+          c_sbase = s_lo;
+        } else if (!sweep) {
 #pragma unroll
-          for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = pv[z];
+          for (int j = 0; j < kR; ++j) {
+            const uint32_t r = tid + j * kThreads;
+            if (r >= rows) continue;
+            const uint32_t sw = s_w[r];
+            const uint64_t sl = sw & KACC_SLOT_MASK;
+            if (sl == (s_cw[r] & KACC_SLOT_MASK)) continue;
+            uint64_t pv[Z];
+            if (sl < st.proc_slots) {
+              load_row<Z>(st.proc_energy, sl, pv);
+            } else {
+#pragma unroll
+              for (int z = 0; z < Z; ++z) pv[z] = 0;
+            }
+#pragma unroll
+            for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = pv[z];
+          }
         }
         if (a_moved) {
           load_row<Z>(role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy, a_s, c_aE);
@@ -1278,6 +1329,28 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
       }
       c_role = a_ok ? role : 0u;
       c_aw = a_ok ? a_w : 0xffffffffu;
+      if (sweep) {  // process.go:118-148 in slot order: slot lo + pos holds row s_inv[pos]
+#pragma unroll
+        for (int j = 0; j < kR; ++j) {
+          const uint32_t pos = tid + j * kThreads;
+          if (pos >= span) continue;
+          const uint32_t r = s_inv[pos];
+          if (r == 0xffffu) continue;  // a free slot of the node's range
+          s_inv[pos] = 0xffffu;        // the map starts empty next interval (this lane's entry)
+          const uint32_t wk = s_w[r];
+          uint64_t pv[Z], E[Z];
+          double P[Z];
+#pragma unroll
+          for (int z = 0; z < Z; ++z) pv[z] = s_cE[pos * Z + z];
+          attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E, P);
+          if constexpr ((V & kCarryNoRowStores) == 0) {
+            store_row<Z, true, uint64_t>(st.proc_energy, static_cast<uint64_t>(s_lo) + pos, E);
+            store_row<Z, true, double>(st.proc_power, static_cast<uint64_t>(s_lo) + pos, P);
+          }
+#pragma unroll
+          for (int z = 0; z < Z; ++z) s_cE[pos * Z + z] = E[z];
+        }
+      } else {
 #pragma unroll
       for (int j = 0; j < kR; ++j) {  // process.go:118-148
         const uint32_t r = tid + j * kThreads;
@@ -1304,6 +1377,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
 #pragma unroll
         for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = E[z];
         s_cw[r] = wk;  // read back only by this lane (same position) next interval
+      }
       }
       c_has_prev = 1u;
       c_ts = ts;

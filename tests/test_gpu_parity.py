@@ -434,6 +434,40 @@ def test_fused_run_intervals_bit_exact(name, kw, K):
     acc.close()
 
 
+@pytest.mark.parametrize("medium", [False, True])
+def test_fused_span_toggles_bit_exact(medium):
+    """One launch whose intervals give node_proc_span only sometimes: the carried totals switch
+    between row keys and the slot window (and back) mid-launch; fragmented slots with churn,
+    read errors and adversarial inputs; nodes whose span exceeds the window stay in row order."""
+    from oracle.oracle import Oracle
+
+    procs = [1000, 700, 1, 0, 1024, 513] if medium else [2000, 1500, 1, 0, 1990, 64]
+    layout = fleet.make_layout(n_nodes=12, procs_per_node=procs * 2, zones=2, seed=29, fragment_slots=0.03)
+    flags = (layout.fast_flag() & ~accel.KACC_F_SMALL_NODES) | accel.KACC_F_NODE_SLOT_RANGES
+    assert bool(flags & accel.KACC_F_MEDIUM_NODES) == medium
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=29, churn=0.05, read_error_frac=0.08, max_energy=fleet.MAX_ENERGY_FAKE,
+                         adversarial=0.1)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    pattern = [0, 1, 1, 0, 1, 0, 0, 1, 1, 1, 0, 1]
+    ivs = [sim.next_interval() for _ in pattern]
+    for a, given in zip(ivs, pattern):
+        if given:
+            a["node_proc_span"] = layout.proc_span()
+    dev = [to_device(a) for a in ivs]
+    descs = [interval_from_tensors(t, sizes, flags) for t in dev]
+    s = current_stream_handle()
+    acc.run_intervals(descs[:1], s)
+    acc.run_intervals(descs[1:], s)
+    acc.sync(s)
+    for a in ivs:
+        ora.interval(a, sizes)
+    for tname, _ in accel.TABLES:
+        assert_table_equal(acc.download(tname), ora.state[tname], tname)
+    acc.close()
+
+
 @pytest.mark.parametrize("procs", [[1000, 1025, 3], [200, 220, 3]])
 def test_medium_flag_rejects_oversized_node(procs):
     """KACC_F_MEDIUM_NODES is a promise: under the one-launch path a node over 1024 rows

@@ -32,6 +32,9 @@ def main():
     acc = accel.Accel(L.zones, **L.capacities())
     s = current_stream_handle()
     acc.run_interval(interval_from_tensors(to_device(prime), L.sizes()), s)
+    if os.environ.get("SPAN", "1") == "1":  # kacc_slot_join's node_proc_span, as in production
+        for a in ivs:
+            a["node_proc_span"] = L.proc_span()
     dev = [to_device(a) for a in ivs]
     base = L.fast_flag()
     fused = [interval_from_tensors(t, L.sizes(), base | accel.KACC_F_NODE_SLOT_RANGES) for t in dev]
