@@ -13,11 +13,19 @@
 // Shortest digits: Adams' Ryū method (PLDI 2018) — the interval of decimals
 // that round to the input, scaled by a 125-bit power of five
 // (kacc_pow5_tables.h), shortened digit by digit; ties round to even.
+// Attribution: shortest() below follows the structure of the published
+// algorithm and of its reference implementation's d2s routine (Ulf Adams,
+// "Ryū: fast float-to-string conversion", PLDI 2018; reference code under
+// Apache-2.0 / Boost-1.0), restated for the device from the paper — the
+// power-of-five tables are generated here (tools/gen_pow5_tables.py), not copied.
+// Go's strconv uses the same shortest-digit definition (ryuFtoaShortest), which
+// is what the exposition needs byte for byte.
 // One thread per value; each writes a fixed kFmtWidth-byte field (three
 // 8-byte stores) and its length.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -276,7 +284,7 @@ __global__ __launch_bounds__(kThreads) void format_kernel(const Args a) {
 // ---- sample lines: NAME{LABELS,zone="ZONE"} VALUE\n ------------------------------
 // Constants of one call, staged in LDS: the metric name, then the zone names.
 constexpr uint32_t kConstCap = 1024;
-constexpr int kLineWaves = 4;  // line_write_kernel: one wave per line in flight
+constexpr int kLineWaves = 2;  // line_write_kernel: waves per workgroup (16 KiB of LDS each)
 
 struct LineArgs {
   const void *src;       // table base
@@ -290,7 +298,8 @@ struct LineArgs {
   const char *consts;         // device: name, then zone names
   uint32_t name_len;
   uint32_t zone_table[KACC_MAX_ZONES];  // table zone of line zone j
-  uint32_t zone_pos[KACC_MAX_ZONES + 1];  // zone name j = consts[zone_pos[j] .. zone_pos[j+1])
+  uint32_t zone_pos[KACC_MAX_ZONES + 1];  // zone name j = consts[zone_pos[j], + zone_len[j]) (4-aligned)
+  uint32_t zone_len[KACC_MAX_ZONES];
   uint32_t const_len;
   char *vals;        // temp [lines * KACC_FMT_WIDTH]
   uint8_t *vlen;     // temp [lines]
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(kThreads) void line_len_kernel(const LineArgs a) {
     dst[2] = w[2];
     a.vlen[i] = static_cast<uint8_t>(o.n);
     const uint64_t ll = a.label_off[r + 1] - a.label_off[r];
-    const uint32_t zl = a.zone_pos[j + 1] - a.zone_pos[j];
+    const uint32_t zl = a.zone_len[j];
     // NAME { LABELS ,zone=" ZONE "}<sp> VALUE \n
     a.len[i] = a.name_len + 1 + ll + 7 + zl + 3 + o.n + 1;
   }
@@ -347,12 +356,100 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t x, int k) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// Pass 2: a wave takes 64 consecutive lines (one contiguous byte range of the
+// text).  Lane l assembles line base + l in a wave-private LDS buffer laid
+// out so that buffer offset ≡ text offset (mod 16): its pieces (name, labels,
+// zone, value, punctuation) are appended a dword at a time through a byte
+// packer (v_alignbyte for unaligned label bytes, ds_write_b32 per full dword,
+// byte stores only for the dwords it shares with its neighbour lines); then
+// the wave stores the range with 16-byte stores (1 KiB per instruction).
+// Lines are taken in the longest prefix that fits the buffer; a single line
+// longer than the buffer is written with per-line 64-byte-wide byte stores.
+constexpr uint32_t kLineBuf = 12288;  // bytes per wave
+
+__device__ __forceinline__ void write_lines_bytewise(const LineArgs &a, const char *s_c, uint64_t base, uint32_t k_beg,
+                                                     uint32_t k_end, uint64_t l0, uint64_t l1, uint64_t o0,
+                                                     uint64_t o1, uint32_t vl, uint32_t zpair) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t k = k_beg; k < k_end; ++k) {
+    const uint64_t L0 = bcast64(l0, k), LL = bcast64(l1, k) - L0;
+    const uint64_t O0 = bcast64(o0, k), N = bcast64(o1, k) - O0;
+    const uint32_t VL = __builtin_amdgcn_readlane(vl, k), ZP = __builtin_amdgcn_readlane(zpair, k);
+    const uint32_t z0 = ZP >> 16, zl = ZP & 0xffffu;
+    if (O0 > a.out_cap || N > a.out_cap - O0) {  // cannot happen with a consistent scan
+      if (lane == 0) atomicOr(a.err, 1u << 8);
+      continue;
+    }
+    const char *val = a.vals + (base + k) * KACC_FMT_WIDTH;
+    const uint64_t cL = a.name_len + 1, cD = cL + LL, cE = cD + 7, cF = cE + zl, cG = cF + 3, cH = cG + VL;
+    for (uint64_t p = lane; p < N; p += 64) {
+      char c;
+      if (p < a.name_len) c = s_c[p];
+      else if (p < cL) c = '{';
+      else if (p < cD) c = a.labels[L0 + (p - cL)];
+      else if (p < cE) c = ",zone=\""[p - cD];
+      else if (p < cF) c = s_c[z0 + (p - cE)];
+      else if (p < cG) c = "\"} "[p - cF];
+      else if (p < cH) c = val[p - cG];
+      else c = '\n';
+      a.out[O0 + p] = c;
+    }
+  }
+}
+
+// One lane's line in LDS: bytes appended to `acc` (nb of them valid), full
+// dwords stored; the first `skip` bytes of the first dword belong to the line
+// before, so that dword (and the last, partial one) is stored byte by byte.
+struct Packer {
+  uint32_t *buf;
+  uint32_t d, nb, skip;
+  uint64_t acc;
+};
+
+__device__ __forceinline__ void pk_put(Packer &p, uint32_t src, uint32_t k) {  // the low k (1..4) bytes of src
+  const uint64_t m = k >= 4 ? 0xffffffffull : ((1ull << (8 * k)) - 1ull);
+  p.acc |= (static_cast<uint64_t>(src) & m) << (8 * p.nb);
+  p.nb += k;
+  if (p.nb >= 4) {
+    const uint32_t w = static_cast<uint32_t>(p.acc);
+    if (p.skip) {
+      char *c = reinterpret_cast<char *>(p.buf + p.d);
+      for (uint32_t b = p.skip; b < 4; ++b) c[b] = static_cast<char>(w >> (8 * b));
+      p.skip = 0;
+    } else {
+      p.buf[p.d] = w;
+    }
+    ++p.d;
+    p.acc >>= 32;
+    p.nb -= 4;
+  }
+}
+
+__device__ __forceinline__ void pk_finish(Packer &p) {
+  char *c = reinterpret_cast<char *>(p.buf + p.d);
+  const uint32_t w = static_cast<uint32_t>(p.acc);
+  for (uint32_t b = p.skip; b < p.nb; ++b) c[b] = static_cast<char>(w >> (8 * b));
+}
+
+__device__ __forceinline__ void pk_lds(Packer &p, const char *s_c, uint32_t pos, uint32_t len) {  // pos 4-aligned
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(s_c + pos);
+  for (uint32_t i = 0; i < len; i += 4) pk_put(p, w[i >> 2], min(4u, len - i));
+}
+
 __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineArgs a) {
-  __shared__ char s_c[kConstCap];
+  __shared__ __attribute__((aligned(16))) char s_c[kConstCap];
+  __shared__ __attribute__((aligned(16))) char s_buf[kLineWaves][kLineBuf];
   for (uint32_t k = threadIdx.x; k < a.const_len; k += 64 * kLineWaves) s_c[k] = a.consts[k];
   __syncthreads();
   const uint64_t lines = a.count * a.n_zones;
   const uint32_t lane = threadIdx.x & 63u;
+  char *buf = s_buf[threadIdx.x >> 6];
+  // label bytes as aligned dwords when the label buffer is dword-aligned: the
+  // last readable dword is the one holding the final label byte
+  const uint64_t label_bytes = a.label_off[a.count];
+  const bool dw_labels = (reinterpret_cast<uintptr_t>(a.labels) & 3u) == 0 && label_bytes > 0;
+  const uint64_t last_dw = label_bytes ? (label_bytes - 1) >> 2 : 0;
+  const uint32_t *lw = reinterpret_cast<const uint32_t *>(a.labels);
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kLineWaves * 64;
   for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kLineWaves + (threadIdx.x >> 6)) * 64; base < lines;
        base += step) {
@@ -364,31 +461,80 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
     const uint64_t l0 = a.label_off[r], l1 = a.label_off[r + 1];
     const uint64_t o0 = a.line_off[i], o1 = a.line_off[i + 1];
     const uint32_t vl = a.vlen[i];
-    const uint32_t zpair = (a.zone_pos[j] << 16) | (a.zone_pos[j + 1] - a.zone_pos[j]);  // z0 | zl
+    const uint32_t zpair = (a.zone_pos[j] << 16) | a.zone_len[j];  // z0 | zl
+    const uint64_t *vw = reinterpret_cast<const uint64_t *>(a.vals + i * KACC_FMT_WIDTH);
+    const uint64_t v0 = vw[0], v1 = vw[1], v2 = vw[2];
     const uint32_t nl = static_cast<uint32_t>(min<uint64_t>(lines - base, 64));
-    for (uint32_t k = 0; k < nl; ++k) {
-      const uint64_t L0 = bcast64(l0, k), LL = bcast64(l1, k) - L0;
-      const uint64_t O0 = bcast64(o0, k), N = bcast64(o1, k) - O0;
-      const uint32_t VL = __builtin_amdgcn_readlane(vl, k), ZP = __builtin_amdgcn_readlane(zpair, k);
-      const uint32_t z0 = ZP >> 16, zl = ZP & 0xffffu;
-      if (O0 > a.out_cap || N > a.out_cap - O0) {  // cannot happen with a consistent scan
-        if (lane == 0) atomicOr(a.err, 1u << 8);
+    for (uint32_t k0 = 0; k0 < nl;) {
+      const uint64_t t0 = bcast64(o0, k0);
+      const uint32_t shift = static_cast<uint32_t>(t0 & 15u);
+      // lanes [k0, k1): the longest run of lines that fits the buffer (and out_cap)
+      const bool fit = lane >= k0 && lane < nl && o1 >= t0 && o1 - t0 + shift <= kLineBuf && o1 <= a.out_cap &&
+                       o0 <= o1;
+      const uint64_t miss = ~__ballot(fit) >> k0;
+      const uint32_t k1 = k0 + (miss ? static_cast<uint32_t>(__builtin_ctzll(miss)) : 64u - k0);
+      if (k1 == k0) {  // one line longer than the buffer (or an inconsistent offset)
+        write_lines_bytewise(a, s_c, base, k0, k0 + 1, l0, l1, o0, o1, vl, zpair);
+        ++k0;
         continue;
       }
-      const char *val = a.vals + (base + k) * KACC_FMT_WIDTH;
-      const uint64_t cL = a.name_len + 1, cD = cL + LL, cE = cD + 7, cF = cE + zl, cG = cF + 3, cH = cG + VL;
-      for (uint64_t p = lane; p < N; p += 64) {
-        char c;
-        if (p < a.name_len) c = s_c[p];
-        else if (p < cL) c = '{';
-        else if (p < cD) c = a.labels[L0 + (p - cL)];
-        else if (p < cE) c = ",zone=\""[p - cD];
-        else if (p < cF) c = s_c[z0 + (p - cE)];
-        else if (p < cG) c = "\"} "[p - cF];
-        else if (p < cH) c = val[p - cG];
-        else c = '\n';
-        a.out[O0 + p] = c;
+      const uint64_t t1 = bcast64(o1, k1 - 1);
+      if (lane >= k0 && lane < k1) {  // assemble line base + lane
+        const uint32_t st = static_cast<uint32_t>(o0 - t0) + shift;
+        Packer p{reinterpret_cast<uint32_t *>(buf), st >> 2, st & 3u, st & 3u, 0ull};
+        pk_lds(p, s_c, 0, a.name_len);
+        pk_put(p, '{', 1);
+        const uint64_t n = l1 - l0;
+        if (dw_labels) {  // 4 label bytes per dword pair (v_alignbyte), 8 dwords in flight
+          const uint64_t q0 = l0 >> 2;
+          const uint32_t sh = static_cast<uint32_t>(l0 & 3u);
+          for (uint64_t p0 = 0; p0 < n; p0 += 28) {
+            uint32_t w[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = lw[min(q0 + (p0 >> 2) + q, last_dw)];
+#pragma unroll
+            for (int q = 0; q < 7; ++q) {
+              const uint64_t at = p0 + 4u * q;
+              if (at < n) pk_put(p, __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), static_cast<uint32_t>(min<uint64_t>(4, n - at)));
+            }
+          }
+        } else {
+          const char *lb = a.labels + l0;
+          for (uint64_t p0 = 0; p0 < n; ++p0) pk_put(p, static_cast<uint8_t>(lb[p0]), 1);
+        }
+        pk_put(p, 0x6e6f7a2cu, 4);  // ",zon"
+        pk_put(p, 0x00223d65u, 3);  // "e=\""
+        pk_lds(p, s_c, zpair >> 16, zpair & 0xffffu);
+        pk_put(p, 0x00207d22u, 3);  // "\"} "
+        const uint32_t vd[6] = {static_cast<uint32_t>(v0), static_cast<uint32_t>(v0 >> 32), static_cast<uint32_t>(v1),
+                                static_cast<uint32_t>(v1 >> 32), static_cast<uint32_t>(v2), static_cast<uint32_t>(v2 >> 32)};
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          if (4u * q < vl) pk_put(p, vd[q], min(4u, vl - 4u * q));
+        pk_put(p, '\n', 1);
+        pk_finish(p);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // ---- the range [t0, t1) out of LDS (word w = text bytes [t0 - shift + 16w, +16))
+      const uint64_t g0 = t0 - shift;
+      const uint32_t words = static_cast<uint32_t>((t1 - g0 + 15) / 16);
+      using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+      for (uint32_t w = lane; w < words; w += 64) {
+        const uint64_t g = g0 + 16ull * w;
+        if (g >= t0 && g + 16 <= t1) {
+          __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(buf + 16 * w),
+                                      reinterpret_cast<u32x4 *>(a.out + g));
+        } else {
+          for (uint32_t b = 0; b < 16; ++b)
+            if (g + b >= t0 && g + b < t1) a.out[g + b] = buf[16 * w + b];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // the buffer is rewritten next
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      k0 = k1;
     }
   }
 }
@@ -523,12 +669,16 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   kacc::fmt::LineArgs a{};
   std::string consts(name);
   a.name_len = static_cast<uint32_t>(consts.size());
+  auto pad4 = [&consts]() { consts.resize((consts.size() + 3) & ~size_t{3}, '\0'); };  // dword-aligned pieces
+  pad4();
   for (uint32_t j = 0; j < n_zones; ++j) {
     const uint32_t z = zone_order ? zone_order[j] : j;
     if (z >= Z || !zone_names[j]) return kacc_fail(ctx, KACC_EINVAL, "format_lines: bad zone %u", j);
     a.zone_table[j] = z;
     a.zone_pos[j] = static_cast<uint32_t>(consts.size());
+    a.zone_len[j] = static_cast<uint32_t>(strlen(zone_names[j]));
     consts += zone_names[j];
+    pad4();
   }
   a.zone_pos[n_zones] = static_cast<uint32_t>(consts.size());
   if (consts.size() > kacc::fmt::kConstCap)
