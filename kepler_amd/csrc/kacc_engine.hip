@@ -315,8 +315,8 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
     const uint32_t idx = piece / kHalf;
     const uint32_t zp = piece % kHalf;
     uint32_t row = row0 + idx;
+    if (idx >= len) continue;
     if constexpr (kInv) {
-      if (idx >= len) continue;
       row = s_inv[row];
       if (row == 0xffffu) continue;  // free slot of the node's range
     }
@@ -613,16 +613,21 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   if (role != 0 && !a_ok) raise_err(st.err, kErrSlot);
 
   // ---- B: stage Δ, ProcessTotalCPUTimeDelta (informer.go:330-333) ------------
+  int moved_rows = 0;  // swept node: some row's slot is not smin + row (else no inverse map needed)
 #pragma unroll
   for (int k = 0; k < kRowsPerThread; ++k) {
     const uint32_t r = tid + k * kThreads;
     if (r < rows) {
       s_d[r] = d[k];
       s_w[r] = w[k];
+      moved_rows |= (w[k] & KACC_SLOT_MASK) != smin + r;
     }
   }
-  __syncthreads();
-  if (swept) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
+  // a swept node whose slots are exactly smin + row (pristine slots with the join's span):
+  // moved in slot order without the inverse map
+  const int any_moved = __syncthreads_or(moved_rows);  // the staging barrier, every node
+  const bool identity = swept && span == rows && !any_moved;
+  if (swept && !identity) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint32_t r = tid + k * kThreads;
@@ -731,9 +736,14 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       for (int k = 0; k < kRowsPerThread; ++k) {
         const uint32_t pos0 = static_cast<uint32_t>(tid & ~63) + k * kThreads;
         const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
-        attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
-                                             static_cast<uint64_t>(smin) + pos0, len, prev[k],
-                                             st.proc_energy, st.proc_power);
+        if (identity)  // row pos0 + i holds slot smin + pos0 + i
+          attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
+                                                static_cast<uint64_t>(smin) + pos0, len, prev[k],
+                                                st.proc_energy, st.proc_power);
+        else
+          attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
+                                               static_cast<uint64_t>(smin) + pos0, len, prev[k],
+                                               st.proc_energy, st.proc_power);
       }
     }
   } else if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
