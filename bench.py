@@ -169,7 +169,8 @@ def exchange_unique_id(rank, world, make_id):
 
 
 def slot_layout_lines(args, frag, K, steps, bytes_per_interval):
-    """Same-box kernel time per interval (HIP events on the launch stream, median of `steps`)
+    """Same-box kernel time per interval (HIP events on the launch stream around back-to-back
+    launches, median of `steps`)
     of this config under three slot layouts: pristine slots without node_proc_span (row
     order), pristine with it, and slots fragmented as the slot join leaves them under churn
     (each node's rows on a random subset of (1+frag) x rows slots, in random row order,
@@ -201,18 +202,16 @@ def slot_layout_lines(args, frag, K, steps, bytes_per_interval):
             t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
                                 if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
             ivs.append(interval_from_tensors(t, sizes, flags))
-        ms = []
-        for i in range(steps + 1):
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps + 1)]
+        for i in range(steps + 1):  # back to back, as the headline's steps (sustained clocks)
+            ev[i][0].record()
             if K == 1:
                 acc.run_interval(ivs[i], stream)
             else:
                 acc.run_intervals(ivs[i * K:(i + 1) * K], stream)
-            b.record()
-            b.synchronize()
-            if i:
-                ms.append(a.elapsed_time(b) / K)
+            ev[i][1].record()
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) / K for a, b in ev[1:]]
         acc.sync(stream)
         acc.close()
         k_ms = float(np.median(ms))
@@ -280,9 +279,8 @@ def main():
     stream = current_stream_handle()
     assert stream != 0
     statics = to_device(layout.static_arrays())
-    # the slot join's per-node spans (kacc_slot_join reports them every interval): nodes whose
-    # slots fit the kernels' windows are moved in slot order
-    statics.update(to_device({"node_proc_span": layout.proc_span()}))
+    if args.fragment > 0:  # the slot join's per-node spans: rows moved in slot order
+        statics.update(to_device({"node_proc_span": layout.proc_span()}))
     dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
                 for a in full]
     node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")

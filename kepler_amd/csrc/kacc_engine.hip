@@ -315,8 +315,8 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
     const uint32_t idx = piece / kHalf;
     const uint32_t zp = piece % kHalf;
     uint32_t row = row0 + idx;
-    if (idx >= len) continue;
     if constexpr (kInv) {
+      if (idx >= len) continue;
       row = s_inv[row];
       if (row == 0xffffu) continue;  // free slot of the node's range
     }
@@ -551,11 +551,13 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   uint32_t contig = 0;  // bit k: group k of this wave is transposed (wave-uniform)
   constexpr bool kSweepable =
       kTransposed<Z> && (V & (kVarNoTranspose | kVarNoSweep | kVarSkipProcs)) == 0;
+  // Z without the transposed paths: the same sweep, one slot position per lane
+  constexpr bool kRowSweep = !kTransposed<Z> && (V & (kVarNoSweep | kVarSkipProcs)) == 0;
   // slot sweep when the caller gives the node's slot span (kacc_slot_join's
   // out_span) and it fits the LDS inverse map; node-uniform -> SGPRs
   uint32_t smin = 0, span = 0;
   bool sweep = false;
-  if constexpr (kSweepable) {
+  if constexpr (kSweepable || kRowSweep) {
     if (b.node_proc_span) {
       const uint32_t lo = uniform_u32(b.node_proc_span[2 * n]);
       const uint32_t hi = uniform_u32(b.node_proc_span[2 * n + 1]);
@@ -568,9 +570,14 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       }
     }
   }
-  const bool swept = kSweepable && sweep;
+  const bool swept = (kSweepable || kRowSweep) && sweep;
   if constexpr ((V & kVarSkipProcs) == 0) {
     if (swept) {  // prev totals of the span's 64-slot groups (free slots read too)
+      if constexpr (kRowSweep) {  // slot smin + position (clamped: loads stay unconditional)
+#pragma unroll
+        for (int k = 0; k < kRowsPerThread; ++k)
+          load_row<Z>(st.proc_energy, static_cast<uint64_t>(smin) + min(tid + k * kThreads, span - 1), prev[k]);
+      }
       if constexpr (kSweepable) {
 #pragma unroll
         for (int k = 0; k < kRowsPerThread; ++k) {
@@ -613,21 +620,16 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   if (role != 0 && !a_ok) raise_err(st.err, kErrSlot);
 
   // ---- B: stage Δ, ProcessTotalCPUTimeDelta (informer.go:330-333) ------------
-  int moved_rows = 0;  // swept node: some row's slot is not smin + row (else no inverse map needed)
 #pragma unroll
   for (int k = 0; k < kRowsPerThread; ++k) {
     const uint32_t r = tid + k * kThreads;
     if (r < rows) {
       s_d[r] = d[k];
       s_w[r] = w[k];
-      moved_rows |= (w[k] & KACC_SLOT_MASK) != smin + r;
     }
   }
-  // a swept node whose slots are exactly smin + row (pristine slots with the join's span):
-  // moved in slot order without the inverse map
-  const int any_moved = __syncthreads_or(moved_rows);  // the staging barrier, every node
-  const bool identity = swept && span == rows && !any_moved;
-  if (swept && !identity) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
+  __syncthreads();
+  if (swept) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
       const uint32_t r = tid + k * kThreads;
@@ -731,19 +733,29 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   };
   if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
+    if constexpr (kRowSweep) {
+#pragma unroll
+      for (int k = 0; k < kRowsPerThread; ++k) {
+        const uint32_t pos = tid + k * kThreads;
+        if (pos >= span) continue;
+        const uint32_t r = s_inv[pos];
+        if (r == 0xffffu) continue;  // a free slot of the node's range
+        const uint32_t wk = s_w[r];
+        uint64_t E[Z];
+        double P[Z];
+        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E, P);
+        store_row<Z, kNT, uint64_t>(st.proc_energy, static_cast<uint64_t>(smin) + pos, E);
+        store_row<Z, kNT, double>(st.proc_power, static_cast<uint64_t>(smin) + pos, P);
+      }
+    }
     if constexpr (kSweepable) {
 #pragma unroll
       for (int k = 0; k < kRowsPerThread; ++k) {
         const uint32_t pos0 = static_cast<uint32_t>(tid & ~63) + k * kThreads;
         const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
-        if (identity)  // row pos0 + i holds slot smin + pos0 + i
-          attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
-                                                static_cast<uint64_t>(smin) + pos0, len, prev[k],
-                                                st.proc_energy, st.proc_power);
-        else
-          attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
-                                               static_cast<uint64_t>(smin) + pos0, len, prev[k],
-                                               st.proc_energy, st.proc_power);
+        attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
+                                             static_cast<uint64_t>(smin) + pos0, len, prev[k],
+                                             st.proc_energy, st.proc_power);
       }
     }
   } else if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
@@ -1435,7 +1447,7 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int Z>
+template <int Z, bool SW>
 __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(Z <= 2 ? 6 : Z <= 4 ? 5 : 1))) void small_kernel(
     const kacc_interval b, const DevState st) {
   constexpr bool kNT = true, kNtLd = true;  // as interval_kernel's production variant
@@ -1444,6 +1456,10 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   // group) paths; otherwise each lane keeps its own in w[] and the LDS per node
   // drops from 8.4 KB to 6.4 KB (Z = 2: 6 nodes' workgroups per CU, not 4)
   constexpr bool kSweepable = kTransposed<Z>;
+  // Z without the transposed paths: with node_proc_span (SW) the rows are moved
+  // in slot order too, one slot position per lane, through an inverse map whose
+  // entries carry the row's NEW bit (the slot words stay in their lanes' registers)
+  constexpr bool kRowSweep = SW && !kTransposed<Z>;
   __shared__ uint32_t s_w_all[kSmallWaves][kSweepable ? kSmallRows : 1];
   __shared__ double s_cd_all[kSmallWaves][kSmallAgg];
   __shared__ double s_ct_all[kSmallWaves][kSmallAgg];
@@ -1497,7 +1513,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   }
   uint32_t smin = 0, span = 0;
   bool swept = false;
-  if constexpr (kSweepable) {
+  if constexpr (kSweepable || kRowSweep) {
     if (b.node_proc_span) {
       const uint32_t lo = uniform_u32(b.node_proc_span[2 * n]);
       const uint32_t hi = uniform_u32(b.node_proc_span[2 * n + 1]);
@@ -1520,6 +1536,12 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     for (int g = 0; g < kSmallBatch; ++g) {
       const int k = kb * kSmallBatch + g;
       const uint32_t pos0 = 64u * k;
+      if constexpr (kRowSweep) {
+        if (swept) {  // slot smin + pos0 + lane (clamped: the load stays unconditional)
+          load_row<Z>(st.proc_energy, static_cast<uint64_t>(smin) + min(pos0 + lane, span - 1), prev[g]);
+          continue;
+        }
+      }
       if constexpr (kSweepable) {
         if (swept) {
           const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
@@ -1608,6 +1630,18 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     }
   }
   wave_sync();  // s_inv reset and the staged rows visible to every lane
+  if (kRowSweep && swept) {  // position -> row | NEW bit << 15 (rows < 512)
+#pragma unroll
+    for (int k = 0; k < kSmallGroups; ++k) {
+      const uint32_t r = lane + 64u * k;
+      if (r >= rows) continue;
+      const uint32_t sl = w[k] & KACC_SLOT_MASK;
+      if (sl - smin < span && sl < st.proc_slots)
+        s_inv[sl - smin] = static_cast<uint16_t>(r | ((w[k] & KACC_SLOT_NEW) ? 0x8000u : 0u));
+      else
+        raise_err(st.err, kErrSlot);
+    }
+  }
   if (kSweepable && swept) {
 #pragma unroll
     for (int k = 0; k < kSmallGroups; ++k) {
@@ -1729,6 +1763,20 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int g = 0; g < kSmallBatch; ++g) {
       const uint32_t pos0 = 64u * (kb * kSmallBatch + g);
+      if constexpr (kRowSweep) {
+        if (swept) {  // slot smin + pos: row s_inv[pos] (0xffff: a free slot)
+          const uint32_t pos = pos0 + lane;
+          if (pos >= span) continue;
+          const uint32_t e = s_inv[pos];
+          if (e == 0xffffu) continue;
+          uint64_t E[Z];
+          double P[Z];
+          attribute_row<Z>(a, a.live, s_d[e & 0x7fffu], (e & 0x8000u) != 0, prev[g], E, P);
+          store_row<Z, kNT, uint64_t>(st.proc_energy, static_cast<uint64_t>(smin) + pos, E);
+          store_row<Z, kNT, double>(st.proc_power, static_cast<uint64_t>(smin) + pos, P);
+          continue;
+        }
+      }
       if constexpr (kSweepable) {
         if (swept) {
           const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
@@ -2608,7 +2656,10 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
 template <int Z>
 void launch_small(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   const uint32_t grid = (b.n_nodes + kacc::kSmallWaves - 1) / kacc::kSmallWaves;
-  hipLaunchKernelGGL((kacc::small_kernel<Z>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
+  if (!kacc::kTransposed<Z> && b.node_proc_span)  // Z without the transposed paths: row-wise slot sweep
+    hipLaunchKernelGGL((kacc::small_kernel<Z, true>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
+  else
+    hipLaunchKernelGGL((kacc::small_kernel<Z, false>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
 }
 
 template <int Z, int V>
