@@ -139,14 +139,18 @@ struct Probe {
     }
     return ~0u;
   }
-  // claim the first empty or tombstone bucket on k's path; returns it (or ~0u)
-  __device__ uint32_t insert(K k, uint32_t rel) const {
+  // claim the first empty or tombstone bucket on k's path; returns it (or ~0u);
+  // *fresh: the bucket was empty (the table's occupancy grew)
+  __device__ uint32_t insert(K k, uint32_t rel, uint32_t *fresh = nullptr) const {
     uint32_t b = bucket(k, shift);
     for (uint32_t p = 0; p < H;) {
       const uint64_t raw = t.raw(b);
       const K kk = static_cast<K>(Tab<K>::key_of(raw));
       if (kk == Tab<K>::kEmpty || kk == Tab<K>::kTomb) {
-        if (t.claim(b, raw, k, rel)) return b;
+        if (t.claim(b, raw, k, rel)) {
+          if (fresh) *fresh += kk == Tab<K>::kEmpty ? 1u : 0u;
+          return b;
+        }
         continue;  // lost the race for this bucket: look at it again
       }
       ++p;
@@ -303,9 +307,9 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     const uint32_t r = tid * kRpl + j;
     key[j] = r < R ? keys[r] : T::kEmpty;
   }
+  uint64_t ev[kPer];
+  uint32_t sv[kWide ? kPer : 1];
   {
-    uint64_t ev[kPer];
-    uint32_t sv[kWide ? kPer : 1];
     if (H) {  // node-uniform; clamped addresses keep the loads unconditional
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
@@ -337,11 +341,26 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   __syncthreads();
   if (a.stop_after == 1u) return;  // timing ablation
 
-  // ---- 2: held slots; lookups --------------------------------------------------------
-  for (uint32_t b = tid; b < H; b += kThreads) {
-    if (!is_live<K>(L.raw(b))) continue;
-    const uint32_t sl = lslot(b);
-    if (sl < S) atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
+  // ---- 2: held slots and the occupancy, from this lane's buckets still in registers;
+  //         lookups ---------------------------------------------------------------------
+  {
+    uint32_t occ = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const uint32_t b = tid + j * kThreads;
+      if (b >= H) break;
+      const auto k = T::key_of(ev[j]);
+      occ += k != T::kEmpty ? 1u : 0u;
+      if (k == T::kEmpty || k == T::kTomb) continue;
+      uint32_t sl;
+      if constexpr (kWide)
+        sl = sv[j];
+      else
+        sl = static_cast<uint32_t>(ev[j]);
+      if (sl < S) atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
+    }
+    occ = wave_sum(occ);
+    if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
   }
   uint32_t mine = 0;  // new rows of this lane
 #pragma unroll
@@ -452,11 +471,13 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
 
   // ---- 6: inserts (one lane per new row), then a re-probe flags an ID twice ---------
   const uint32_t n_ins = min(n_new, total_free);
+  uint32_t fresh = 0;  // inserts into empty buckets (occupancy)
   if (compact) {
     for (uint32_t i = tid; i < n_ins; i += kThreads) {
-      const uint32_t b = pr.insert(s_newkey[i], s_free[i]);
+      const uint32_t b = pr.insert(s_newkey[i], s_free[i], &fresh);
       if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
     }
+    if (fresh) atomicAdd(&s_occ, fresh);
     __syncthreads();
     for (uint32_t i = tid; i < n_ins; i += kThreads) {
       const uint32_t b = pr.find(s_newkey[i]);
@@ -473,9 +494,10 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
 #pragma unroll
     for (int j = 0; j < kRpl; ++j) {
       if (rk[j] == ~0u) continue;
-      const uint32_t b = pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0);
+      const uint32_t b = pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0, &fresh);
       if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
     }
+    if (fresh) atomicAdd(&s_occ, fresh);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kRpl; ++j) {
@@ -488,14 +510,10 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     }
   }
 
-  // ---- 7: occupancy; write back the changed buckets (or rebuild); slot words --------
-  {
-    uint32_t occ = 0;
-    for (uint32_t b = tid; b < H; b += kThreads) occ += L.key(b) != T::kEmpty ? 1u : 0u;
-    occ = wave_sum(occ);
-    if ((tid & 63) == 0) atomicAdd(&s_occ, occ);
-  }
-  __syncthreads();
+  // ---- 7: write back the changed buckets (or rebuild); slot words -------------------
+  // s_occ: the buckets not empty at load (step 2) + inserts into empty buckets (step 6;
+  // tombstones of step 4 keep their buckets occupied) — every write of s_occ is
+  // behind step 6's barriers
   const bool rebuild = s_occ * 4 > H * 3;  // tombstones crowd the table
   if (rebuild) {
     for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
