@@ -9,8 +9,8 @@ O=$R/gpurun_out/prof_r02
 mkdir -p "$O"
 step() { local n=$1 s=$2; shift 2; echo "== $n"; timeout -k 10 "$s" "$@" > "$O/$n.log" 2>&1; local rc=$?; echo "== $n rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
 cd /tmp
-step stats_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c3" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --json-out "$O/bench_c3_prof.json"
-step stats_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c2" -o run -- python3 "$R/bench.py" --config 2 --intervals 60 --steps 10 --warmup 2 --no-cpu-baseline --json-out "$O/bench_c2_prof.json"
+step stats_c3 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c3" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --frag-line 0 --json-out "$O/bench_c3_prof.json"
+step stats_c2 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats_c2" -o run -- python3 "$R/bench.py" --config 2 --intervals 60 --steps 10 --warmup 2 --no-cpu-baseline --frag-line 0 --json-out "$O/bench_c2_prof.json"
 export VARIANTS=0 ROUNDS=3
 step fetch_c3 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch_c3" -o run -- python3 "$R/tools/bench_variants.py"
 step write_c3 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write_c3" -o run -- python3 "$R/tools/bench_variants.py"
