@@ -260,6 +260,36 @@ __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, 
   store_row<Z, NT, double>(power, s, P);
 }
 
+// A container's CPU time (informer.go:229-233, 481-486): delta and total summed
+// over rows [i, e) of s_d in listing order — Go's order, so one lane adds them
+// one after the other.  kB reads are issued together per step; a tail step adds
+// +0.0 for rows past e, an identity on sums that start at +0.0 (neither sum can
+// ever be -0.0), and reads a clamped in-bounds row.
+template <int kB>
+__device__ __forceinline__ void segment_load(const double *s_d, uint32_t i, uint32_t e, double (&v)[kB]) {
+#pragma unroll
+  for (int u = 0; u < kB; ++u) v[u] = s_d[min(i + u, e - 1)];  // e > i: in bounds
+}
+template <int kB>
+__device__ __forceinline__ void segment_add(const double (&v)[kB], uint32_t i, uint32_t e, double &delta,
+                                            double &total) {
+#pragma unroll
+  for (int u = 0; u < kB; ++u) {
+    const double x = i + u < e ? v[u] : 0.0;
+    delta = delta + x;
+    total = total + x;
+  }
+}
+// One batch at a time (kernels short of registers).
+template <int kB>
+__device__ __forceinline__ void segment_sum(const double *s_d, uint32_t i, uint32_t e, double &delta,
+                                            double &total) {
+  for (; i < e; i += kB) {
+    double v[kB];
+    segment_load<kB>(s_d, i, e, v);
+    segment_add<kB>(v, i, e, delta, total);
+  }
+}
 // Slot sweep: a node whose rows' slots span at most kRowsLds slots (the slot
 // join keeps each node in its own slot range) is attributed in SLOT order:
 // 64-slot groups [smin + pos0, +64) moved with 1 KiB-contiguous wave
@@ -676,11 +706,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     }
     if (role == 1) {
       // resetCPUTime on the first process (informer.go:229-233, 481-486)
-      for (uint32_t i = beg - p0; i < end - p0; ++i) {
-        const double di = s_d[i];
-        a_delta = a_delta + di;
-        a_total = a_total + di;
-      }
+      segment_sum<8>(s_d, beg - p0, end - p0, a_delta, a_total);
       s_cd[j] = a_ok ? a_delta : 0.0;
       s_ct[j] = a_ok ? a_total : 0.0;
     } else {
@@ -1266,24 +1292,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           end = max(min(end, p1), beg);
         }
         if (role == 1) {  // informer.go:229-233, 481-486: in order, 4 LDS reads in flight
-          uint32_t i = beg - p0;
-          const uint32_t e = end - p0;
-          for (; i + 4 <= e; i += 4) {
-            const double x0 = s_d[i], x1 = s_d[i + 1], x2 = s_d[i + 2], x3 = s_d[i + 3];
-            a_delta = a_delta + x0;
-            a_total = a_total + x0;
-            a_delta = a_delta + x1;
-            a_total = a_total + x1;
-            a_delta = a_delta + x2;
-            a_total = a_total + x2;
-            a_delta = a_delta + x3;
-            a_total = a_total + x3;
-          }
-          for (; i < e; ++i) {
-            const double di = s_d[i];
-            a_delta = a_delta + di;
-            a_total = a_total + di;
-          }
+          segment_sum<4>(s_d, beg - p0, end - p0, a_delta, a_total);
           s_cd[tid] = a_ok ? a_delta : 0.0;
           s_ct[tid] = a_ok ? a_total : 0.0;
         } else {  // informer.go:445: the last process in listing order wins
@@ -1694,11 +1703,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     double ad = 0.0;
     if (role == 1) {  // informer.go:229-233, 481-486
       double at = a_total[h];
-      for (uint32_t r = beg - p0; r < end - p0; ++r) {
-        const double dr = s_d[r];
-        ad = ad + dr;
-        at = at + dr;
-      }
+      segment_sum<4>(s_d, beg - p0, end - p0, ad, at);
       a_total[h] = at;
       s_cd[j] = a_ok ? ad : 0.0;
       s_ct[j] = a_ok ? at : 0.0;

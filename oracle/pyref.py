@@ -77,8 +77,12 @@ def energy_delta(cur: int, prev: int, max_e: int) -> int:
 class PyRef:
     """Go-shaped state of a fleet of PowerMonitors (one per node)."""
 
-    def __init__(self, zones: int):
+    def __init__(self, zones: int, map_order_rng=None):
+        """map_order_rng: a numpy Generator — sum the node's processes (informer.go:330-333)
+        and each pod's containers (:284-310) in a random order, as Go's map iteration may;
+        None = listing order."""
         self.Z = zones
+        self.rng = map_order_rng
         self.node = {}         # n -> dict(ts, zones=[NodeUsage dict] , ratio, cpu_delta, status)
         self.snap = {k: {} for k in ("proc", "ctr", "vm", "pod")}  # kind -> {slot: [(E, P)] * Z}
         self.ctr_cache = {}    # slot -> [CPUTimeDelta, CPUTotalTime]  (informer containerCache)
@@ -181,13 +185,19 @@ class PyRef:
                 s = w & SLOT_MASK
                 cache = [0.0, 0.0] if (w & SLOT_NEW) else list(self.pod_cache.get(s, [0.0, 0.0]))
                 cache[0] = 0.0
-                for c in range(cbeg, int(a["pod_ctr_end"][q])):
+                members = list(range(cbeg, int(a["pod_ctr_end"][q])))
+                if self.rng is not None:
+                    self.rng.shuffle(members)
+                for c in members:
                     cache[0] += ctr_delta[c][0]
                     cache[1] += ctr_delta[c][1]  # quirk: the container's running total
                 cbeg = int(a["pod_ctr_end"][q])
                 self.pod_cache[s] = cache
-            node_delta = 0.0  # refreshNode: Σ over running processes (listing order here)
-            for i in range(p0, p1):
+            node_delta = 0.0  # refreshNode: Σ over running processes (a map in Go)
+            order = np.arange(p0, p1)
+            if self.rng is not None:
+                self.rng.shuffle(order)
+            for i in order:
                 node_delta += float(d[i])
             self.node[n]["cpu_delta"] = node_delta
             for kind, rows, slots, deltas, pod in (

@@ -126,3 +126,38 @@ def test_adversarial_scenarios_reach_their_edges(oracle_lib):
             seen["idle_wrap"] |= bool((idle < prev_idle).any())  # u64 modular add wrapped
         prev_idle = idle
     assert all(seen.values()), seen
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_any_go_map_order_within_documented_bound(seed, oracle_lib):
+    """The engine fixes one order for the two sums Go takes over maps (the node's
+    ProcessTotalCPUTimeDelta, informer.go:330-333; a pod's containers, :284-310).  Against
+    the Python restatement summing both in random orders (one of Go's map orders per node
+    and pod per interval), over 6 intervals with churn and pods of several containers:
+    CPU-time deltas / totals within 1e-12 relative, energies within 1 µJ per interval per
+    workload, powers within 1e-12 relative."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.make_layout(8, [300, 1200, 64, 2000, 7, 900, 450, 1], 4, seed=seed, ctrs_per_pod=4.0)
+    caps = layout.capacities()
+    sim = fleet.FleetSim(layout, seed=seed, churn=0.05)
+    ora = Oracle(layout.zones, **caps)
+    ref = PyRef(layout.zones, map_order_rng=np.random.default_rng(100 + seed))
+    K = 6
+    for _ in range(K):
+        a = sim.next_interval()
+        ora.interval(a, layout.sizes())
+        ref.interval(a)
+    got = ref.tables(layout.n_nodes, caps)
+    for tname, _ in accel.TABLES:
+        want, have = ora.state[tname], got[tname]
+        if want.dtype == np.float64:
+            np.testing.assert_allclose(have, want, rtol=1e-12, atol=0, err_msg=tname)
+        elif tname.endswith(("energy", "_total")) and want.dtype == np.uint64:
+            diff = np.abs(have.astype(np.int64) - want.astype(np.int64))
+            assert diff.max() <= K, (tname, int(diff.max()))
+        else:
+            np.testing.assert_array_equal(have, want, err_msg=tname)
+    # the random orders did change some low bits (the test exercises the bound)
+    assert any(not np.array_equal(got[t].view(np.uint64), ora.state[t].view(np.uint64))
+               for t in ("node_cpu_delta", "pod_cpu_delta", "pod_cpu_total", "proc_energy", "pod_energy"))
