@@ -28,6 +28,10 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *batches
 int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                             uint32_t *out_slot, uint64_t *term_key, uint32_t *term_slot,
                             uint32_t *term_count, void *stream, uint32_t stop_after);
+/* Small-node join variant (bits: 1 lock-step lookups, 2 error bits in a register,
+ * 4 LDS-only barriers, 8 duplicates found by the insert, 16 shared scan barrier);
+ * -1 = production.  Every variant computes the same results.  Returns the old value. */
+int kacc_debug_set_join_variant(int variant);
 
 #ifdef __cplusplus
 }

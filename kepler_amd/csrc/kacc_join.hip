@@ -259,10 +259,71 @@ __device__ __forceinline__ void span_out(const Args &a, uint32_t n, uint32_t lo,
 // workgroup at <= 40 KiB of LDS, i.e. 4 workgroups (8 waves/SIMD) per CU.
 constexpr uint32_t kNewCap = 512;  // new rows handled as a compact list
 
-template <typename K>
-__global__ __launch_bounds__(kThreads) void join_small(const Args a) {
+// Variant bits of join_small (timing ablations; production = kJoinDefault):
+constexpr int kJLock = 1;      // lookups of a lane's rows in lock-step (one LDS round trip per depth)
+constexpr int kJErrReg = 2;    // error bits gathered in a register, one atomic per lane at the end
+constexpr int kJLdsBar = 4;    // LDS-only barriers (never wait for the node's global stores)
+constexpr int kJInsDup = 8;    // duplicates found by the insert itself (no re-probe pass)
+constexpr int kJScan2 = 16;    // the two block scans of step 3 share their barrier
+
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int V>
+__device__ __forceinline__ void jbar() {
+  if constexpr ((V & kJLdsBar) != 0)
+    lds_barrier();
+  else
+    __syncthreads();
+}
+
+// Two exclusive block-wide scans at once (one barrier; s_wave [2 * waves]).
+// The caller puts a barrier between this and the next write of s_wave.
+template <int V>
+__device__ __forceinline__ void block_scan2(uint32_t v0, uint32_t v1, uint32_t *s_wave, uint32_t &ex0,
+                                            uint32_t &ex1, uint32_t &tot0, uint32_t &tot1) {
+  constexpr int kW = kThreads / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t x0 = v0, x1 = v1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y0 = __shfl_up(x0, d, 64), y1 = __shfl_up(x1, d, 64);
+    if (lane >= d) {
+      x0 += y0;
+      x1 += y1;
+    }
+  }
+  if (lane == 63) {
+    s_wave[wave] = x0;
+    s_wave[kW + wave] = x1;
+  }
+  jbar<V>();
+  uint32_t b0 = 0, b1 = 0, t0 = 0, t1 = 0;
+#pragma unroll
+  for (int w = 0; w < kW; ++w) {
+    const uint32_t a0 = s_wave[w], a1 = s_wave[kW + w];
+    if (w < wave) {
+      b0 += a0;
+      b1 += a1;
+    }
+    t0 += a0;
+    t1 += a1;
+  }
+  ex0 = b0 + x0 - v0;
+  ex1 = b1 + x1 - v1;
+  tot0 = t0;
+  tot1 = t1;
+}
+
+template <typename K, int V>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(K) == 8 ? 4 : 8))) void join_small(const Args a) {
   using T = Tab<K>;
   constexpr bool kWide = sizeof(K) == 8;
+  constexpr bool kLock = (V & kJLock) != 0, kErrReg = (V & kJErrReg) != 0, kInsDup = (V & kJInsDup) != 0;
+  constexpr bool kScan2 = (V & kJScan2) != 0;
   __shared__ uint64_t s_ent[kLdsBuckets];              // entries (u32 keys) / keys (u64)
   __shared__ uint32_t s_slot[kWide ? kLdsBuckets : 1];  // slots (u64 keys)
   __shared__ uint32_t s_used[kSmallWords];  // bit s: slot s held by a live ID
@@ -273,14 +334,14 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   __shared__ K s_newkey[kNewCap];
   __shared__ uint8_t s_newbad[kNewCap];
   __shared__ uint32_t s_dirty[kLdsBuckets / 32];
-  __shared__ uint32_t s_wave[kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
+  __shared__ uint32_t s_wave[2 * kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
   __shared__ uint32_t s_occ;
 
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
   if (n >= a.n_nodes) return;
   NodeView v;
   if (!node_view<true>(a, n, v)) return;
-  const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H;
+  const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H, hmask = H - 1;
   const uint32_t W = (S + 31) / 32;
   const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
   T G, L;
@@ -294,7 +355,14 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     L.e = s_ent;
   }
   auto lslot = [&](uint32_t b) -> uint32_t { return L.slot(b); };
-  const Probe<K> pr{L, v.shift, H - 1, H};
+  const Probe<K> pr{L, v.shift, hmask, H};
+  uint32_t errs = 0;  // kErrReg: this lane's error bits
+  auto raise = [&](uint32_t bits) {
+    if constexpr (kErrReg)
+      errs |= bits;
+    else
+      atomicOr(a.err, bits);
+  };
 
   // ---- 1: table -> LDS, keys -> registers, marks cleared ---------------------------
   // All loads of the phase are issued before the first LDS store (register
@@ -338,7 +406,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
       }
     }
   }
-  __syncthreads();
+  jbar<V>();
   if (a.stop_after == 1u) return;  // timing ablation
 
   // ---- 2: held slots and the occupancy, from this lane's buckets still in registers;
@@ -363,32 +431,85 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
   }
   uint32_t mine = 0;  // new rows of this lane
+  if constexpr (kLock) {
+    // every row of the lane probes in lock-step: unconditional LDS reads per depth
+    uint32_t pb[kRpl];
+    uint32_t state = 0;  // 2 bits per row: 0 idle, 1 probing, 2 found, 3 absent
 #pragma unroll
-  for (int j = 0; j < kRpl; ++j) {
-    const uint32_t r = tid * kRpl + j;
-    res[j] = kInvalid;
-    if (r >= R) continue;
-    const K k = key[j];
-    if (k == T::kEmpty || k == T::kTomb) {
-      atomicOr(a.err, kErrKey);
-      continue;
+    for (int j = 0; j < kRpl; ++j) {
+      const uint32_t r = tid * kRpl + j;
+      res[j] = kInvalid;
+      pb[j] = bucket(key[j], v.shift);
+      if (r >= R) continue;
+      if (key[j] == T::kEmpty || key[j] == T::kTomb) {
+        raise(kErrKey);
+        continue;
+      }
+      state |= 1u << (2 * j);
     }
-    const uint32_t b = pr.find(k);
-    if (b == ~0u) {
-      res[j] = kPending;
-      ++mine;
-      continue;
+    for (uint32_t depth = 0; depth < H; ++depth) {
+      K kk[kRpl];
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) kk[j] = static_cast<K>(L.key(pb[j]));
+      uint32_t probing = 0;
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        const uint32_t sj = (state >> (2 * j)) & 3u;
+        const bool hit = kk[j] == key[j], empty = kk[j] == T::kEmpty;
+        const bool act = sj == 1u;
+        const uint32_t nv = hit ? 2u : empty ? 3u : 1u;  // found / absent / next bucket
+        state = act ? (state & ~(3u << (2 * j))) | (nv << (2 * j)) : state;
+        const bool step = act && !hit && !empty;
+        pb[j] = step ? ((pb[j] + 1) & hmask) : pb[j];
+        probing |= step ? 1u : 0u;
+      }
+      if (__ballot(probing) == 0) break;
     }
-    const uint32_t sl = lslot(b);
-    if (sl >= S) continue;
-    const uint32_t bit = 1u << (sl & 31);
-    if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
-      atomicOr(a.err, kErrKey);
-      continue;
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j) {
+      const uint32_t sj = (state >> (2 * j)) & 3u;
+      if (sj == 3u) {
+        res[j] = kPending;
+        ++mine;
+      } else if (sj == 2u) {
+        const uint32_t sl = lslot(pb[j]);
+        if (sl >= S) continue;
+        const uint32_t bit = 1u << (sl & 31);
+        if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
+          raise(kErrKey);
+          continue;
+        }
+        res[j] = s0 + sl;
+      }
     }
-    res[j] = s0 + sl;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j) {
+      const uint32_t r = tid * kRpl + j;
+      res[j] = kInvalid;
+      if (r >= R) continue;
+      const K k = key[j];
+      if (k == T::kEmpty || k == T::kTomb) {
+        raise(kErrKey);
+        continue;
+      }
+      const uint32_t b = pr.find(k);
+      if (b == ~0u) {
+        res[j] = kPending;
+        ++mine;
+        continue;
+      }
+      const uint32_t sl = lslot(b);
+      if (sl >= S) continue;
+      const uint32_t bit = 1u << (sl & 31);
+      if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
+        raise(kErrKey);
+        continue;
+      }
+      res[j] = s0 + sl;
+    }
   }
-  __syncthreads();
+  jbar<V>();
   if (a.stop_after == 2u) return;  // timing ablation
 
   // ---- 3: per-word free / terminated bits and their prefixes -------------------------
@@ -401,13 +522,17 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     s_tmask[tid] = tm;
     packed = (static_cast<uint32_t>(__popc(fm)) << 16) | static_cast<uint32_t>(__popc(tm));
   }
-  uint32_t ptot, ntot;
-  const uint32_t pex = block_scan(packed, s_wave, ptot);
-  const uint32_t rank0 = block_scan(mine, s_wave, ntot);  // this lane's first new-row rank
+  uint32_t ptot, ntot, pex, rank0;  // rank0: this lane's first new-row rank
+  if constexpr (kScan2) {
+    block_scan2<V>(packed, mine, s_wave, pex, rank0, ptot, ntot);
+  } else {
+    pex = block_scan(packed, s_wave, ptot);
+    rank0 = block_scan(mine, s_wave, ntot);
+  }
   if (tid < W) s_wpre[tid] = pex;
   const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot;
   if (tid == 0) a.term_count[n] = n_term;
-  __syncthreads();
+  jbar<V>();
   if (a.stop_after == 3u) return;  // timing ablation
 
   // ---- 4: terminated list (slot order) + tombstones; the first free slots ------------
@@ -432,7 +557,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     for (uint32_t fm = s_fmask[tid]; fm && p < want; fm &= fm - 1, ++p)
       s_free[p] = static_cast<uint16_t>(tid * 32 + __builtin_ctz(fm));
   }
-  __syncthreads();
+  jbar<V>();
   if (a.stop_after == 4u) return;  // timing ablation
 
   // ---- 5: new rows take slots in row order ------------------------------------------
@@ -452,7 +577,7 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     rk[j] = ~0u;
     if (res[j] != kPending) continue;
     if (q >= total_free) {
-      atomicOr(a.err, kErrRange);
+      raise(kErrRange);
       res[j] = kInvalid;
       ++q;
       continue;
@@ -466,46 +591,88 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
     }
     ++q;
   }
-  __syncthreads();
+  jbar<V>();
   if (a.stop_after == 5u) return;  // timing ablation
 
-  // ---- 6: inserts (one lane per new row), then a re-probe flags an ID twice ---------
+  // ---- 6: inserts (one lane per new row); an ID given twice in the node is flagged ---
+  // kJInsDup: by the insert that meets its own key on the probe path (buckets only
+  // fill during this step, so of two rows with one ID the later claimant always
+  // passes the earlier's bucket); otherwise by a re-probe after every insert.
   const uint32_t n_ins = min(n_new, total_free);
   uint32_t fresh = 0;  // inserts into empty buckets (occupancy)
+  auto insert_dup = [&](K k, uint32_t rel) -> uint32_t {  // bucket, ~0u full, ~1u duplicate
+    uint32_t b = bucket(k, v.shift);
+    for (uint32_t p = 0; p < H;) {
+      const uint64_t raw = L.raw(b);
+      const K kk = static_cast<K>(T::key_of(raw));
+      if (kk == k) return ~1u;
+      if (kk == T::kEmpty || kk == T::kTomb) {
+        if (L.claim(b, raw, k, rel)) {
+          fresh += kk == T::kEmpty ? 1u : 0u;
+          return b;
+        }
+        continue;  // lost the race for this bucket: look at it again
+      }
+      ++p;
+      b = (b + 1) & hmask;
+    }
+    return ~0u;
+  };
   if (compact) {
     for (uint32_t i = tid; i < n_ins; i += kThreads) {
-      const uint32_t b = pr.insert(s_newkey[i], s_free[i], &fresh);
-      if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+      if constexpr (kInsDup) {
+        const uint32_t b = insert_dup(s_newkey[i], s_free[i]);
+        if (b >= ~1u) s_newbad[i] = 1;
+        else atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+      } else {
+        const uint32_t b = pr.insert(s_newkey[i], s_free[i], &fresh);
+        if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+      }
     }
     if (fresh) atomicAdd(&s_occ, fresh);
-    __syncthreads();
-    for (uint32_t i = tid; i < n_ins; i += kThreads) {
-      const uint32_t b = pr.find(s_newkey[i]);
-      if (b == ~0u || lslot(b) != s_free[i]) s_newbad[i] = 1;
+    jbar<V>();
+    if constexpr (!kInsDup) {
+      for (uint32_t i = tid; i < n_ins; i += kThreads) {
+        const uint32_t b = pr.find(s_newkey[i]);
+        if (b == ~0u || lslot(b) != s_free[i]) s_newbad[i] = 1;
+      }
+      jbar<V>();
     }
-    __syncthreads();
 #pragma unroll
     for (int j = 0; j < kRpl; ++j)
       if (rk[j] != ~0u && s_newbad[rk[j]]) {
-        atomicOr(a.err, kErrKey);
+        raise(kErrKey);
         res[j] = kInvalid;
       }
   } else {  // first interval / mass churn: each lane inserts its own rows
 #pragma unroll
     for (int j = 0; j < kRpl; ++j) {
       if (rk[j] == ~0u) continue;
-      const uint32_t b = pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0, &fresh);
-      if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+      if constexpr (kInsDup) {
+        const uint32_t b = insert_dup(key[j], (res[j] & KACC_SLOT_MASK) - s0);
+        if (b >= ~1u) {
+          raise(kErrKey);
+          res[j] = kInvalid;
+          rk[j] = ~0u;
+        } else {
+          atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+        }
+      } else {
+        const uint32_t b = pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0, &fresh);
+        if (b != ~0u) atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+      }
     }
     if (fresh) atomicAdd(&s_occ, fresh);
-    __syncthreads();
+    jbar<V>();
+    if constexpr (!kInsDup) {
 #pragma unroll
-    for (int j = 0; j < kRpl; ++j) {
-      if (rk[j] == ~0u) continue;
-      const uint32_t b = pr.find(key[j]);
-      if (b == ~0u || lslot(b) != (res[j] & KACC_SLOT_MASK) - s0) {
-        atomicOr(a.err, kErrKey);
-        res[j] = kInvalid;
+      for (int j = 0; j < kRpl; ++j) {
+        if (rk[j] == ~0u) continue;
+        const uint32_t b = pr.find(key[j]);
+        if (b == ~0u || lslot(b) != (res[j] & KACC_SLOT_MASK) - s0) {
+          raise(kErrKey);
+          res[j] = kInvalid;
+        }
       }
     }
   }
@@ -517,12 +684,12 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
   const bool rebuild = s_occ * 4 > H * 3;  // tombstones crowd the table
   if (rebuild) {
     for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
-    __syncthreads();
+    jbar<V>();
 #pragma unroll
     for (int j = 0; j < kRpl; ++j) {
       if (res[j] != kInvalid) pr.insert(key[j], (res[j] & KACC_SLOT_MASK) - s0);
     }
-    __syncthreads();
+    jbar<V>();
     for (uint32_t b = tid; b < H; b += kThreads) {
       if constexpr (kWide) {
         G.k[b] = s_ent[b];
@@ -554,7 +721,31 @@ __global__ __launch_bounds__(kThreads) void join_small(const Args a) {
       hi = max(hi, res[j] & KACC_SLOT_MASK);
     }
   }
-  if (a.out_span) span_out(a, n, lo, hi, s_lo, s_hi);
+  if constexpr (kErrReg) {
+    if (errs) atomicOr(a.err, errs);
+  }
+  if (a.out_span) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
+      hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
+    }
+    if ((tid & 63) == 0) {
+      s_lo[tid >> 6] = lo;
+      s_hi[tid >> 6] = hi;
+    }
+    jbar<V>();
+    if (tid == 0) {
+#pragma unroll
+      for (int w = 1; w < kThreads / 64; ++w) {
+        lo = min(lo, s_lo[w]);
+        hi = max(hi, s_hi[w]);
+      }
+      const bool none = lo > hi;
+      a.out_span[2 * n] = none ? 1u : lo;
+      a.out_span[2 * n + 1] = none ? 0u : hi;
+    }
+  }
 }
 
 // ============================ big nodes (global table) =============================
@@ -853,6 +1044,12 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
                      uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream,
                      uint32_t stop_after);
 
+namespace {
+constexpr int kJoinDefault = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
+                             kacc::join::kJInsDup | kacc::join::kJScan2;
+int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
+}  // namespace
+
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                    uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream) {
@@ -865,6 +1062,12 @@ int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *ro
                             uint32_t *term_count, void *stream, uint32_t stop_after) {
   return slot_join(m, n_rows, row_off, keys, nullptr, out_slot, term_key, term_slot, term_count,
                    nullptr, stream, stop_after);
+}
+
+int kacc_debug_set_join_variant(int variant) {
+  const int prev = g_join_variant;
+  g_join_variant = variant;
+  return prev;
 }
 
 }  // extern "C"
@@ -901,11 +1104,23 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   (void)hipGetLastError();  // a stale error of an earlier call must not be blamed on this launch
   using namespace kacc::join;
   const dim3 grid(m->n_nodes), block(kThreads);
+  auto small = [&](auto key) {
+    using K = decltype(key);
+    switch (g_join_variant) {
+      case 0: hipLaunchKernelGGL((join_small<K, 0>), grid, block, 0, st, a); break;
+      case 1: hipLaunchKernelGGL((join_small<K, 1>), grid, block, 0, st, a); break;
+      case 3: hipLaunchKernelGGL((join_small<K, 3>), grid, block, 0, st, a); break;
+      case 7: hipLaunchKernelGGL((join_small<K, 7>), grid, block, 0, st, a); break;
+      case 15: hipLaunchKernelGGL((join_small<K, 15>), grid, block, 0, st, a); break;
+      case 6: hipLaunchKernelGGL((join_small<K, 6>), grid, block, 0, st, a); break;
+      default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
+    }
+  };
   if (m->kind == KACC_KIND_PROC) {
-    hipLaunchKernelGGL((join_small<uint32_t>), grid, block, 0, st, a);
+    small(uint32_t{});
     if (m->has_big) hipLaunchKernelGGL((join_big<uint32_t>), grid, block, 0, st, a);
   } else {
-    hipLaunchKernelGGL((join_small<uint64_t>), grid, block, 0, st, a);
+    small(uint64_t{});
     if (m->has_big) hipLaunchKernelGGL((join_big<uint64_t>), grid, block, 0, st, a);
   }
   KACC_HIP(ctx, hipGetLastError());
