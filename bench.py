@@ -354,7 +354,6 @@ def main():
     wall = time.perf_counter() - t0
     acc.sync(stream)  # surfaces any device-detected range error
     kernel_ms = [a.elapsed_time(b) / K for a, b in events]  # per interval
-
     # same-box reference for the roofline: a 1.28 GB device-to-device copy
     src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
     dst = torch.empty_like(src)
@@ -428,6 +427,7 @@ def main():
         },
         "node_snapshots_per_s": total_nodes_done * K * args.steps / wall_max,
         "kernel_ms": k_avg_ms,
+        "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
