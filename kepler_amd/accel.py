@@ -17,7 +17,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libkepler_accel.so")
+LIB_PATH = os.environ.get("KACC_LIB", os.path.join(_HERE, "lib", "libkepler_accel.so"))  # KACC_LIB: A/B builds
 
 KACC_ABI_VERSION = 2
 KACC_MAX_ZONES = 8

@@ -191,67 +191,187 @@ __device__ Dec shortest(uint64_t frac, uint32_t bexp) {
   return Dec{out, e10 + removed};
 }
 
-// Field writer: up to kFmtWidth bytes in registers.
-struct Field {
-  char c[KACC_FMT_WIDTH];
-  uint32_t n = 0;
-  __device__ void put(char ch) { c[n++] = ch; }
-  __device__ void puts(const char *s) {
-    while (*s) put(*s++);
-  }
+// The value field in registers: a 24-byte little-endian byte string (byte k
+// of the text = bits 8(k & 7) of word k >> 3), assembled with whole-word
+// shifts and masks — no per-byte indexing (a dynamically indexed register
+// array compiles to select chains: ~4k instructions per value before).
+struct Text {
+  uint64_t w[3];
+  uint32_t n;  // bytes
 };
 
+__device__ __forceinline__ void shl_bytes(uint64_t (&w)[3], uint32_t k) {  // bytes move up by k (< 24)
+  const uint32_t s = 8 * k;
+  if (s >= 128) {
+    w[2] = w[0] << (s - 128);
+    w[1] = 0;
+    w[0] = 0;
+  } else if (s >= 64) {
+    const uint32_t t = s - 64;
+    w[2] = (w[1] << t) | (t ? w[0] >> (64 - t) : 0);
+    w[1] = w[0] << t;
+    w[0] = 0;
+  } else if (s) {
+    w[2] = (w[2] << s) | (w[1] >> (64 - s));
+    w[1] = (w[1] << s) | (w[0] >> (64 - s));
+    w[0] <<= s;
+  }
+}
+__device__ __forceinline__ void shr_bytes(uint64_t (&w)[3], uint32_t k) {  // bytes move down by k (< 24)
+  const uint32_t s = 8 * k;
+  if (s >= 128) {
+    w[0] = w[2] >> (s - 128);
+    w[1] = 0;
+    w[2] = 0;
+  } else if (s >= 64) {
+    const uint32_t t = s - 64;
+    w[0] = (w[1] >> t) | (t ? w[2] << (64 - t) : 0);
+    w[1] = w[2] >> t;
+    w[2] = 0;
+  } else if (s) {
+    w[0] = (w[0] >> s) | (w[1] << (64 - s));
+    w[1] = (w[1] >> s) | (w[2] << (64 - s));
+    w[2] >>= s;
+  }
+}
+// bytes [0, k) of w stay, the rest are cleared (k <= 24)
+__device__ __forceinline__ void keep_bytes(uint64_t (&w)[3], uint32_t k) {
+  const uint32_t s = 8 * k;
+  w[0] &= s >= 64 ? ~0ull : (1ull << s) - 1;
+  w[1] &= s >= 128 ? ~0ull : s <= 64 ? 0ull : (1ull << (s - 64)) - 1;
+  w[2] &= s >= 192 ? ~0ull : s <= 128 ? 0ull : (1ull << (s - 128)) - 1;
+}
+// the byte string c (up to 8 bytes, at most 24 - k of them) ORed in at byte k
+__device__ __forceinline__ void or_at(uint64_t (&w)[3], uint32_t k, uint64_t c) {
+  uint64_t v[3] = {c, 0, 0};
+  shl_bytes(v, k);
+  w[0] |= v[0];
+  w[1] |= v[1];
+  w[2] |= v[2];
+}
+// byte c inserted at position p: bytes [p, 23) move up by one
+__device__ __forceinline__ void insert_byte(uint64_t (&w)[3], uint32_t p, uint8_t c) {
+  uint64_t hi[3] = {w[0], w[1], w[2]};
+  shl_bytes(hi, 1);
+  uint64_t m[3] = {~0ull, ~0ull, ~0ull};
+  keep_bytes(m, p + 1);  // bytes [0, p] of the shifted copy are dropped
+  keep_bytes(w, p);
+  w[0] |= hi[0] & ~m[0];
+  w[1] |= hi[1] & ~m[1];
+  w[2] |= hi[2] & ~m[2];
+  or_at(w, p, c);
+}
+
+// Four / eight ASCII digits of v (leading zeros kept), most significant at byte 0.
+__device__ __forceinline__ uint32_t ascii4(uint32_t v) {  // v < 10^4
+  const uint32_t a = (v * 5243u) >> 19;                    // v / 100 (exact for v < 43699)
+  const uint32_t b = v - a * 100u;
+  const uint32_t a1 = (a * 103u) >> 10, b1 = (b * 103u) >> 10;  // / 10 (exact below 179)
+  return 0x30303030u | a1 | ((a - a1 * 10u) << 8) | (b1 << 16) | ((b - b1 * 10u) << 24);
+}
+__device__ __forceinline__ uint64_t ascii8(uint32_t v) {  // v < 10^8
+  const uint32_t hi = __umulhi(v, 0xD1B71759u) >> 13;      // v / 10^4
+  return static_cast<uint64_t>(ascii4(hi)) | (static_cast<uint64_t>(ascii4(v - hi * 10000u)) << 32);
+}
+
+// Digit count of m (1 <= m < 10^17).
+__device__ __forceinline__ uint32_t digits10(uint64_t m) {
+  uint32_t nd = 1;
+  uint64_t p = 10;
+#pragma unroll
+  for (int k = 1; k < 17; ++k, p *= 10) nd += m >= p ? 1u : 0u;
+  return nd;
+}
+
+// strconv 'g' -1 layout (the %e / %f choice of Go's %g with shortest digits) of
+// the decimal m x 10^e10 (m < 10^17 with no trailing zero), after the sign.
+__device__ void write_dec(bool neg, Dec d, Text &t) {
+  const uint64_t m = d.m;
+  const uint64_t q = __umul64hi(m, 0xABCC77118461CEFDull) >> 26;  // m / 10^8 (m < 2^64)
+  const uint32_t r = static_cast<uint32_t>(m - q * 100000000ull);
+  const uint32_t q32 = static_cast<uint32_t>(q);                  // < 10^9
+  const uint32_t q1 = __umulhi(q32, 0xABCC7712u) >> 26;          // q / 10^8 (< 10)
+  const uint32_t q0 = q32 - q1 * 100000000u;
+  const uint64_t a0 = ascii8(q0), a1 = ascii8(r);
+  // the 17 digits, most significant first, then drop the leading zeros
+  uint64_t w[3] = {(0x30ull + q1) | (a0 << 8), (a0 >> 56) | (a1 << 8), a1 >> 56};
+  const uint32_t nd = digits10(m);
+  shr_bytes(w, 17 - nd);
+  keep_bytes(w, nd);
+  const int32_t dp = static_cast<int32_t>(nd) + d.e;  // value = 0.DIGITS x 10^dp
+  const int32_t x = dp - 1;
+  uint32_t n;
+  if (x < -4 || x >= 6) {  // %e with nd - 1 fraction digits
+    n = nd;
+    if (nd > 1) {
+      insert_byte(w, 1, '.');
+      ++n;
+    }
+    const uint32_t ax = static_cast<uint32_t>(x < 0 ? -x : x);
+    const uint32_t h = ax / 100, tt = (ax / 10) % 10, u = ax % 10;
+    uint64_t suf = 'e' | (static_cast<uint64_t>(x < 0 ? '-' : '+') << 8);
+    uint32_t sl = 2;
+    if (h) suf |= static_cast<uint64_t>('0' + h) << (8 * sl++);
+    suf |= static_cast<uint64_t>('0' + tt) << (8 * sl++);
+    suf |= static_cast<uint64_t>('0' + u) << (8 * sl++);
+    or_at(w, n, suf);
+    n += sl;
+  } else if (dp >= static_cast<int32_t>(nd)) {  // integer: dp - nd zeros (at most 5)
+    or_at(w, nd, 0x303030303030ull & ((1ull << (8 * (dp - nd))) - 1));
+    n = static_cast<uint32_t>(dp);
+  } else if (dp > 0) {  // d.ddd
+    insert_byte(w, static_cast<uint32_t>(dp), '.');
+    n = nd + 1;
+  } else {  // 0.000ddd: 2 - dp bytes before the digits (dp >= -3)
+    const uint32_t pre = static_cast<uint32_t>(2 - dp);
+    shl_bytes(w, pre);
+    w[0] |= 0x303030302E30ull & ((1ull << (8 * pre)) - 1);  // "0." then zeros
+    n = nd + pre;
+  }
+  if (neg) {
+    shl_bytes(w, 1);
+    w[0] |= '-';
+    ++n;
+  }
+  t.w[0] = w[0];
+  t.w[1] = w[1];
+  t.w[2] = w[2];
+  t.n = n;
+}
+
 // expfmt writeFloat / strconv.AppendFloat(f, 'g', -1, 64)
-__device__ void write_float(double f, Field &o) {
-  if (f == 1.0) return o.put('1');
-  if (f == 0.0) return o.put('0');
-  if (f == -1.0) return o.puts("-1");
-  if (f != f) return o.puts("NaN");
+__device__ void write_float(double f, Text &t) {
+  t.w[1] = t.w[2] = 0;
+  if (f == 1.0) { t.w[0] = '1'; t.n = 1; return; }
+  if (f == 0.0) { t.w[0] = '0'; t.n = 1; return; }
+  if (f == -1.0) { t.w[0] = 0x312Dull; t.n = 2; return; }        // "-1"
+  if (f != f) { t.w[0] = 0x4E614Eull; t.n = 3; return; }          // "NaN"
   const uint64_t bits = static_cast<uint64_t>(__double_as_longlong(f));
   const bool neg = (bits >> 63) != 0;
   const uint32_t bexp = static_cast<uint32_t>((bits >> 52) & 0x7ff);
   const uint64_t frac = bits & ((1ull << 52) - 1);
-  if (bexp == 0x7ff) return o.puts(neg ? "-Inf" : "+Inf");
-  const Dec d = shortest(frac, bexp);
-  // digits of d.m, most significant first
-  char dig[20];
-  int nd = 0;
-  for (uint64_t m = d.m; m;) {
+  if (bexp == 0x7ff) { t.w[0] = neg ? 0x666E492Dull : 0x666E492Bull; t.n = 4; return; }  // "-Inf" / "+Inf"
+  write_dec(neg, shortest(frac, bexp), t);
+}
+
+// Joules() of a u64 µJ energy, float64(e) / 1e6 (energy.go:30-32), written as
+// write_float writes it.  Below 10^15 µJ the decimal e·10^-6 has at most 15
+// significant digits, and it rounds to the quotient (a correctly rounded
+// division); distinct decimals of <= 15 significant digits are distinct
+// doubles (DBL_DIG = 15), so no other decimal of that length or shorter lies
+// in the quotient's rounding interval: the shortest round-trip digits are e's
+// own digits with the trailing zeros dropped — no Ryū step needed.
+__device__ void write_joules(uint64_t e, Text &t) {
+  if (e == 0 || e == 1000000u || e >= 1000000000000000ull) return write_float(static_cast<double>(e) / 1e6, t);
+  uint64_t m = e;
+  int32_t x = -6;
+  for (;;) {
     const uint64_t q = div10(m);
-    dig[nd++] = static_cast<char>('0' + (m - 10 * q));
+    if (m - 10 * q != 0) break;
     m = q;
+    ++x;
   }
-  for (int i = 0; i < nd / 2; ++i) {
-    const char t = dig[i];
-    dig[i] = dig[nd - 1 - i];
-    dig[nd - 1 - i] = t;
-  }
-  const int dp = nd + d.e;  // value = 0.dig x 10^dp
-  const int x = dp - 1;
-  if (neg) o.put('-');
-  if (x < -4 || x >= 6) {  // %e with nd-1 fraction digits
-    o.put(dig[0]);
-    if (nd > 1) {
-      o.put('.');
-      for (int i = 1; i < nd; ++i) o.put(dig[i]);
-    }
-    o.put('e');
-    o.put(x < 0 ? '-' : '+');
-    const int a = x < 0 ? -x : x;
-    if (a >= 100) o.put(static_cast<char>('0' + a / 100));
-    o.put(static_cast<char>('0' + (a / 10) % 10));
-    o.put(static_cast<char>('0' + a % 10));
-    return;
-  }
-  if (dp > 0) {  // %f with max(nd - dp, 0) fraction digits
-    for (int i = 0; i < dp; ++i) o.put(i < nd ? dig[i] : '0');
-  } else {
-    o.put('0');
-  }
-  if (nd > dp) {
-    o.put('.');
-    for (int i = dp; i < nd; ++i) o.put(i >= 0 ? dig[i] : '0');
-  }
+  write_dec(false, Dec{m, x}, t);
 }
 
 struct Args {
@@ -265,19 +385,15 @@ struct Args {
 __global__ __launch_bounds__(kThreads) void format_kernel(const Args a) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= a.count) return;
-  double f;
+  Text o;
   if (a.is_energy)
-    f = static_cast<double>(static_cast<const uint64_t *>(a.src)[i]) / 1e6;  // energy.go:30-32
+    write_joules(static_cast<const uint64_t *>(a.src)[i], o);  // energy.go:30-32
   else
-    f = static_cast<const double *>(a.src)[i] / 1e6;  // energy.go:57-59
-  Field o;
-  write_float(f, o);
-  uint64_t w[3] = {0, 0, 0};
-  for (uint32_t k = 0; k < o.n; ++k) w[k >> 3] |= static_cast<uint64_t>(static_cast<uint8_t>(o.c[k])) << (8 * (k & 7));
+    write_float(static_cast<const double *>(a.src)[i] / 1e6, o);  // energy.go:57-59
   uint64_t *dst = reinterpret_cast<uint64_t *>(a.out + i * KACC_FMT_WIDTH);
-  dst[0] = w[0];
-  dst[1] = w[1];
-  dst[2] = w[2];
+  dst[0] = o.w[0];
+  dst[1] = o.w[1];
+  dst[2] = o.w[2];
   a.len[i] = static_cast<uint8_t>(o.n);
 }
 
@@ -301,8 +417,6 @@ struct LineArgs {
   uint32_t zone_pos[KACC_MAX_ZONES + 1];  // zone name j = consts[zone_pos[j], + zone_len[j]) (4-aligned)
   uint32_t zone_len[KACC_MAX_ZONES];
   uint32_t const_len;
-  char *vals;        // temp [lines * KACC_FMT_WIDTH]
-  uint8_t *vlen;     // temp [lines]
   uint64_t *len;     // temp [lines + 1]
   uint64_t *line_off;  // [lines + 1]
   char *out;
@@ -315,7 +429,16 @@ __device__ __forceinline__ uint64_t line_row(const LineArgs &a, uint64_t r) {
   return a.row_order ? min(static_cast<uint64_t>(a.row_order[r]), a.count - 1) : r;
 }
 
-// Pass 1: the value field of every line and the line's length.
+// The value field of table entry e (the write pass formats it again instead
+// of reading a stored copy: the formatting is cheaper than 2 x 24 B of traffic).
+__device__ __forceinline__ void line_value(const LineArgs &a, uint64_t e, Text &o) {
+  if (a.is_energy)
+    write_joules(static_cast<const uint64_t *>(a.src)[e], o);  // energy.go:30-32
+  else
+    write_float(static_cast<const double *>(a.src)[e] / 1e6, o);  // energy.go:57-59
+}
+
+// Pass 1: the length of every line.
 __global__ __launch_bounds__(kThreads) void line_len_kernel(const LineArgs a) {
   const uint64_t lines = a.count * a.n_zones;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < lines;
@@ -324,20 +447,8 @@ __global__ __launch_bounds__(kThreads) void line_len_kernel(const LineArgs a) {
     const uint32_t j = static_cast<uint32_t>(i - ri * a.n_zones);
     const uint64_t r = line_row(a, ri);
     const uint64_t e = (a.first + r) * a.Z + a.zone_table[j];
-    double f;
-    if (a.is_energy)
-      f = static_cast<double>(static_cast<const uint64_t *>(a.src)[e]) / 1e6;  // energy.go:30-32
-    else
-      f = static_cast<const double *>(a.src)[e] / 1e6;  // energy.go:57-59
-    Field o;
-    write_float(f, o);
-    uint64_t w[3] = {0, 0, 0};
-    for (uint32_t k = 0; k < o.n; ++k) w[k >> 3] |= static_cast<uint64_t>(static_cast<uint8_t>(o.c[k])) << (8 * (k & 7));
-    uint64_t *dst = reinterpret_cast<uint64_t *>(a.vals + i * KACC_FMT_WIDTH);
-    dst[0] = w[0];
-    dst[1] = w[1];
-    dst[2] = w[2];
-    a.vlen[i] = static_cast<uint8_t>(o.n);
+    Text o;
+    line_value(a, e, o);
     const uint64_t ll = a.label_off[r + 1] - a.label_off[r];
     const uint32_t zl = a.zone_len[j];
     // NAME { LABELS ,zone=" ZONE "}<sp> VALUE \n
@@ -365,11 +476,15 @@ __device__ __forceinline__ uint64_t bcast64(uint64_t x, int k) {
 // the wave stores the range with 16-byte stores (1 KiB per instruction).
 // Lines are taken in the longest prefix that fits the buffer; a single line
 // longer than the buffer is written with per-line 64-byte-wide byte stores.
-constexpr uint32_t kLineBuf = 12288;  // bytes per wave
+#ifndef KACC_LINE_BUF
+#define KACC_LINE_BUF 12288
+#endif
+constexpr uint32_t kLineBuf = KACC_LINE_BUF;  // bytes per wave
 
 __device__ __forceinline__ void write_lines_bytewise(const LineArgs &a, const char *s_c, uint64_t base, uint32_t k_beg,
                                                      uint32_t k_end, uint64_t l0, uint64_t l1, uint64_t o0,
-                                                     uint64_t o1, uint32_t vl, uint32_t zpair) {
+                                                     uint64_t o1, uint32_t vl, uint32_t zpair, uint64_t v0,
+                                                     uint64_t v1, uint64_t v2) {
   const uint32_t lane = threadIdx.x & 63u;
   for (uint32_t k = k_beg; k < k_end; ++k) {
     const uint64_t L0 = bcast64(l0, k), LL = bcast64(l1, k) - L0;
@@ -380,7 +495,7 @@ __device__ __forceinline__ void write_lines_bytewise(const LineArgs &a, const ch
       if (lane == 0) atomicOr(a.err, 1u << 8);
       continue;
     }
-    const char *val = a.vals + (base + k) * KACC_FMT_WIDTH;
+    const uint64_t V0 = bcast64(v0, k), V1 = bcast64(v1, k), V2 = bcast64(v2, k);
     const uint64_t cL = a.name_len + 1, cD = cL + LL, cE = cD + 7, cF = cE + zl, cG = cF + 3, cH = cG + VL;
     for (uint64_t p = lane; p < N; p += 64) {
       char c;
@@ -390,7 +505,10 @@ __device__ __forceinline__ void write_lines_bytewise(const LineArgs &a, const ch
       else if (p < cE) c = ",zone=\""[p - cD];
       else if (p < cF) c = s_c[z0 + (p - cE)];
       else if (p < cG) c = "\"} "[p - cF];
-      else if (p < cH) c = val[p - cG];
+      else if (p < cH) {
+        const uint32_t q = static_cast<uint32_t>(p - cG);
+        c = static_cast<char>((q < 8 ? V0 : q < 16 ? V1 : V2) >> (8 * (q & 7)));
+      }
       else c = '\n';
       a.out[O0 + p] = c;
     }
@@ -460,10 +578,11 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
     const uint64_t r = line_row(a, ri);
     const uint64_t l0 = a.label_off[r], l1 = a.label_off[r + 1];
     const uint64_t o0 = a.line_off[i], o1 = a.line_off[i + 1];
-    const uint32_t vl = a.vlen[i];
     const uint32_t zpair = (a.zone_pos[j] << 16) | a.zone_len[j];  // z0 | zl
-    const uint64_t *vw = reinterpret_cast<const uint64_t *>(a.vals + i * KACC_FMT_WIDTH);
-    const uint64_t v0 = vw[0], v1 = vw[1], v2 = vw[2];
+    Text val;
+    line_value(a, (a.first + r) * a.Z + a.zone_table[j], val);
+    const uint32_t vl = val.n;
+    const uint64_t v0 = val.w[0], v1 = val.w[1], v2 = val.w[2];
     const uint32_t nl = static_cast<uint32_t>(min<uint64_t>(lines - base, 64));
     for (uint32_t k0 = 0; k0 < nl;) {
       const uint64_t t0 = bcast64(o0, k0);
@@ -474,7 +593,7 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
       const uint64_t miss = ~__ballot(fit) >> k0;
       const uint32_t k1 = k0 + (miss ? static_cast<uint32_t>(__builtin_ctzll(miss)) : 64u - k0);
       if (k1 == k0) {  // one line longer than the buffer (or an inconsistent offset)
-        write_lines_bytewise(a, s_c, base, k0, k0 + 1, l0, l1, o0, o1, vl, zpair);
+        write_lines_bytewise(a, s_c, base, k0, k0 + 1, l0, l1, o0, o1, vl, zpair, v0, v1, v2);
         ++k0;
         continue;
       }
@@ -701,19 +820,16 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   a.out = out;
   a.out_cap = out_cap;
   a.err = ctx->d_err;
-  // temporaries, stream ordered: consts, value fields, lengths, tile sums
+  // temporaries, stream ordered: consts, lengths, tile sums
   const uint64_t tiles = (lines + 1 + kacc::fmt::kTile - 1) / kacc::fmt::kTile;
   if (tiles > 0x7fffffffull) return kacc_fail(ctx, KACC_EINVAL, "format_lines: too many lines");
   const size_t scan_bytes = 8 * tiles;
   char *tmp = nullptr;
   // every sub-buffer 256-B aligned (the scan's look-back state needs aligned storage)
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
-  const uint64_t off_vals = 1024, off_vlen = al(off_vals + lines * KACC_FMT_WIDTH),
-                 off_len = al(off_vlen + lines), off_scan = al(off_len + 8 * (lines + 1));
+  const uint64_t off_len = 1024, off_scan = al(off_len + 8 * (lines + 1));
   KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), off_scan + scan_bytes, st));
   a.consts = tmp;
-  a.vals = tmp + off_vals;
-  a.vlen = reinterpret_cast<uint8_t *>(tmp + off_vlen);
   a.len = reinterpret_cast<uint64_t *>(tmp + off_len);
   int rc = KACC_OK;
   auto done = [&](int code) {

@@ -43,6 +43,10 @@ def edge_energies():
     v = [0, 1, 2, 5, 999_999, 10**6, 10**6 + 1, 1_500_000, 10**12, 10**15, 123_456_789_012, 2**53, 2**53 + 1,
          2**63, 2**64 - 1, 2**64 - 1024, 10**19, 7 * 10**18 + 3]
     v += [10**k for k in range(20)] + [10**k - 1 for k in range(1, 20)]
+    # the integer fast path's boundary (write_joules: e < 10^15 µJ) and trailing zeros
+    v += [10**15 - 1, 10**15 + 1, 10**15 - 10, 999_999_999_999_990, 2**49, 2**50 - 1, 120_000, 3_000_000,
+          4_500_000_000, 10**14 + 1, 987_654_321_000_000]
+    v += [d * 10**k for d in (1, 7, 25, 123) for k in range(14)]
     return np.array(v, dtype=np.uint64)
 
 

@@ -61,6 +61,7 @@ def main():
         return float(np.median(ms[1:]))
 
     ms_lines = timed(lambda: acc.format_lines(*args, out_ptr=out.data_ptr(), out_cap=total, stream=s))
+    ms_size = timed(lambda: acc.format_lines(*args, stream=s))  # the sizing call alone (lengths, scan, total)
     fv = torch.empty(n * accel.KACC_FMT_WIDTH, dtype=torch.uint8, device="cuda")
     fl = torch.empty(n, dtype=torch.uint8, device="cuda")
     ms_vals = timed(lambda: acc.format_values("proc_energy", 0, n, fv.data_ptr(), fl.data_ptr(), s))
@@ -70,6 +71,8 @@ def main():
         "rows": rows, "zones": Z, "lines": n, "text_bytes": total,
         "format_lines_ms": ms_lines, "lines_per_s": n / (ms_lines * 1e-3),
         "text_GBps": total / (ms_lines * 1e-3) / 1e9,
+        "sizing_call_ms": ms_size, "write_pass_ms": ms_lines - ms_size,
+        "write_pass_text_GBps": total / ((ms_lines - ms_size) * 1e-3) / 1e9,
         "format_values_ms": ms_vals, "values_per_s": n / (ms_vals * 1e-3),
         "sample": head,
         "note": "format_lines = sizing pass (values + lengths + scan + total read back) and the write pass",
