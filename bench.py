@@ -168,61 +168,130 @@ def exchange_unique_id(rank, world, make_id):
     return uid
 
 
-def slot_layout_lines(args, frag, K, steps, bytes_per_interval):
+def slot_layout_lines(args, frag, K, steps, bytes_per_interval, steady_intervals=40, rounds=3):
     """Same-box kernel time per interval (HIP events on the launch stream around back-to-back
-    launches, median of `steps`)
-    of this config under three slot layouts: pristine slots without node_proc_span (row
-    order), pristine with it, and slots fragmented as the slot join leaves them under churn
-    (each node's rows on a random subset of (1+frag) x rows slots, in random row order,
-    node_proc_span given).  Same rows, same algorithmic bytes."""
+    launches, median over `rounds` interleaved rounds of `steps`) of this config under four
+    process-slot layouts, all on ONE engine context (contexts of one box differ by up to 12 %:
+    table placement, profiles/r02/placement/): pristine slots (slot = row) without and with
+    node_proc_span; the layout the slot join itself produces in production — kacc_slot_join
+    with KACC_JOIN_REUSE_TERMINATED over `steady_intervals` intervals of /proc-shaped churn
+    (fleet.ProcChurn, 2 % per interval), its spans given; and a synthetic one (each node's rows
+    on a random subset of (1+frag) x rows slots in random row order).  Same rows, same
+    algorithmic bytes."""
     import torch
 
     from kepler_amd import accel, fleet
     from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
 
-    def one(fr, span):
-        _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes),
-                                          fragment_slots=fr)
-        sizes = layout.sizes()
-        sim = fleet.FleetSim(layout, seed=fleet.SEED)
-        acc = accel.Accel(layout.zones, **layout.capacities())
-        stream = current_stream_handle()
-        statics = to_device(layout.static_arrays())
-        if span:
-            statics.update(to_device({"node_proc_span": layout.proc_span()}))
-        flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
-        prime = to_device(sim.next_interval())
-        acc.run_interval(interval_from_tensors(prime, sizes), stream)
-        del prime
-        full = [to_device(sim.next_interval()) for _ in range(2)]
+    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes))
+    sizes = layout.sizes()
+    N, P = layout.n_nodes, sizes["n_procs"]
+    off = layout.proc_off.astype(np.int64)
+    rows = np.diff(off)
+    node_of_row = np.repeat(np.arange(N), rows)
+    local = np.arange(P) - off[node_of_row]
+    slot_off = np.r_[0, np.cumsum(np.ceil(rows * (1 + max(frag, 0.05))).astype(np.int64) + 8)].astype(np.uint32)
+    caps = layout.capacities()
+    caps["proc_slots"] = int(slot_off[-1])
+    acc = accel.Accel(layout.zones, **caps)
+    stream = current_stream_handle()
+
+    # the production layout: the slot join's own output after steady_intervals of churn
+    sm = accel.SlotMap(acc, accel.KACC_KIND_PROC, slot_off)
+    sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
+    churn = fleet.ProcChurn(layout, churn=0.02)
+    d_off = torch.from_numpy(layout.proc_off.view(np.int32)).cuda()
+    d_out = torch.zeros(P, dtype=torch.int32, device="cuda")
+    tk = torch.zeros(int(slot_off[-1]), dtype=torch.int64, device="cuda")
+    ts = torch.zeros(int(slot_off[-1]), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda")
+    d_span = torch.zeros(2 * N, dtype=torch.int32, device="cuda")
+    for _ in range(steady_intervals + 1):
+        d_keys = torch.from_numpy(churn.next_keys().view(np.int32)).cuda()
+        sm.join(P, d_off.data_ptr(), d_keys.data_ptr(), 0, d_out.data_ptr(), tk.data_ptr(), ts.data_ptr(),
+                cnt.data_ptr(), stream, d_span.data_ptr())
+    acc.sync(stream)
+    steady = d_out.cpu().numpy().view(np.uint32).copy()
+    steady_span = d_span.cpu().numpy().view(np.uint32).copy()
+    sm.close()
+    del d_keys, d_out, tk, ts, cnt, d_span
+
+    pristine = (slot_off[node_of_row].astype(np.int64) + local).astype(np.uint32)
+    pristine_span = np.stack([slot_off[:-1], slot_off[:-1] + rows.astype(np.uint32) - 1], 1).reshape(-1)
+    flay = fleet.config_layout(args.config, nodes=N, fragment_slots=frag)
+    assert np.array_equal(flay.proc_off, layout.proc_off)
+    fcap = (rows * (1.0 + frag)).astype(np.int64) + 1
+    fslot = (slot_off[node_of_row].astype(np.int64) + flay.proc_slot.astype(np.int64)
+             - np.repeat(np.r_[0, np.cumsum(fcap)[:-1]], rows)).astype(np.uint32)
+    fspan = np.zeros(2 * N, dtype=np.uint32)
+    if P:
+        nz = rows > 0
+        fspan[0::2][nz] = np.minimum.reduceat(fslot.astype(np.int64), off[:-1][nz])
+        fspan[1::2][nz] = np.maximum.reduceat(fslot.astype(np.int64), off[:-1][nz])
+        fspan[0::2][~nz] = 1
+
+    sim = fleet.FleetSim(layout, seed=fleet.SEED)
+    statics = to_device(layout.static_arrays())
+    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+    prime = sim.next_interval()
+    prime["proc_slot"] = pristine
+    tp = dict(statics)
+    tp.update(to_device(prime))
+    acc.run_interval(interval_from_tensors(tp, sizes), stream)
+    full = [sim.next_interval() for _ in range(2)]
+    keys_iv = ("proc_cpu_delta", "ctr_slot", "vm_slot", "pod_slot", "node_ts_ns", "node_usage_ratio",
+               "node_status", "zone_energy", "zone_max")
+    dev_full = [to_device({n: f[n] for n in keys_iv}) for f in full]
+
+    def layout_ivs(proc_slot, span):
+        base = dict(statics)
+        base.update(to_device({"proc_slot": proc_slot}))
+        if span is not None:
+            base.update(to_device({"node_proc_span": span}))
         ivs = []
         for k in range((steps + 1) * K):
-            t = dict(statics)
-            t.update(full[k % 2])
+            t = dict(base)
+            t.update(dev_full[k % 2])
             t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
                                 if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
-            ivs.append(interval_from_tensors(t, sizes, flags))
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps + 1)]
-        for i in range(steps + 1):  # back to back, as the headline's steps (sustained clocks)
-            ev[i][0].record()
-            if K == 1:
-                acc.run_interval(ivs[i], stream)
-            else:
-                acc.run_intervals(ivs[i * K:(i + 1) * K], stream)
-            ev[i][1].record()
-        torch.cuda.synchronize()
-        ms = [a.elapsed_time(b) / K for a, b in ev[1:]]
-        acc.sync(stream)
-        acc.close()
+            ivs.append((interval_from_tensors(t, sizes, flags), t))
+        return ivs
+
+    cases = {"pristine_no_span": layout_ivs(pristine, None), "pristine_span": layout_ivs(pristine, pristine_span),
+             "join_steady_state_span": layout_ivs(steady, steady_span),
+             f"fragmented_{frag:g}_span": layout_ivs(fslot, fspan)}
+    times = {n: [] for n in cases}
+    for _ in range(rounds):
+        for name, ivs in cases.items():
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps + 1)]
+            for i in range(steps + 1):  # back to back, as the headline's steps (sustained clocks)
+                ev[i][0].record()
+                if K == 1:
+                    acc.run_interval(ivs[i][0], stream)
+                else:
+                    acc.run_intervals([x[0] for x in ivs[i * K:(i + 1) * K]], stream)
+                ev[i][1].record()
+            torch.cuda.synchronize()
+            times[name] += [a.elapsed_time(b) / K for a, b in ev[1:]]
+    acc.sync(stream)
+    acc.close()
+    out = {}
+    for name, ms in times.items():
         k_ms = float(np.median(ms))
         achieved = bytes_per_interval / (k_ms * 1e-3) / 1e9
-        return {"kernel_ms": k_ms, "achieved_GBps": achieved, "frac": achieved / HBM_PEAK_GBPS}
-
-    out = {"pristine_no_span": one(0.0, False), "pristine_span": one(0.0, True),
-           f"fragmented_{frag:g}_span": one(frag, True)}
-    out["fragmented_over_pristine"] = out[f"fragmented_{frag:g}_span"]["kernel_ms"] / out["pristine_span"]["kernel_ms"]
-    out["note"] = ("same box, same method, same rows / algorithmic bytes; fragmented = each node's rows on a "
-                   "random subset of (1+F) x rows slots in random row order (the slot join's steady state)")
+        out[name] = {"kernel_ms": k_ms, "achieved_GBps": achieved, "frac": achieved / HBM_PEAK_GBPS}
+    ps = out["pristine_no_span"]["kernel_ms"]
+    out["join_steady_state_over_pristine"] = out["join_steady_state_span"]["kernel_ms"] / ps
+    out["fragmented_over_pristine"] = out[f"fragmented_{frag:g}_span"]["kernel_ms"] / ps
+    out["join_steady_state"] = {
+        "policy": "KACC_JOIN_REUSE_TERMINATED", "intervals": steady_intervals, "churn": 0.02,
+        "span_over_rows": float(np.mean((steady_span[1::2].astype(np.int64) - steady_span[0::2] + 1)[rows > 0]
+                                        / rows[rows > 0])),
+    }
+    out["note"] = ("one context, interleaved rounds, same rows / algorithmic bytes; join_steady_state = the slot "
+                   "words and spans kacc_slot_join returns after /proc-shaped churn (newcomers listed last in "
+                   "their container, fleet.ProcChurn); fragmented = synthetic random subset of (1+F) x rows slots "
+                   "in random row order")
     return out
 
 

@@ -421,6 +421,16 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
 void kacc_slotmap_destroy(kacc_slotmap *m); /* safe before or after kacc_destroy(ctx); other
                                                calls need the context alive */
 int kacc_slotmap_reset(kacc_slotmap *m); /* forget every ID (PowerMonitor restart) */
+/* Slot numbering policy of later kacc_slot_join calls (default 0: the rules
+ * below).  KACC_JOIN_REUSE_TERMINATED: the new rows of a node take, in row
+ * order, first the slots of the IDs this same call finds terminated (ascending
+ * by slot), then the lowest free slots — so a node whose processes exit and
+ * start at the same rate keeps exactly its live rows' slots and, when /proc
+ * lists a newcomer where an exited process was, its slot order.  The caller
+ * must read the terminated slots' final values (kacc_tracker_add, or its own
+ * copy) BEFORE the next interval kernel writes those slots.                  */
+#define KACC_JOIN_REUSE_TERMINATED 1u
+int kacc_slotmap_set_policy(kacc_slotmap *m, uint32_t policy);
 /* Device pointers, asynchronous on `stream` (NULL = the context's stream).
  * n_rows = row_off[n_nodes] (the batch's n_procs / n_ctrs / n_vms / n_pods);
  * row_off [n_nodes+1]: the batch's proc_off / ctr_off / vm_off / pod_off;

@@ -36,6 +36,7 @@ KACC_NODE_SKIPPED = 2
 KACC_F_NODE_CPU_DELTA_GIVEN = 0x1
 KACC_FMT_WIDTH = 24
 KACC_KIND_PROC, KACC_KIND_CTR, KACC_KIND_VM, KACC_KIND_POD = 0, 1, 2, 3
+KACC_JOIN_REUSE_TERMINATED = 1  # kacc_slotmap_set_policy
 KACC_KEY_EMPTY = 0xFFFFFFFFFFFFFFFF
 KACC_F_FAST_NODES = 0x2
 KACC_F_TRUSTED_LAYOUT = 0x4
@@ -99,6 +100,7 @@ EXPORTS = [
     "kacc_slotmap_create",
     "kacc_slotmap_destroy",
     "kacc_slotmap_reset",
+    "kacc_slotmap_set_policy",
     "kacc_slot_join",
     "kacc_abi_version",
     "kacc_create",
@@ -309,6 +311,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_slotmap_destroy.argtypes = [c_void_p]
     lib.kacc_slotmap_destroy.restype = None
     lib.kacc_slotmap_reset.argtypes = [c_void_p]
+    lib.kacc_slotmap_set_policy.argtypes = [c_void_p, c_uint32]
     lib.kacc_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     if lib.kacc_abi_version() != KACC_ABI_VERSION:
@@ -581,6 +584,10 @@ class SlotMap:
 
     def reset(self) -> None:
         self.accel._check(self.lib.kacc_slotmap_reset(self.handle))
+
+    def set_policy(self, policy: int) -> None:
+        """KACC_JOIN_REUSE_TERMINATED: new rows take this call's terminated slots first."""
+        self.accel._check(self.lib.kacc_slotmap_set_policy(self.handle, policy))
 
     def join(self, n_rows: int, row_off_ptr: int, keys_ptr: int, node_status_ptr: int, out_slot_ptr: int,
              term_key_ptr: int, term_slot_ptr: int, term_count_ptr: int, stream: int = 0,

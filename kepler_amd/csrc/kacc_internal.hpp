@@ -61,6 +61,7 @@ struct kacc_slotmap {
   uint32_t *d_slot_off = nullptr;
   uint64_t *d_hoff = nullptr;
   bool has_big = false;         // some node's table exceeds the LDS size
+  uint32_t policy = 0;          // KACC_JOIN_* bits (kacc_slotmap_set_policy)
   uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
   uint32_t *d_slots = nullptr;  // 64-bit IDs only
 };

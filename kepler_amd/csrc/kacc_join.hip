@@ -57,6 +57,7 @@ constexpr uint32_t kErrRange = 1u << 7;    // more live IDs than the node's slot
 struct Args {
   uint32_t n_nodes, n_rows;
   uint32_t stop_after;  // timing ablation (kacc_debug_join_variant): 0 = full join
+  uint32_t reuse;       // KACC_JOIN_REUSE_TERMINATED
   const uint32_t *row_off;
   const void *keys;
   const uint32_t *node_status;
@@ -531,6 +532,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   }
   if (tid < W) s_wpre[tid] = pex;
   const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot;
+  // KACC_JOIN_REUSE_TERMINATED: new rows take this call's terminated slots first
+  // (slot order), then the free ones; otherwise terminated slots are held
+  const uint32_t t_first = a.reuse ? n_term : 0u, n_avail = total_free + t_first;
   if (tid == 0) a.term_count[n] = n_term;
   jbar<V>();
   if (a.stop_after == 3u) return;  // timing ablation
@@ -544,16 +548,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       const uint32_t w = sl >> 5, bit = 1u << (sl & 31);
       const uint32_t tm = s_tmask[w];
       if (!(tm & bit)) continue;
-      const uint32_t pos = s0 + (s_wpre[w] & 0xffffu) + __popc(tm & (bit - 1u));
+      const uint32_t rank = (s_wpre[w] & 0xffffu) + __popc(tm & (bit - 1u)), pos = s0 + rank;
       a.term_key[pos] = static_cast<uint64_t>(L.key(b));
       a.term_slot[pos] = s0 + sl;
+      if (a.reuse && rank < kNewCap) s_free[rank] = static_cast<uint16_t>(sl);
       L.tomb(b);
       atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
     }
   }
-  const uint32_t want = min(min(n_new, total_free), kNewCap);
+  const uint32_t want = min(min(n_new, n_avail), kNewCap);
   if (tid < W) {
-    uint32_t p = s_wpre[tid] >> 16;
+    uint32_t p = t_first + (s_wpre[tid] >> 16);
     for (uint32_t fm = s_fmask[tid]; fm && p < want; fm &= fm - 1, ++p)
       s_free[p] = static_cast<uint16_t>(tid * 32 + __builtin_ctz(fm));
   }
@@ -561,13 +566,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   if (a.stop_after == 4u) return;  // timing ablation
 
   // ---- 5: new rows take slots in row order ------------------------------------------
-  auto take_slow = [&](uint32_t q) -> uint32_t {  // q-th free slot, q >= kNewCap
+  auto take_slow = [&](uint32_t q) -> uint32_t {  // q-th available slot, q >= kNewCap
+    const bool term = q < t_first;
+    const uint32_t sh = term ? 0u : 16u, msk = term ? 0xffffu : 0xffffffffu;
+    if (!term) q -= t_first;
     uint32_t lo = 0, hi = W;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) / 2;
-      if ((s_wpre[mid] >> 16) <= q) lo = mid; else hi = mid;
+      if (((s_wpre[mid] >> sh) & msk) <= q) lo = mid; else hi = mid;
     }
-    return lo * 32 + select_bit(s_fmask[lo], q - (s_wpre[lo] >> 16));
+    return lo * 32 + select_bit(term ? s_tmask[lo] : s_fmask[lo], q - ((s_wpre[lo] >> sh) & msk));
   };
   const bool compact = n_new <= kNewCap;
   uint32_t q = rank0;
@@ -576,7 +584,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   for (int j = 0; j < kRpl; ++j) {
     rk[j] = ~0u;
     if (res[j] != kPending) continue;
-    if (q >= total_free) {
+    if (q >= n_avail) {
       raise(kErrRange);
       res[j] = kInvalid;
       ++q;
@@ -598,7 +606,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // kJInsDup: by the insert that meets its own key on the probe path (buckets only
   // fill during this step, so of two rows with one ID the later claimant always
   // passes the earlier's bucket); otherwise by a re-probe after every insert.
-  const uint32_t n_ins = min(n_new, total_free);
+  const uint32_t n_ins = min(n_new, n_avail);
   uint32_t fresh = 0;  // inserts into empty buckets (occupancy)
   auto insert_dup = [&](K k, uint32_t rel) -> uint32_t {  // bucket, ~0u full, ~1u duplicate
     uint32_t b = bucket(k, v.shift);
@@ -829,6 +837,7 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
     carry += tot;
   }
   if (tid == 0) a.term_count[n] = carry;
+  const uint32_t t_first = a.reuse ? carry : 0u;  // KACC_JOIN_REUSE_TERMINATED: terminated slots first
   __syncthreads();
   if (carry) {
     for (uint32_t b = tid; b < H; b += kThreads) {
@@ -862,11 +871,20 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
   }
   const uint32_t total_free = carry;
   __syncthreads();
-  auto take = [&](uint32_t q) -> uint32_t {  // q-th free slot, as a slot word
-    if (q >= total_free) {
+  auto take = [&](uint32_t q) -> uint32_t {  // q-th available slot, as a slot word
+    if (q >= total_free + t_first) {
       atomicOr(a.err, kErrRange);
       return kInvalid;
     }
+    if (q < t_first) {  // the q-th terminated slot (last word with s_tpre[w] <= q)
+      uint32_t lo = 0, hi = W;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (s_tpre[mid] <= q) lo = mid; else hi = mid;
+      }
+      return (s0 + lo * 32 + select_bit(s_used[lo] & ~s_seen[lo], q - s_tpre[lo])) | KACC_SLOT_NEW;
+    }
+    q -= t_first;
     uint32_t lo = 0, hi = W;  // last word with s_wpre[w] <= q
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) / 2;
@@ -1064,6 +1082,14 @@ int kacc_debug_join_variant(kacc_slotmap *m, uint32_t n_rows, const uint32_t *ro
                    nullptr, stream, stop_after);
 }
 
+int kacc_slotmap_set_policy(kacc_slotmap *m, uint32_t policy) {
+  if (!m) return KACC_EINVAL;
+  if (policy & ~KACC_JOIN_REUSE_TERMINATED)
+    return kacc_fail(m->ctx, KACC_EINVAL, "slot map policy: unknown bits 0x%x", policy & ~KACC_JOIN_REUSE_TERMINATED);
+  m->policy = policy;
+  return KACC_OK;
+}
+
 int kacc_debug_set_join_variant(int variant) {
   const int prev = g_join_variant;
   g_join_variant = variant;
@@ -1088,6 +1114,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   a.n_nodes = m->n_nodes;
   a.n_rows = n_rows;
   a.stop_after = stop_after;
+  a.reuse = (m->policy & KACC_JOIN_REUSE_TERMINATED) ? 1u : 0u;
   a.row_off = row_off;
   a.keys = keys;
   a.node_status = node_status;

@@ -563,3 +563,45 @@ class KeyedChurn:
             else:
                 self.keys[born] = self._new_ids(born.size)
         return self.keys.copy()
+
+
+class ProcChurn:
+    """PIDs of a fleet's process rows under /proc-shaped churn, for the slot join.
+
+    Rows are grouped by container (then VM, then the node's pod-less rest) in
+    /proc listing order (informer.go:167-205), i.e. ascending PID inside a
+    group.  Each interval a ``churn`` fraction of the processes exits and as
+    many new ones start in the same group, each with a PID above every PID
+    its node has used, so /proc lists it last in its group: the group sizes,
+    hence the layout's CSR, stay fixed while rows shift inside the groups.
+    """
+
+    def __init__(self, layout: "FleetLayout", churn: float = 0.02, seed: int = SEED):
+        self.rng = np.random.default_rng(seed ^ 0x50524F43)
+        self.churn = churn
+        off = layout.proc_off.astype(np.int64)
+        self.n_rows = int(off[-1])
+        self.node_of_row = np.repeat(np.arange(layout.n_nodes), np.diff(off))
+        ends = np.unique(np.concatenate([layout.ctr_proc_end.astype(np.int64),
+                                         layout.vm_proc_end.astype(np.int64), off[1:]]))
+        # a row's group = the first segment end after it
+        self.group = np.searchsorted(ends, np.arange(self.n_rows), side="right").astype(np.int64)
+        local = np.arange(self.n_rows) - off[self.node_of_row]
+        self.keys = (300 + 3 * local + self.rng.integers(0, 3, size=self.n_rows)).astype(np.uint32)
+        self.next_pid = np.full(layout.n_nodes, 1 << 22, dtype=np.int64)
+        self.started = False
+
+    def next_keys(self) -> np.ndarray:
+        """The keys of the next interval (the first call: the initial processes)."""
+        if self.started:
+            die = self.rng.random(self.n_rows) < self.churn
+            k = np.flatnonzero(die)
+            nd = self.node_of_row[k]  # ascending, as k is
+            rank = np.arange(k.size) - np.searchsorted(nd, nd)
+            keys = self.keys.copy()
+            keys[k] = (self.next_pid[nd] + rank).astype(np.uint32)
+            np.add.at(self.next_pid, nd, 1)
+            # survivors keep their order, newcomers go last in their group
+            self.keys = keys[np.argsort(self.group * 2 + die, kind="stable")]
+        self.started = True
+        return self.keys.copy()

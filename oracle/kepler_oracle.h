@@ -96,6 +96,7 @@ int kor_gf_interval(kor_gofaithful *g, kor_state *st, const kacc_interval *b);
 typedef struct kor_slotmap kor_slotmap;
 kor_slotmap *kor_slotmap_create(uint32_t n_nodes, const uint32_t *slot_off);
 void kor_slotmap_destroy(kor_slotmap *m);
+void kor_slotmap_set_policy(kor_slotmap *m, uint32_t policy);
 int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                   uint32_t *term_slot, uint32_t *term_count);

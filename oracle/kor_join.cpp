@@ -9,7 +9,8 @@
 // :236-246 containers, :260-270 VMs, :311-322 pods).  The slot numbering rule
 // is the engine's own (the reference has no slots): a new ID takes the lowest
 // slot of its node's range not held by any ID of the previous set, new rows
-// taking slots in row order.
+// taking slots in row order; with KACC_JOIN_REUSE_TERMINATED the slots of the
+// IDs terminated in the same call come first (ascending by slot).
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -21,6 +22,7 @@
 struct kor_slotmap {
   std::vector<uint32_t> slot_off;
   std::vector<std::unordered_map<uint64_t, uint32_t>> live;  // per node: ID -> slot
+  uint32_t policy = 0;  // KACC_JOIN_REUSE_TERMINATED
 };
 
 extern "C" {
@@ -33,6 +35,8 @@ kor_slotmap *kor_slotmap_create(uint32_t n_nodes, const uint32_t *slot_off) {
 }
 
 void kor_slotmap_destroy(kor_slotmap *m) { delete m; }
+
+void kor_slotmap_set_policy(kor_slotmap *m, uint32_t policy) { m->policy = policy; }
 
 int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const uint64_t *keys,
                   const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
@@ -51,6 +55,18 @@ int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, cons
     std::unordered_map<uint64_t, uint32_t> cur;
     cur.reserve(r1 - r0);
     uint32_t next_free = 0;
+    // KACC_JOIN_REUSE_TERMINATED: the previous IDs absent from this batch, their
+    // slots ascending, go to the new rows first (in row order)
+    std::vector<uint32_t> reuse;
+    size_t next_reuse = 0;
+    if (m->policy & KACC_JOIN_REUSE_TERMINATED) {
+      std::unordered_map<uint64_t, uint8_t> now;
+      now.reserve(r1 - r0);
+      for (uint32_t r = r0; r < r1; ++r) now.emplace(keys[r], 1);
+      for (const auto &kv : prev)
+        if (!now.count(kv.first)) reuse.push_back(kv.second);
+      std::sort(reuse.begin(), reuse.end());
+    }
     for (uint32_t r = r0; r < r1; ++r) {
       const uint64_t k = keys[r];
       if (k == KACC_KEY_EMPTY || k == KACC_KEY_TOMB || cur.count(k)) {
@@ -62,6 +78,12 @@ int kor_slot_join(kor_slotmap *m, uint32_t n_rows, const uint32_t *row_off, cons
       if (it != prev.end()) {  // running total continues (process.go:134-137)
         out_slot[r] = s0 + it->second;
         cur.emplace(k, it->second);
+        continue;
+      }
+      if (next_reuse < reuse.size()) {  // a slot terminated in this call
+        const uint32_t sl = reuse[next_reuse++];
+        out_slot[r] = (s0 + sl) | KACC_SLOT_NEW;
+        cur.emplace(k, sl);
         continue;
       }
       while (next_free < S && used[next_free]) ++next_free;

@@ -59,6 +59,8 @@ def load():
     lib.kor_aggregated_energy.restype = c_uint64
     lib.kor_slotmap_create.argtypes = [c_uint32, c_void_p]
     lib.kor_slotmap_create.restype = c_void_p
+    lib.kor_slotmap_set_policy.argtypes = [c_void_p, c_uint32]
+    lib.kor_slotmap_set_policy.restype = None
     lib.kor_slotmap_destroy.argtypes = [c_void_p]
     lib.kor_slotmap_destroy.restype = None
     lib.kor_slot_join.argtypes = [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -229,10 +231,12 @@ class OracleZoneAgg:
 class OracleSlotMap:
     """CPU restatement of kacc_slot_join (oracle/kor_join.cpp)."""
 
-    def __init__(self, slot_off: np.ndarray):
+    def __init__(self, slot_off: np.ndarray, policy: int = 0):
         self.lib = load()
         self.off = np.ascontiguousarray(slot_off, dtype=np.uint32)
         self.h = self.lib.kor_slotmap_create(self.off.size - 1, self.off.ctypes.data)
+        if policy:  # KACC_JOIN_REUSE_TERMINATED
+            self.lib.kor_slotmap_set_policy(self.h, policy)
 
     def join(self, row_off, keys, node_status=None):
         """Returns (rc, out_slot, term_key, term_slot, term_count) on host arrays;

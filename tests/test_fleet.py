@@ -124,3 +124,36 @@ def test_namespace_order_close_to_list_order(oracle_lib):
         assert np.array_equal(e.reshape(-1, L.zones)[k], pe[sl].sum(axis=0, dtype=np.uint64))
         ref = np.array([sum(pp[s, z] for s in sl) for z in range(L.zones)])
         np.testing.assert_allclose(p.reshape(-1, L.zones)[k], ref, rtol=1e-12)
+
+
+def test_proc_churn_model_keeps_groups_and_listing_order():
+    """ProcChurn: PIDs unique per node, ascending inside every container / VM / rest group
+    (/proc listing order), the CSR fixed; with KACC_JOIN_REUSE_TERMINATED the oracle join
+    keeps every node on exactly its first `rows` slots."""
+    from oracle.oracle import OracleSlotMap
+
+    layout = fleet.make_layout(6, [300, 1000, 40, 0, 2000, 7], 2, seed=4)
+    off = layout.proc_off.astype(np.int64)
+    ch = fleet.ProcChurn(layout, churn=0.05, seed=3)
+    rows = np.diff(off)
+    slot_off = np.r_[0, np.cumsum(rows + 4)].astype(np.uint32)
+    join = OracleSlotMap(slot_off, policy=1)
+    ends = np.unique(np.concatenate([layout.ctr_proc_end, layout.vm_proc_end, off[1:]]).astype(np.int64))
+    starts = np.r_[0, ends[:-1]]
+    changed = 0
+    prev = None
+    for _ in range(12):
+        keys = ch.next_keys()
+        for n in range(layout.n_nodes):
+            assert len(np.unique(keys[off[n]:off[n + 1]])) == rows[n]
+        for a, b in zip(starts, ends):
+            assert np.all(np.diff(keys[a:b].astype(np.int64)) > 0)
+        if prev is not None:
+            changed += int(np.sum(~np.isin(keys, prev)))
+        prev = keys
+        rc, out, _, _, _ = join.join(layout.proc_off, keys)
+        assert rc == 0
+        for n in range(layout.n_nodes):
+            s = np.sort((out[off[n]:off[n + 1]] & 0x7FFFFFFF) - slot_off[n])
+            np.testing.assert_array_equal(s, np.arange(rows[n]))
+    assert 0.03 < changed / (11 * off[-1]) < 0.07

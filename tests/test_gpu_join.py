@@ -27,10 +27,12 @@ def gpu_ready():
 
 
 class GpuJoin:
-    def __init__(self, acc, kind, slot_off):
+    def __init__(self, acc, kind, slot_off, policy=0):
         self.acc = acc
         self.kind = kind
         self.m = accel.SlotMap(acc, kind, slot_off)
+        if policy:
+            self.m.set_policy(policy)
         self.slot_off = slot_off
         cap = max(int(slot_off[-1]), 1)
         self.tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
@@ -88,13 +90,14 @@ JOIN_FLEETS = [
 ]
 
 
+@pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
 @pytest.mark.parametrize("name,sizes,churn,kind", JOIN_FLEETS, ids=[f[0] for f in JOIN_FLEETS])
-def test_join_bit_exact(name, sizes, churn, kind):
+def test_join_bit_exact(name, sizes, churn, kind, policy):
     row_off = np.r_[0, np.cumsum(sizes)].astype(np.uint32)
     slot_off = np.r_[0, np.cumsum([int(s * 1.2) + 4 for s in sizes])].astype(np.uint32)
     acc = accel.Accel(1, **caps_for(slot_off))
-    gpu = GpuJoin(acc, accel.KACC_KIND_PROC if kind == "proc" else accel.KACC_KIND_CTR, slot_off)
-    ora = OracleSlotMap(slot_off)
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC if kind == "proc" else accel.KACC_KIND_CTR, slot_off, policy)
+    ora = OracleSlotMap(slot_off, policy)
     sim = fleet.KeyedChurn(row_off, seed=7, churn=churn, kind=kind)
     rng = np.random.default_rng(2)
     for it in range(5):
@@ -133,7 +136,8 @@ def test_join_errors_raise_erange():
     assert term == []
 
 
-def test_join_feeds_interval_bit_exact():
+@pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
+def test_join_feeds_interval_bit_exact(policy):
     """Keyed fleet: device join -> interval kernel == oracle join -> oracle interval."""
     layout = fleet.make_layout(12, [1500, 2000, 40, 0, 700, 2048] * 2, 4, seed=21)
     sizes = layout.sizes()
@@ -142,8 +146,8 @@ def test_join_feeds_interval_bit_exact():
     caps = layout.capacities()
     caps["proc_slots"] = int(proc_slot_off[-1])
     acc = accel.Accel(layout.zones, **caps)
-    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, proc_slot_off)
-    ojoin = OracleSlotMap(proc_slot_off)
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, proc_slot_off, policy)
+    ojoin = OracleSlotMap(proc_slot_off, policy)
     ora = Oracle(layout.zones, **caps)
     sim = fleet.FleetSim(layout, seed=21, churn=0.0, read_error_frac=0.1)
     keys_sim = fleet.KeyedChurn(layout.proc_off, seed=21, churn=0.04)

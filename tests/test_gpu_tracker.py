@@ -70,13 +70,19 @@ FLEETS = [
 ]
 
 
-@pytest.mark.parametrize("concurrent", [False, True], ids=["one-stream", "tracker-beside-interval"])
+@pytest.mark.parametrize("concurrent", [False, True, "reuse"],
+                         ids=["one-stream", "tracker-beside-interval", "reuse-tracker-first"])
 @pytest.mark.parametrize("name,sizes,Z,churn,max_size", FLEETS, ids=[f[0] for f in FLEETS])
 def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurrent):
     """One tracker per node (every node's PowerMonitor owns one): each node keeps its own top
     max_size, against one Go heap per node.  concurrent: the tracker runs on a second stream
     beside the interval kernel (it reads only terminated slots, which the interval never
-    writes) and clears only the odd nodes (a per-node export); otherwise every node."""
+    writes) and clears only the odd nodes (a per-node export); otherwise every node.
+    "reuse": the join hands terminated slots to new rows at once (KACC_JOIN_REUSE_TERMINATED),
+    so the tracker adds the terminated batch right after the join, before the interval
+    kernel overwrites those slots."""
+    reuse = concurrent == "reuse"
+    concurrent = concurrent is True
     layout = fleet.make_layout(len(sizes), sizes, Z, seed=31)
     sizes_d = layout.sizes()
     rows = np.diff(layout.proc_off.astype(np.int64))
@@ -85,9 +91,11 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
     caps["proc_slots"] = int(slot_off[-1])
     acc = accel.Accel(Z, **caps)
     sm = accel.SlotMap(acc, accel.KACC_KIND_PROC, slot_off)
+    if reuse:
+        sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
     thr = 2 * 10**6  # 2 J
     tr = accel.Tracker(acc, accel.KACC_KIND_PROC, max_size, zone=0, min_energy=thr, capacity=200_000)
-    ojoin, ora = OracleSlotMap(slot_off), Oracle(Z, **caps)
+    ojoin, ora = OracleSlotMap(slot_off, int(reuse)), Oracle(Z, **caps)
     otr = OracleTracker(max_size, thr, Z, 0)
     sim = fleet.FleetSim(layout, seed=31, churn=0.0, read_error_frac=0.05)
     keys_sim = fleet.KeyedChurn(layout.proc_off, seed=31, churn=churn)
@@ -115,7 +123,8 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
             joined = torch.cuda.Event()
             joined.record(torch.cuda.current_stream())
             s2.wait_event(joined)
-        acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
+        if not reuse:
+            acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         if it == 3:  # an export happened: Clear() before this interval's adds (process.go:80-84)
             if concurrent:  # only the odd nodes exported
                 mask = (np.arange(layout.n_nodes) % 2).astype(np.int32)
@@ -128,7 +137,11 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
         tr.add(sm, tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), ts2)
         if concurrent:  # the next join rewrites the terminated lists the tracker reads
             torch.cuda.current_stream().wait_stream(s2)
+        if reuse:  # after the tracker read the terminated slots' final values
+            acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         acc.sync(s)
+        if reuse:  # the oracle tracker reads the same final values: the tables before this interval
+            pre_e, pre_p = ora.state["proc_energy"].copy(), ora.state["proc_power"].copy()
         ora.interval(a_ora, sizes_d)
         # oracle: the same terminated batch (per-node segments), values from the oracle tables
         nodes, kk, ss = [], [], []
@@ -137,7 +150,8 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
             nodes += [n] * c
             kk += otk[s0:s0 + c].tolist()
             ss += ots[s0:s0 + c].tolist()
-        otr.add_batch(nodes, kk, ss, ora.state["proc_energy"], ora.state["proc_power"])
+        otr.add_batch(nodes, kk, ss, pre_e if reuse else ora.state["proc_energy"],
+                      pre_p if reuse else ora.state["proc_power"])
         gk, gn, ge, gp = tr.items()
         order = np.lexsort((gk, gn))
         ok_, on_, oe_, op_ = otr.items()

@@ -21,9 +21,10 @@ KACC_ERANGE = -4
 class PySlotMap:
     """Go-map restatement: per node dict ID -> slot."""
 
-    def __init__(self, slot_off):
+    def __init__(self, slot_off, reuse=False):
         self.off = [int(x) for x in slot_off]
         self.live = [dict() for _ in range(len(self.off) - 1)]
+        self.reuse = reuse  # KACC_JOIN_REUSE_TERMINATED
 
     def join(self, row_off, keys, node_status=None):
         out = np.zeros(int(row_off[-1]), dtype=np.uint32)
@@ -34,6 +35,9 @@ class PySlotMap:
             s0, S = self.off[n], self.off[n + 1] - self.off[n]
             held = set(prev.values())
             free = [s for s in range(S) if s not in held]
+            if self.reuse:  # the slots of IDs absent from this batch first, ascending
+                now = set(int(k) for k in keys[int(row_off[n]):int(row_off[n + 1])])
+                free = sorted(s for k, s in prev.items() if k not in now) + free
             cur = {}
             for r in range(int(row_off[n]), int(row_off[n + 1])):
                 k = int(keys[r])
@@ -56,12 +60,12 @@ def ranges(sizes, slack=1.25):
     return row_off, slot_off
 
 
-@pytest.mark.parametrize("kind", ["proc", "ctr"])
-def test_oracle_join_matches_go_maps(kind):
+@pytest.mark.parametrize("kind,reuse", [("proc", False), ("ctr", False), ("proc", True), ("ctr", True)])
+def test_oracle_join_matches_go_maps(kind, reuse):
     sizes = [0, 1, 7, 64, 300, 1000]
     row_off, slot_off = ranges(sizes)
     sim = fleet.KeyedChurn(row_off, seed=3, churn=0.1, kind=kind)
-    ora, py = OracleSlotMap(slot_off), PySlotMap(slot_off)
+    ora, py = OracleSlotMap(slot_off, policy=int(reuse)), PySlotMap(slot_off, reuse)
     rng = np.random.default_rng(1)
     live_slot = {}
     for it in range(6):
@@ -85,9 +89,26 @@ def test_oracle_join_matches_go_maps(kind):
                 if (n, k) in live_slot and not (w & KACC_SLOT_NEW):
                     assert live_slot[(n, k)] == w & 0x7FFFFFFF
                 live_slot[(n, k)] = w & 0x7FFFFFFF
-        # terminated slots are not handed to new rows in the same interval
         new_slots = set((out[(out & KACC_SLOT_NEW) != 0] & 0x7FFFFFFF).tolist())
-        assert not new_slots & set(ts.tolist())
+        if reuse:  # KeyedChurn: as many new rows as terminated IDs -> the terminated slots exactly
+            assert set(ts.tolist()) <= new_slots or status is not None
+        else:  # terminated slots are not handed to new rows in the same interval
+            assert not new_slots & set(ts.tolist())
+
+
+def test_oracle_join_reuse_keeps_slot_order():
+    """/proc-shaped churn (a newcomer listed where an exited process was): with
+    KACC_JOIN_REUSE_TERMINATED every node keeps exactly slots 0..rows-1 in row order."""
+    row_off, slot_off = ranges([40, 300, 1000])
+    sim = fleet.KeyedChurn(row_off, seed=5, churn=0.05)
+    ora = OracleSlotMap(slot_off, policy=1)
+    for _ in range(8):
+        rc, out, _, _, cnt = ora.join(row_off, sim.next_keys())
+        assert rc == 0
+        for n in range(3):
+            s = (out[row_off[n]:row_off[n + 1]] & 0x7FFFFFFF) - slot_off[n]
+            np.testing.assert_array_equal(s, np.arange(row_off[n + 1] - row_off[n]))
+    assert cnt.sum() > 0
 
 
 def test_oracle_join_first_interval_consecutive():
