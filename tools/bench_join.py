@@ -119,6 +119,43 @@ def main():
         e3.synchronize()
         tpipe.append(e0.elapsed_time(e3))
     acc.sync(stream)
+    # production order with KACC_JOIN_REUSE_TERMINATED: join -> tracker (reads the
+    # terminated slots' final values) -> interval (rewrites them), one stream, keys
+    # of /proc-shaped churn (fleet.ProcChurn); the interval runs on the join's spans
+    sm2 = accel.SlotMap(acc, accel.KACC_KIND_PROC, slot_off)
+    sm2.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
+    pchurn = fleet.ProcChurn(layout, churn=0.02)
+    pkeys = [torch.from_numpy(pchurn.next_keys().view(np.int32)).cuda() for _ in range(steps + n_sets + 1)]
+    tr2 = accel.Tracker(acc, accel.KACC_KIND_PROC, 500, zone=0, min_energy=10 * 10**6)
+
+    def join2(k):
+        sm2.join(P, off.data_ptr(), pkeys[k].data_ptr(), 0, t["proc_slot"].data_ptr(), tk.data_ptr(),
+                 ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
+
+    for k in range(n_sets + 1):  # warm: the steady state of the first few intervals
+        join2(k)
+    acc.run_interval(interval_from_tensors(t, sizes, flag), stream)
+    acc.sync(stream)
+    treuse, treuse_j, treuse_i = [], [], []
+    for s_ in range(steps):
+        k = s_ % n_sets
+        t.update(t_next[k])
+        it = interval_from_tensors(t, sizes, flag)
+        e0, e1, e2, e3 = (torch.cuda.Event(enable_timing=True) for _ in range(4))
+        e0.record()
+        join2(n_sets + 1 + s_)  # consecutive intervals of churn
+        e1.record()
+        if s_ % 2:
+            tr2.clear(stream)
+        tr2.add(sm2, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), stream)
+        e2.record()
+        acc.run_interval(it, stream)
+        e3.record()
+        e3.synchronize()
+        treuse.append(e0.elapsed_time(e3))
+        treuse_j.append(e0.elapsed_time(e1))
+        treuse_i.append(e2.elapsed_time(e3))
+    acc.sync(stream)
     n_term = int(cnt.sum().item())
     # exposition values of every process row x zone (kacc_format_values), energy and power
     nval = int(slot_off[-1]) * layout.zones
@@ -180,6 +217,8 @@ def main():
         "join_ms": jm, "join_plus_interval_ms": am, "tracker_ms": float(np.median(ttr)),
         "tracker_items": int(tr.items()[0].size),
         "pipeline_ms": float(np.median(tseq)), "pipeline_tracker_beside_interval_ms": float(np.median(tpipe)),
+        "pipeline_reuse_tracker_first_ms": float(np.median(treuse)),
+        "pipeline_reuse_join_ms": float(np.median(treuse_j)), "pipeline_reuse_interval_ms": float(np.median(treuse_i)),
         "join_rows_per_s": P / (jm * 1e-3), "join_plus_interval_proc_attr_per_s": P / (am * 1e-3),
         "join_bytes": join_bytes, "join_GBps": join_bytes / (jm * 1e-3) / 1e9,
         "terminated_last": n_term, "phase_ms": phases,
