@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--frag-line", type=float, default=0.02,
                     help="N = 1: also time this workload under three slot layouts on the same box (pristine "
                          "without / with node_proc_span, F fragmented) and report them as `slot_layouts` (0 = off)")
+    ap.add_argument("--no-pipeline-line", dest="pipeline_line", action="store_false",
+                    help="N = 1, config 3: skip the join -> tracker -> interval line (`pipeline`)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -293,6 +295,82 @@ def slot_layout_lines(args, frag, K, steps, bytes_per_interval, steady_intervals
                    "their container, fleet.ProcChurn); fragmented = synthetic random subset of (1+F) x rows slots "
                    "in random row order")
     return out
+
+
+def pipeline_line(args, steps=10, warm=8):
+    """The production interval at N = 1: kacc_slot_join (KACC_JOIN_REUSE_TERMINATED) on
+    /proc-shaped churn (fleet.ProcChurn, 2 % per interval) -> the terminated trackers
+    (top 500 per node, 10 J, cleared every other interval: config.go:210-211,
+    process.go:80-99) -> the interval kernel on the join's slot words and spans, one
+    stream, HIP events around the three; keys already on the device.  Reported beside
+    the headline, never as `value`."""
+    import torch
+
+    from kepler_amd import accel, fleet
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes))
+    sizes = layout.sizes()
+    N, P = layout.n_nodes, sizes["n_procs"]
+    rows = np.diff(layout.proc_off.astype(np.int64))
+    slot_off = np.r_[0, np.cumsum(np.ceil(rows * 1.05).astype(np.int64) + 8)].astype(np.uint32)
+    caps = layout.capacities()
+    caps["proc_slots"] = int(slot_off[-1])
+    acc = accel.Accel(layout.zones, **caps)
+    stream = current_stream_handle()
+    sm = accel.SlotMap(acc, accel.KACC_KIND_PROC, slot_off)
+    sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
+    tr = accel.Tracker(acc, accel.KACC_KIND_PROC, 500, zone=0, min_energy=10 * 10**6)
+    churn = fleet.ProcChurn(layout, churn=0.02)
+    keys = [torch.from_numpy(churn.next_keys().view(np.int32)).cuda() for _ in range(warm + steps)]
+    sim = fleet.FleetSim(layout, seed=fleet.SEED)
+    statics = to_device(layout.static_arrays())
+    cap = int(slot_off[-1])
+    d_slot = torch.zeros(P, dtype=torch.int32, device="cuda")
+    tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda")
+    span = torch.zeros(2 * N, dtype=torch.int32, device="cuda")
+    full = [to_device({n: a for n, a in sim.next_interval().items() if n != "proc_slot"}) for _ in range(2)]
+    ivs = []
+    for k in range(warm + steps):
+        t = dict(statics)
+        t.update(full[k % 2])
+        t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
+                            if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
+        t["proc_slot"] = d_slot  # the join writes the batch's slot words in place
+        t["node_proc_span"] = span
+        ivs.append((interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES), t))
+    tj, tt, ti, tall = [], [], [], []
+    for k in range(warm + steps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        sm.join(P, ivs[k][1]["proc_off"].data_ptr(), keys[k].data_ptr(), 0, d_slot.data_ptr(), tk.data_ptr(),
+                ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
+        ev[1].record()
+        if k % 2:
+            tr.clear(stream)
+        tr.add(sm, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), stream)
+        ev[2].record()
+        acc.run_interval(ivs[k][0], stream)
+        ev[3].record()
+        if k >= warm:
+            ev[3].synchronize()
+            tj.append(ev[0].elapsed_time(ev[1]))
+            tt.append(ev[1].elapsed_time(ev[2]))
+            ti.append(ev[2].elapsed_time(ev[3]))
+            tall.append(ev[0].elapsed_time(ev[3]))
+    acc.sync(stream)
+    n_term = int(cnt.sum().item())
+    tr.close()
+    sm.close()
+    acc.close()
+    ms = float(np.mean(tall))
+    return {"ms_per_interval": ms, "proc_attr_per_s": P / (ms * 1e-3),
+            "join_ms": float(np.mean(tj)), "tracker_ms": float(np.mean(tt)), "interval_ms": float(np.mean(ti)),
+            "terminated_last_interval": n_term, "intervals": steps,
+            "note": "kacc_slot_join (reuse policy) -> kacc_tracker_add -> kacc_run_interval on one stream, "
+                    "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device"}
 
 
 def bench_nodes(config, world, nodes=None):
@@ -555,6 +633,12 @@ def main():
                                                        bytes_per_launch)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["slot_layouts"] = {"error": repr(e)}
+
+    if world == 1 and args.pipeline_line and args.fragment == 0 and args.config == 3 and K == 1:
+        try:
+            result["pipeline"] = pipeline_line(args)
+        except Exception as e:  # a secondary line: report, never lose the headline
+            result["pipeline"] = {"error": repr(e)}
 
     if rank == 0:
         line = json.dumps(result)

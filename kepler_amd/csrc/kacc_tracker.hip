@@ -38,7 +38,7 @@ namespace kacc {
 namespace trk {
 
 constexpr int kThreads = 256;
-constexpr uint32_t kChunk = 1024;  // batch items filtered / sorted per step
+constexpr uint32_t kChunk = 512;  // batch items filtered / sorted per step; tracked set staged in LDS up to this
 constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node capacity
 
 struct Args {
@@ -101,6 +101,7 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
   __shared__ uint16_t s_ix[kChunk];
   __shared__ uint32_t s_rank[kChunk];
   __shared__ uint64_t s_tk[kChunk];     // a block of tracked keys (duplicate check)
+  __shared__ uint64_t s_te[kChunk];     // tracked target-zone energies (size <= kChunk: the rank search)
   __shared__ uint32_t s_cnt;
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
   const uint32_t Z = a.Z, z0 = a.z0, cap = a.cap;
@@ -130,10 +131,14 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
         pass[u] = e[u] >= a.min_e && !(full && e[u] <= min_full);  // :102, :124
       }
     }
+    const bool lds_set = size <= kChunk;  // block-uniform
     for (uint32_t t0 = 0; t0 < size; t0 += kChunk) {  // :90 already tracked
       const uint32_t tn = min(kChunk, size - t0);
       __syncthreads();
-      for (uint32_t t = tid; t < tn; t += kThreads) s_tk[t] = a.set_key[base + t0 + t];
+      for (uint32_t t = tid; t < tn; t += kThreads) {
+        s_tk[t] = a.set_key[base + t0 + t];
+        if (lds_set) s_te[t] = a.set_e[(base + t) * Z + z0];
+      }
       __syncthreads();
 #pragma unroll
       for (uint32_t u = 0; u < kChunk / kThreads; ++u)
@@ -173,9 +178,9 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
     for (uint32_t j = tid; j < m; j += kThreads) {  // survivor j: + #tracked with e >= its e
       const uint64_t ej = ~s_k1[j];
       uint32_t lo = 0, hi = size;
-      while (lo < hi) {
+      while (lo < hi) {  // the staged energies when the set fits LDS (no dependent global loads)
         const uint32_t mid = (lo + hi) >> 1;
-        if (a.set_e[(base + mid) * Z + z0] >= ej)
+        if ((lds_set ? s_te[mid] : a.set_e[(base + mid) * Z + z0]) >= ej)
           lo = mid + 1;
         else
           hi = mid;
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       uint64_t E[KACC_MAX_ZONES];
       double P[KACC_MAX_ZONES];
       if (have) {  // i + #survivors with a strictly higher energy (ties: tracked first)
-        const uint64_t ei = a.set_e[(base + i) * Z + z0];
+        const uint64_t ei = lds_set ? s_te[i] : a.set_e[(base + i) * Z + z0];
         uint32_t lo = 0, hi = m;
         while (lo < hi) {
           const uint32_t mid = (lo + hi) >> 1;
