@@ -2550,55 +2550,6 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
   if (tid == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
 }
 
-// ProcessTotalCPUTimeDelta of every node of K intervals in one launch
-// (kacc_run_intervals over batches that may hold big nodes): workgroup (n, k)
-// evaluates interval k's node n with the canonical 256-lane tree — lane l adds
-// rows l, l + 256, ... in order from +0.0, then l += l + s for s = 128 ... 1 —
-// the additions big_node_prepare makes, in the same order, so the intervals
-// then run with KACC_F_NODE_CPU_DELTA_GIVEN and bit-identical results.  The
-// K x N workgroups fill the chip: one bandwidth-bound pass over the K
-// intervals' Δ instead of a latency-bound chain per node inside each
-// interval's node phase (BASELINE config 5: 10-50k rows per node).
-__global__ __launch_bounds__(kTree) void node_totals_kernel(const kacc_interval *bs, uint32_t N, double *out) {
-  __shared__ double red[kTree];
-  const uint32_t n = blockIdx.x, k = blockIdx.y, tid = threadIdx.x;
-  const kacc_interval &b = bs[k];
-  if (n >= b.n_nodes) return;  // workgroup-uniform
-  const uint32_t e1 = min(gbl(b.proc_off)[n + 1], b.n_procs);  // clamped: a bad batch never faults here
-  const uint32_t p0 = min(gbl(b.proc_off)[n], e1), rows = e1 - p0;
-  const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
-  double s = 0.0;
-  double v[kTotLoads];
-#pragma unroll
-  for (int j = 0; j < kTotLoads; ++j) {
-    const uint32_t i = tid + j * kTree;
-    v[j] = i < rows ? gbl(dcpu)[i] : 0.0;
-  }
-  for (uint32_t r0 = 0; r0 < rows; r0 += kTree * kTotLoads) {
-    double nx[kTotLoads];
-#pragma unroll
-    for (int j = 0; j < kTotLoads; ++j) {
-      const uint32_t i = r0 + kTree * kTotLoads + tid + j * kTree;
-      nx[j] = i < rows ? gbl(dcpu)[i] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < kTotLoads; ++j)
-      if (r0 + tid + j * kTree < rows) s = s + v[j];
-#pragma unroll
-    for (int j = 0; j < kTotLoads; ++j) v[j] = nx[j];
-  }
-  red[tid] = s;
-  __syncthreads();
-  if (tid < 128) red[tid] = red[tid] + red[tid + 128];
-  __syncthreads();
-  if (tid < 64) {
-    double x = red[tid] + red[tid + 64];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) x = x + __shfl_down(x, d, 64);
-    if (tid == 0) out[static_cast<uint64_t>(k) * N + n] = x;
-  }
-}
-
 }  // namespace kacc
 
 // =============================================================================
@@ -3095,7 +3046,6 @@ void kacc_destroy(kacc_ctx *ctx) {
     (void)hipEventDestroy(ctx->batch_copied);
   }
   if (ctx->d_batches) (void)hipFree(ctx->d_batches);
-  if (ctx->d_nd_pre) (void)hipFree(ctx->d_nd_pre);
   if (ctx->h_batches) (void)hipHostFree(ctx->h_batches);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   if (ctx->copy_stream) {
@@ -3174,41 +3124,8 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
     KACC_HIP(ctx, hipGetLastError());
     return KACC_OK;
   }
-  // batches that may hold big nodes: every node CPU total of the K intervals in
-  // one launch first (node_totals_kernel), then the intervals with them given
-  bool pre = count > 1 && max_nodes > 0;
-  bool any_big = false;
-  for (uint32_t k = 0; k < count && pre; ++k) {
-    pre = !(dev_batches[k].flags & KACC_F_NODE_CPU_DELTA_GIVEN);
-    any_big |= !(dev_batches[k].flags & KACC_F_FAST_NODES) && dev_batches[k].n_nodes > 0;
-  }
-  static const bool no_pre = [] {  // KACC_NODE_PREPASS=0: timing ablation
-    const char *v = getenv("KACC_NODE_PREPASS");
-    return v && !strcmp(v, "0");
-  }();
-  pre = pre && any_big && !no_pre;
-  if (pre) {
-    const uint64_t need = static_cast<uint64_t>(count) * max_nodes;
-    if (need > ctx->nd_pre_cap) {
-      if (ctx->d_nd_pre) KACC_HIP(ctx, hipFree(ctx->d_nd_pre));  // synchronizes: no launch still reads it
-      ctx->d_nd_pre = nullptr;
-      ctx->nd_pre_cap = 0;
-      KACC_HIP(ctx, hipMalloc(&ctx->d_nd_pre, sizeof(double) * need));
-      ctx->nd_pre_cap = need;
-    }
-    if ((rc = stage_batches(ctx, dev_batches, count, st)) != KACC_OK) return rc;
-    hipLaunchKernelGGL(kacc::node_totals_kernel, dim3(static_cast<uint32_t>(max_nodes), count), dim3(kacc::kTree), 0,
-                       st, ctx->d_batches, static_cast<uint32_t>(max_nodes), ctx->d_nd_pre);
-  }
-  for (uint32_t k = 0; k < count; ++k) {
-    if (!dev_batches[k].n_nodes) continue;
-    kacc_interval bk = dev_batches[k];
-    if (pre) {
-      bk.flags |= KACC_F_NODE_CPU_DELTA_GIVEN;
-      bk.node_cpu_delta = ctx->d_nd_pre + static_cast<uint64_t>(k) * max_nodes;
-    }
-    launch(ctx->cfg.zones, bk, ds, st);
-  }
+  for (uint32_t k = 0; k < count; ++k)
+    if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }

@@ -34,8 +34,6 @@ struct kacc_ctx {
   kacc_interval *h_batches = nullptr;  //   and their pinned staging copy
   uint32_t batch_cap = 0;
   hipEvent_t batch_copied = nullptr;
-  double *d_nd_pre = nullptr;  // kacc_run_intervals: node CPU totals of K intervals [K][nodes]
-  uint64_t nd_pre_cap = 0;
   std::string err;
 };
 
