@@ -427,10 +427,36 @@ struct NodeRanges {
 };
 
 // Row ranges of node n, clamped so a malformed batch cannot fault.
+__device__ __forceinline__ NodeRanges clamp_ranges(const kacc_interval &b, const DevState &st, NodeRanges r,
+                                                   int tid);
 __device__ __forceinline__ NodeRanges node_ranges(const kacc_interval &b, const DevState &st,
                                                   uint32_t n, int tid) {
-  NodeRanges r{b.proc_off[n], b.proc_off[n + 1], b.ctr_off[n], b.ctr_off[n + 1],
-               b.vm_off[n],   b.vm_off[n + 1],   b.pod_off[n], b.pod_off[n + 1]};
+  return clamp_ranges(b, st,
+                      NodeRanges{b.proc_off[n], b.proc_off[n + 1], b.ctr_off[n], b.ctr_off[n + 1], b.vm_off[n],
+                                 b.vm_off[n + 1], b.pod_off[n], b.pod_off[n + 1]},
+                      tid);
+}
+
+// Status and row ranges of node n as ONE batch of vector loads through an index
+// the compiler must treat as per-lane, waited for once, then made uniform: as
+// scalar loads they took two dependent round trips (the offsets behind the
+// status branch) before a workgroup could issue its row loads.
+__device__ __forceinline__ void node_words(const kacc_interval &b, uint32_t n, uint32_t &status, NodeRanges &r) {
+  uint32_t ni = n;
+  asm volatile("" : "+v"(ni));
+  const uint32_t *sp = b.node_status ? b.node_status : b.proc_off;  // a stand-in address: no branch
+  const uint32_t s = sp[ni];
+  uint32_t w[8] = {b.proc_off[ni], b.proc_off[ni + 1], b.ctr_off[ni], b.ctr_off[ni + 1],
+                   b.vm_off[ni],   b.vm_off[ni + 1],   b.pod_off[ni], b.pod_off[ni + 1]};
+  asm volatile("" ::"v"(s), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]),
+               "v"(w[7]));  // the one wait
+  status = b.node_status ? __builtin_amdgcn_readfirstlane(s) : 0u;
+  auto u = [](uint32_t x) { return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(x)); };
+  r = NodeRanges{u(w[0]), u(w[1]), u(w[2]), u(w[3]), u(w[4]), u(w[5]), u(w[6]), u(w[7])};
+}
+
+__device__ __forceinline__ NodeRanges clamp_ranges(const kacc_interval &b, const DevState &st, NodeRanges r,
+                                                   int tid) {
   if (r.p1 > b.n_procs || r.p0 > r.p1 || r.c1 > b.n_ctrs || r.c0 > r.c1 || r.v1 > b.n_vms ||
       r.v0 > r.v1 || r.q1 > b.n_pods || r.q0 > r.q1) {
     if (tid == 0) raise_err(st.err, kErrOffsets);
@@ -485,13 +511,15 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     if (tid == 0) raise_err(st.err, kErrNode);
     return;
   }
-  const uint32_t status = b.node_status ? b.node_status[n] : 0u;
+  uint32_t status;
+  NodeRanges raw;
+  node_words(b, n, status, raw);
   if (status & KACC_NODE_READ_ERROR) {
     // node.go:39-44 -> calculatePower fails, previous snapshot kept.
     if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
     return;
   }
-  const NodeRanges rg = node_ranges(b, st, n, tid);
+  const NodeRanges rg = clamp_ranges(b, st, raw, tid);
   if (!fits_fast<V>(rg)) {  // node phase here, the rest in chunk_kernel (+ pod_kernel)
     if (b.flags & KACC_F_FAST_NODES) {  // the caller promised no such node: no launch follows
       if (tid == 0) raise_err(st.err, kErrBigNode);
@@ -1492,12 +1520,14 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     if (lane == 0) raise_err(st.err, kErrNode);
     return;
   }
-  const uint32_t status = b.node_status ? b.node_status[n] : 0u;
+  uint32_t status;
+  NodeRanges raw;
+  node_words(b, n, status, raw);
   if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44
     if (lane == 0) st.node_status[n] = KACC_NODE_SKIPPED;
     return;
   }
-  const NodeRanges rg = node_ranges(b, st, n, static_cast<int>(lane));
+  const NodeRanges rg = clamp_ranges(b, st, raw, static_cast<int>(lane));
   const uint32_t p0 = rg.p0, p1 = rg.p1, c0 = rg.c0, c1 = rg.c1, q0 = rg.q0, q1 = rg.q1;
   const uint32_t rows = p1 - p0, nc = c1 - c0, nv = rg.v1 - rg.v0, nq = q1 - q0;
   if (rows > static_cast<uint32_t>(kSmallRows) || nc + nv + nq > static_cast<uint32_t>(kSmallAgg)) {
