@@ -136,9 +136,12 @@ def test_join_errors_raise_erange():
     assert term == []
 
 
+@pytest.mark.parametrize("churn_model", ["keyed", "proc"])
 @pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
-def test_join_feeds_interval_bit_exact(policy):
-    """Keyed fleet: device join -> interval kernel == oracle join -> oracle interval."""
+def test_join_feeds_interval_bit_exact(policy, churn_model):
+    """Keyed fleet: device join -> interval kernel == oracle join -> oracle interval.
+    churn_model "proc": /proc-shaped churn (fleet.ProcChurn: newcomers listed last in
+    their container), the layout the reuse policy keeps near row order."""
     layout = fleet.make_layout(12, [1500, 2000, 40, 0, 700, 2048] * 2, 4, seed=21)
     sizes = layout.sizes()
     P = layout.n_procs
@@ -150,7 +153,8 @@ def test_join_feeds_interval_bit_exact(policy):
     ojoin = OracleSlotMap(proc_slot_off, policy)
     ora = Oracle(layout.zones, **caps)
     sim = fleet.FleetSim(layout, seed=21, churn=0.0, read_error_frac=0.1)
-    keys_sim = fleet.KeyedChurn(layout.proc_off, seed=21, churn=0.04)
+    keys_sim = (fleet.KeyedChurn(layout.proc_off, seed=21, churn=0.04) if churn_model == "keyed"
+                else fleet.ProcChurn(layout, churn=0.04, seed=21))
     stream = current_stream_handle()
     for it in range(4):
         a = sim.next_interval()
