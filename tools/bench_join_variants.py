@@ -74,7 +74,11 @@ def main():
                 for n in range(0, N, 97):  # a sample of nodes' terminated lists
                     terms.append((tkn[s[n]:s[n] + c[n]].copy(), tsn[s[n]:s[n] + c[n]].copy()))
                 outs.append((out.cpu().numpy().copy(), c, span.cpu().numpy().copy(), terms))
-        acc.sync(stream)
+        try:
+            acc.sync(stream)
+        except accel.AccelError:
+            if variant < 32:  # bits >= 32 are timing ablations that do not compute the join
+                raise
         return ms, outs
 
     ref = None
