@@ -569,18 +569,39 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
   const uint64_t last_dw = label_bytes ? (label_bytes - 1) >> 2 : 0;
   const uint32_t *lw = reinterpret_cast<const uint32_t *>(a.labels);
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kLineWaves * 64;
-  for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kLineWaves + (threadIdx.x >> 6)) * 64; base < lines;
-       base += step) {
-    // ---- this lane's line: offsets and lengths (all loads in flight together)
-    const uint64_t i = min(base + lane, lines - 1);
+  // this lane's line of the batch at `bs`: its offsets and the raw table value,
+  // all loads in flight together (indices clamped: the loads stay unconditional)
+  struct Pre {
+    uint64_t l0, l1, o0, o1, raw;
+    uint32_t j;
+  };
+  auto fetch = [&](uint64_t bs) {
+    Pre p;
+    const uint64_t i = min(bs + lane, lines - 1);
     const uint64_t ri = i / a.n_zones;
-    const uint32_t j = static_cast<uint32_t>(i - ri * a.n_zones);
+    p.j = static_cast<uint32_t>(i - ri * a.n_zones);
     const uint64_t r = line_row(a, ri);
-    const uint64_t l0 = a.label_off[r], l1 = a.label_off[r + 1];
-    const uint64_t o0 = a.line_off[i], o1 = a.line_off[i + 1];
+    p.l0 = a.label_off[r];
+    p.l1 = a.label_off[r + 1];
+    p.o0 = a.line_off[i];
+    p.o1 = a.line_off[i + 1];
+    p.raw = static_cast<const uint64_t *>(a.src)[(a.first + r) * a.Z + a.zone_table[p.j]];
+    return p;
+  };
+  const uint64_t base0 = (static_cast<uint64_t>(blockIdx.x) * kLineWaves + (threadIdx.x >> 6)) * 64;
+  Pre nxt = fetch(min(base0, lines - 1));
+  for (uint64_t base = base0; base < lines; base += step) {
+    // ---- this lane's line (loaded one batch ahead); the next batch's loads go out now
+    const Pre cur = nxt;
+    nxt = fetch(min(base + step, lines - 1));
+    const uint64_t l0 = cur.l0, l1 = cur.l1, o0 = cur.o0, o1 = cur.o1;
+    const uint32_t j = cur.j;
     const uint32_t zpair = (a.zone_pos[j] << 16) | a.zone_len[j];  // z0 | zl
     Text val;
-    line_value(a, (a.first + r) * a.Z + a.zone_table[j], val);
+    if (a.is_energy)
+      write_joules(cur.raw, val);  // energy.go:30-32
+    else
+      write_float(__longlong_as_double(static_cast<long long>(cur.raw)) / 1e6, val);  // energy.go:57-59
     const uint32_t vl = val.n;
     const uint64_t v0 = val.w[0], v1 = val.w[1], v2 = val.w[2];
     const uint32_t nl = static_cast<uint32_t>(min<uint64_t>(lines - base, 64));
@@ -607,15 +628,20 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
         if (dw_labels) {  // 4 label bytes per dword pair (v_alignbyte), 8 dwords in flight
           const uint64_t q0 = l0 >> 2;
           const uint32_t sh = static_cast<uint32_t>(l0 & 3u);
-          for (uint64_t p0 = 0; p0 < n; p0 += 28) {
-            uint32_t w[8];
+          uint32_t w[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) w[q] = lw[min(q0 + (p0 >> 2) + q, last_dw)];
+          for (int q = 0; q < 8; ++q) w[q] = lw[min(q0 + q, last_dw)];
+          for (uint64_t p0 = 0; p0 < n; p0 += 28) {
+            uint32_t wn[8];  // the next 28 bytes' dwords go out before these are packed
+#pragma unroll
+            for (int q = 0; q < 8; ++q) wn[q] = lw[min(q0 + ((p0 + 28) >> 2) + q, last_dw)];
 #pragma unroll
             for (int q = 0; q < 7; ++q) {
               const uint64_t at = p0 + 4u * q;
               if (at < n) pk_put(p, __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh), static_cast<uint32_t>(min<uint64_t>(4, n - at)));
             }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w[q] = wn[q];
           }
         } else {
           const char *lb = a.labels + l0;
