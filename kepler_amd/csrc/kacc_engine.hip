@@ -2079,27 +2079,50 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
   uint32_t idx = blockIdx.x;  // first item static, the rest dequeued
   for (uint32_t parity = 0; idx < count; parity ^= 1u) {
     if (tid == 0) s_next[parity] = atomicAdd(st.item_ctr + 1, 1u) + gridDim.x;
-    const ChunkItem *it = st.items + idx;
-    const uint32_t n = uniform_u32(it->node);
-    const uint32_t k = uniform_u32(it->chunk);
-    const uint32_t nch = uniform_u32(it->nchunks);
+    // the item's words and its successor's begins as ONE batch of vector loads
+    // (waited for once), then the node's ranges as another: as scalar loads
+    // behind the `last` selects they took nine dependent round trips per chunk
+    uint32_t f[9];
+    {
+      uint32_t ii = idx;
+      asm volatile("" : "+v"(ii));
+      const uint32_t *w0 = reinterpret_cast<const uint32_t *>(st.items + ii);
+      const uint32_t *w1 = reinterpret_cast<const uint32_t *>(st.items + min(ii + 1, st.item_cap - 1));
+      f[0] = w0[0];
+      f[1] = w0[1];
+      f[2] = w0[2];
+      f[3] = w0[3];
+      f[4] = w0[4];
+      f[5] = w0[5];
+      f[6] = w1[3];
+      f[7] = w1[4];
+      f[8] = w1[5];
+      asm volatile("" ::"v"(f[0]), "v"(f[1]), "v"(f[2]), "v"(f[3]), "v"(f[4]), "v"(f[5]), "v"(f[6]), "v"(f[7]),
+                   "v"(f[8]));
+#pragma unroll
+      for (int q = 0; q < 9; ++q) f[q] = uniform_u32(f[q]);
+    }
+    const uint32_t n = f[0], k = f[1], nch = f[2];
     if (n >= b.n_nodes) {  // corrupt item: cannot happen unless the list overflowed
       if (tid == 0) raise_err(st.err, kErrCapacity);
       __syncthreads();
       idx = uniform_u32(s_next[parity]);
       continue;
     }
-    const NodeRanges rg = node_ranges(b, st, n, tid);
+    uint32_t status_unused;
+    NodeRanges raw;
+    node_words(b, n, status_unused, raw);
+    const NodeRanges rg = clamp_ranges(b, st, raw, tid);
     const bool last = k + 1 >= nch;
     const uint32_t lo = min(rg.p0 + min(k, nch) * static_cast<uint32_t>(kChunkRows), rg.p1);
     const uint32_t hi = last ? rg.p1 : min(lo + static_cast<uint32_t>(kChunkRows), rg.p1);
     const uint32_t rows = hi - lo;
-    const uint32_t cb = min(max(uniform_u32(it->ctr_begin), rg.c0), rg.c1);
-    const uint32_t ce = max(min(last ? rg.c1 : uniform_u32(it[1].ctr_begin), rg.c1), cb);
-    const uint32_t vb = min(max(uniform_u32(it->vm_begin), rg.v0), rg.v1);
-    const uint32_t ve = max(min(last ? rg.v1 : uniform_u32(it[1].vm_begin), rg.v1), vb);
-    const uint32_t qb = min(max(uniform_u32(it->pod_begin), rg.q0), rg.q1);
-    const uint32_t qe = max(min(last ? rg.q1 : uniform_u32(it[1].pod_begin), rg.q1), qb);
+    const uint32_t cb = min(max(f[3], rg.c0), rg.c1);
+    const uint32_t ce = max(min(last ? rg.c1 : f[6], rg.c1), cb);
+    const uint32_t vb = min(max(f[4], rg.v0), rg.v1);
+    const uint32_t ve = max(min(last ? rg.v1 : f[7], rg.v1), vb);
+    const uint32_t qb = min(max(f[5], rg.q0), rg.q1);
+    const uint32_t qe = max(min(last ? rg.q1 : f[8], rg.q1), qb);
     const uint32_t nca = kAgg ? ce - cb : 0u;
     const uint32_t ncv = kAgg ? nca + (ve - vb) : 0u;  // containers + VMs
     const uint32_t nagg = kAgg ? ncv + (qe - qb) : 0u;  // + pods
