@@ -67,6 +67,7 @@ FLEETS = [
     ("config3-like", [2000] * 16, 4, 0.02, 500),
     ("unlimited", [500, 200, 1500], 2, 0.05, -1),
     ("big-node", [12000, 300, 2500], 4, 0.03, 200),
+    ("config3-shape-1k-nodes", [2000] * 1000, 4, 0.02, 500),  # 2M rows: the production pipeline's scale per node
 ]
 
 
@@ -98,7 +99,8 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
     ojoin, ora = OracleSlotMap(slot_off, int(reuse)), Oracle(Z, **caps)
     otr = OracleTracker(max_size, thr, Z, 0)
     sim = fleet.FleetSim(layout, seed=31, churn=0.0, read_error_frac=0.05)
-    keys_sim = fleet.KeyedChurn(layout.proc_off, seed=31, churn=churn)
+    keys_sim = (fleet.ProcChurn(layout, churn=churn, seed=31) if reuse  # the production pairing
+                else fleet.KeyedChurn(layout.proc_off, seed=31, churn=churn))
     cap = int(slot_off[-1])
     tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
     ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
