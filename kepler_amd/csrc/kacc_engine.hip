@@ -55,10 +55,25 @@ constexpr int kVarTemporalStores = 8;  // plain (temporal) stores for the row ou
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
 constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
 constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row order only)
+constexpr int kVarNtAgg = 4096;        // non-temporal stores for the aggregate rows too (round 2)
 constexpr int kVarTemporalLoads = 16384;  // plain loads of the streamed inputs and prev totals
 constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
 constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
 constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk kernel idles)
+
+// interval_kernel stores the aggregate rows (containers / VMs / pods: 32 B
+// energy + 32 B power per row, at slots scattered over the tables) through L2,
+// unlike the process row streams: a non-temporal 32 B store goes to HBM as a
+// partial line, while L2 merges the rows of one line written by different
+// nodes' blocks.  Measured 2-9 % of interval_kernel<4,0> at config 3 in three
+// in-process A/Bs (profiles/r02/aggab); the hint on the process rows stays
+// (5 %, profiles/r01/ablations).  The other kernels keep non-temporal stores:
+// process-to-process A/Bs at configs 1, 2, 5 were inside the placement spread.
+// KACC_NT_AGG=1 builds the earlier behaviour for A/B.
+#ifndef KACC_NT_AGG
+#define KACC_NT_AGG 0
+#endif
+constexpr bool kNtAggStores = KACC_NT_AGG != 0;
 constexpr uint32_t kPodGrid = 256;     // deferred-pod kernel workgroups (kBlock threads)
 constexpr int kChunkRows = kRowsLds;   // big-node rows per chunk item
 constexpr int kChunkThreads = 512;     // chunk kernel workgroup
@@ -493,6 +508,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   // Cache): loads + stores together measured 5 % faster (profiles/r01/ablations)
   constexpr bool kNT = (V & kVarTemporalStores) == 0;
   constexpr bool kNtLd = (V & kVarTemporalLoads) == 0;
+  constexpr bool kNtAgg = kNT && (kNtAggStores || (V & kVarNtAgg) != 0);
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
   __shared__ uint32_t s_w[kRowsLds];  // and their slot words (frees VGPRs across barriers)
   __shared__ double s_cd[kThreads];  // container Δ of this interval
@@ -782,8 +798,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     double P[Z];
     attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0,
                      a_prev, E, P);
-    store_row<Z, kNT, uint64_t>(a_energy(), a_s, E);
-    store_row<Z, kNT, double>(a_power(), a_s, P);
+    store_row<Z, kNtAgg, uint64_t>(a_energy(), a_s, E);
+    store_row<Z, kNtAgg, double>(a_power(), a_s, P);
   };
   if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
@@ -2763,6 +2779,7 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 768: launch_zv<4, 768>(b, s, st); return true;
     case 1024: launch_zv<4, 1024>(b, s, st); return true;
     case 2048: launch_zv<4, 2048>(b, s, st); return true;
+    case 4096: launch_zv<4, 4096>(b, s, st); return true;
     case 16384: launch_zv<4, 16384>(b, s, st); return true;
     case 16392: launch_zv<4, 16392>(b, s, st); return true;
     case 65536: launch_small<4>(b, s, st); return true;  // one wavefront per node

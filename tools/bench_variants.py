@@ -59,24 +59,46 @@ def main():
     sizes = layout.sizes()
     nbytes = accel.interval_bytes(Z, *[sizes[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
     times = {v: [] for v in variants}
+    step_t = {v: [] for v in variants}
+    off, slots = layout.namespace_csr()
+    ns = to_device({"o": off, "s": slots})
+    n_ns = len(off) - 1
+    # STEP=1: bench.py's step, the variant followed by the cluster partials (namespace + node
+    # totals, world 1) on the same stream; times both the variant alone and the pair
+    step_mode = bool(os.environ.get("STEP"))
+    if step_mode:
+        cluster = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
+        pe = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
+        pp = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
+        ne = torch.zeros(2 * Z, dtype=torch.int64, device="cuda")
+        npw = torch.zeros(3 * Z, dtype=torch.float64, device="cuda")
+
+    def partials():
+        cluster.allreduce_namespaces(n_ns, [ns["o"].data_ptr()], [ns["s"].data_ptr()], [pe.data_ptr()],
+                                     [pp.data_ptr()], [ne.data_ptr()], [npw.data_ptr()], streams=[stream],
+                                     comm_streams=[stream])
+
     for v in variants:  # warm
         acc.run_variant(it, stream, v)
+        if step_mode:
+            partials()
     acc.sync(stream)
     launch = 0
     for _ in range(rounds):
         for v in variants:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             it = ivs[launch % n_distinct]
             launch += 1
             e0.record()
             acc.run_variant(it, stream, v)
             e1.record()
-            e1.synchronize()
+            if step_mode:
+                partials()
+            e2.record()
+            e2.synchronize()
             times[v].append(e0.elapsed_time(e1))
+            step_t[v].append(e0.elapsed_time(e2))
     acc.sync(stream)
-    off, slots = layout.namespace_csr()
-    ns = to_device({"o": off, "s": slots})
-    n_ns = len(off) - 1
     oe = torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda")
     op = torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda")
     ns_t = []
@@ -103,6 +125,11 @@ def main():
     out = {"config": cfg, "copy_GBps": copy_gbps, "sizes": sizes, "bytes_per_launch": nbytes,
            "variants": {str(v): {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for v, t in times.items()},
            "namespace_ms": float(np.median(ns_t))}
+    if step_mode:
+        out["step_median_ms"] = {str(v): float(np.median(t)) for v, t in step_t.items()}
+        out["partials_median_ms"] = {str(v): float(np.median(np.array(step_t[v]) - np.array(times[v])))
+                                     for v in variants}
+        cluster.close()
     if 0 in times:
         out["achieved_GBps_v0"] = nbytes / (np.median(times[0]) * 1e-3) / 1e9
     print(json.dumps(out, indent=1))
