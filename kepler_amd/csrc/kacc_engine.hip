@@ -56,6 +56,7 @@ constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group 
 constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
 constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row order only)
 constexpr int kVarNtAgg = 4096;        // non-temporal stores for the aggregate rows too (round 2)
+constexpr int kVarNtScatter = 8192;    // non-temporal per-row scattered process stores (round 2)
 constexpr int kVarTemporalLoads = 16384;  // plain loads of the streamed inputs and prev totals
 constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
 constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
@@ -74,6 +75,16 @@ constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk 
 #define KACC_NT_AGG 0
 #endif
 constexpr bool kNtAggStores = KACC_NT_AGG != 0;
+// Process rows that take the per-row fallback (a node's slots neither sweepable
+// nor in contiguous 64-slot groups: fragmented ranges, the held join policy)
+// are stored through L2 too: one 32 B row per lane at scattered slots is the
+// aggregate case again, and non-temporal partial lines made that fallback 3.2x
+// slower at config 3 with 10 % slot fragmentation (profiles/r02/fragst).
+// KACC_NT_SCATTER=1 builds the earlier behaviour.
+#ifndef KACC_NT_SCATTER
+#define KACC_NT_SCATTER 0
+#endif
+constexpr bool kNtScatterStores = KACC_NT_SCATTER != 0;
 constexpr uint32_t kPodGrid = 256;     // deferred-pod kernel workgroups (kBlock threads)
 constexpr int kChunkRows = kRowsLds;   // big-node rows per chunk item
 constexpr int kChunkThreads = 512;     // chunk kernel workgroup
@@ -509,6 +520,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   constexpr bool kNT = (V & kVarTemporalStores) == 0;
   constexpr bool kNtLd = (V & kVarTemporalLoads) == 0;
   constexpr bool kNtAgg = kNT && (kNtAggStores || (V & kVarNtAgg) != 0);
+  constexpr bool kNtScat = kNT && (kNtScatterStores || (V & kVarNtScatter) != 0);
   __shared__ double s_d[kRowsLds];   // this node's Δcpu rows
   __shared__ uint32_t s_w[kRowsLds];  // and their slot words (frees VGPRs across barriers)
   __shared__ double s_cd[kThreads];  // container Δ of this interval
@@ -851,8 +863,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       uint64_t E[Z];
       double P[Z];
       attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E, P);
-      store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
-      store_row<Z, kNT, double>(st.proc_power, sl, P);
+      store_row<Z, kNtScat, uint64_t>(st.proc_energy, sl, E);
+      store_row<Z, kNtScat, double>(st.proc_power, sl, P);
     }
   }
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
@@ -1446,8 +1458,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         for (int z = 0; z < Z; ++z) pv[z] = s_cE[r * Z + z];
         attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E, P);
         if constexpr ((V & kCarryNoRowStores) == 0) {
-          store_row<Z, true, uint64_t>(st.proc_energy, sl, E);
-          store_row<Z, true, double>(st.proc_power, sl, P);
+          store_row<Z, kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
+          store_row<Z, kNtScatterStores, double>(st.proc_power, sl, P);
         }
 #pragma unroll
         for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = E[z];
@@ -1857,8 +1869,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
       uint64_t E[Z];
       double P[Z];
       attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[g], E, P);
-      store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
-      store_row<Z, kNT, double>(st.proc_power, sl, P);
+      store_row<Z, kNT && kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
+      store_row<Z, kNT && kNtScatterStores, double>(st.proc_power, sl, P);
     }
   };
   attr_batch(0);
@@ -2341,8 +2353,8 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
         uint64_t E[Z];
         double P[Z];
         attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E, P);
-        store_row<Z, kNT, uint64_t>(st.proc_energy, sl, E);
-        store_row<Z, kNT, double>(st.proc_power, sl, P);
+        store_row<Z, kNT && kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
+        store_row<Z, kNT && kNtScatterStores, double>(st.proc_power, sl, P);
       }
     }
     // aggregates beyond one per lane (chunks of mostly empty containers):
@@ -2780,6 +2792,7 @@ bool launch_variant(uint32_t Z, int v, const kacc_interval &b, const kacc::DevSt
     case 1024: launch_zv<4, 1024>(b, s, st); return true;
     case 2048: launch_zv<4, 2048>(b, s, st); return true;
     case 4096: launch_zv<4, 4096>(b, s, st); return true;
+    case 8192: launch_zv<4, 8192>(b, s, st); return true;
     case 16384: launch_zv<4, 16384>(b, s, st); return true;
     case 16392: launch_zv<4, 16392>(b, s, st); return true;
     case 65536: launch_small<4>(b, s, st); return true;  // one wavefront per node
