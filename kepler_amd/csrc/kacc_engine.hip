@@ -68,8 +68,9 @@ constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk 
 // partial line, while L2 merges the rows of one line written by different
 // nodes' blocks.  Measured 2-9 % of interval_kernel<4,0> at config 3 in three
 // in-process A/Bs (profiles/r02/aggab); the hint on the process rows stays
-// (5 %, profiles/r01/ablations).  The other kernels keep non-temporal stores:
-// process-to-process A/Bs at configs 1, 2, 5 were inside the placement spread.
+// (5 %, profiles/r01/ablations).  The carry kernel does the same (1.4 %, config
+// 2 x 60); small / chunk / pod kernels keep non-temporal aggregate stores:
+// process-to-process A/Bs at configs 1 and 5 were inside the placement spread.
 // KACC_NT_AGG=1 builds the earlier behaviour for A/B.
 #ifndef KACC_NT_AGG
 #define KACC_NT_AGG 0
@@ -1081,6 +1082,8 @@ constexpr int kCarryPrefetch = 2;      // rows loaded an interval ahead into reg
 constexpr int kCarryNoAggregates = 4;  // containers / VMs / pods skipped
 constexpr int kCarryNeverMoved = 8;    // never take the moved path (no barrier, no reload)
 constexpr int kCarryStamps = 16;       // per-wave s_memtime phase totals into st.items (diagnostic)
+constexpr int kCarryNtAgg = 32;        // aggregate rows stored non-temporal (round 2; production
+                                       // stores them through L2: 1.4 %, profiles/r02/aggab/carry_c2.log)
 constexpr int kCarryPhases = 8;
 
 template <int Z, int V = 0, int T = 512>
@@ -1408,8 +1411,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, c_aE, E, P);
         uint64_t *ae = role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy;
         double *ap = role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
-        store_row<Z, true, uint64_t>(ae, a_s, E);
-        store_row<Z, true, double>(ap, a_s, P);
+        store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, uint64_t>(ae, a_s, E);
+        store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, double>(ap, a_s, P);
 #pragma unroll
         for (int z = 0; z < Z; ++z) c_aE[z] = E[z];
         c_atotal = a_total;
@@ -3676,6 +3679,7 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint
     case 4: launch_carry<4>(2, medium, ctx->d_batches, count, nn, ds, st); break;
     case 5: launch_carry<5>(2, medium, ctx->d_batches, count, nn, ds, st); break;
     case 8: launch_carry<8>(2, medium, ctx->d_batches, count, nn, ds, st); break;
+    case 32: launch_carry<32>(2, medium, ctx->d_batches, count, nn, ds, st); break;
     default: return fail(ctx, KACC_EINVAL, "variant %d not built", variant);
   }
   KACC_HIP(ctx, hipGetLastError());
