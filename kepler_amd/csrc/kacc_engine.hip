@@ -68,9 +68,10 @@ constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk 
 // partial line, while L2 merges the rows of one line written by different
 // nodes' blocks.  Measured 2-9 % of interval_kernel<4,0> at config 3 in three
 // in-process A/Bs (profiles/r02/aggab); the hint on the process rows stays
-// (5 %, profiles/r01/ablations).  The carry kernel does the same (1.4 %, config
-// 2 x 60); small / chunk / pod kernels keep non-temporal aggregate stores:
-// process-to-process A/Bs at configs 1 and 5 were inside the placement spread.
+// (5 %, profiles/r01/ablations).  The carry kernel (1.4 %, config 2 x 60) and
+// small_kernel (1.1 %, config 1, three process pairs, profiles/r02/aggrest) do
+// the same; chunk_kernel / pod_kernel keep non-temporal aggregate stores (1.5 %
+// slower plain at config 5, where a big node's aggregates are long runs).
 // KACC_NT_AGG=1 builds the earlier behaviour for A/B.
 #ifndef KACC_NT_AGG
 #define KACC_NT_AGG 0
@@ -1822,8 +1823,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     double P[Z];
     attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h], (a_w[h] & KACC_SLOT_NEW) != 0,
                      a_prev[h], E, P);
-    store_row<Z, kNT, uint64_t>(energy_of(role), a_s, E);
-    store_row<Z, kNT, double>(power_of(role), a_s, P);
+    store_row<Z, kNT && kNtAggStores, uint64_t>(energy_of(role), a_s, E);
+    store_row<Z, kNT && kNtAggStores, double>(power_of(role), a_s, P);
   }
   auto attr_batch = [&](int kb) {  // process.go:118-148
 #pragma unroll
