@@ -7,18 +7,22 @@ node split + segmented CPU-time sums + process/container/VM/pod attribution
 (one kacc_run_interval launch) followed by the cluster namespace totals
 (kacc_namespace_totals, then an RCCL all-reduce across GPUs when N > 1).
 
-Workload: BASELINE config 3 per GPU — 10k nodes x 2k processes, Z = 4 RAPL
-zones (package/core/uncore/dram), ~1.6k container processes / 200 containers /
-71 pods / 20 VMs per node, synthetic inputs (kepler_amd/fleet.py) resident in
-HBM before timing.  Scaling is weak: the fleet has N x 10k nodes, cut into N
-node ranges by shard.plan_node_ranges (balanced process rows), and every rank
+Workload: BASELINE config 3 — a 10k-node fleet of 2k processes per node, Z = 4
+RAPL zones (package/core/uncore/dram), ~1.6k container processes / 200
+containers / 71 pods / 20 VMs per node, synthetic inputs (kepler_amd/fleet.py)
+resident in HBM before timing.  Scaling is STRONG (the north star's "10k-node x
+2k-process fleet interval" at 1/2/4/8 GPUs): the fixed fleet is cut into N node
+ranges by shard.plan_node_ranges (balanced process rows) and every rank
 generates and owns only its range (node snapshots are independent), so N GPUs
-process N x 20M process rows per interval.  Only the cluster totals cross GPUs:
-per-namespace and cluster node totals, all-reduced by the library's own RCCL
-communicator (kacc_cluster_join + kacc_allreduce_namespaces, the C ABI a cgo
-caller uses; at N = 1 the same call runs with a one-rank communicator).
-torch.distributed (gloo) is only the control plane: rank-0 unique-id
-broadcast, barriers, max-over-ranks timing.
+share one 20M-row interval.  At N > 1 a weak-scaling line (a full 10k-node shard
+per GPU) is added as `weak_scaling`; `--scaling weak` makes it the headline.
+`--shard-of W` runs rank 0's shard of a W-way split on one GPU (the per-GPU step
+of a W-GPU run).  Only the cluster totals cross GPUs: per-namespace and cluster
+node totals, all-reduced by the library's own RCCL communicator
+(kacc_cluster_join + kacc_allreduce_namespaces, the C ABI a cgo caller uses; at
+N = 1 the same call runs with a one-rank communicator).  torch.distributed
+(gloo) is only the control plane: rank-0 unique-id broadcast, barriers,
+max-over-ranks timing.
 
 Prints ONE JSON line on rank 0.  Launch with N > 1 as
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
@@ -67,6 +71,14 @@ def parse():
                          "without / with node_proc_span, F fragmented) and report them as `slot_layouts` (0 = off)")
     ap.add_argument("--no-pipeline-line", dest="pipeline_line", action="store_false",
                     help="N = 1, config 3: skip the join -> tracker -> interval line (`pipeline`)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="N > 1: strong = the config's fixed fleet (config 3: 10k nodes) cut into N node ranges "
+                         "(the north star's 8-GPU target); weak = N x the fleet, a full shard per GPU")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="N = 1 only: run rank 0's shard of a W-way split of the fleet on this GPU (the per-GPU "
+                         "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
+    ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
+                    help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -373,120 +385,130 @@ def pipeline_line(args, steps=10, warm=8):
                     "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device"}
 
 
-def bench_nodes(config, world, nodes=None):
-    """Fleet size of a config at `world` GPUs: weak scaling (a fixed shard per GPU) except
-    config 4, whose 100k-node fleet is split over the GPUs (strong scaling)."""
+def bench_nodes(config, world, nodes=None, scaling="strong"):
+    """Fleet size of a config at `world` GPUs.  Strong scaling (the north star's "10k-node x
+    2k-process fleet interval" at 1/2/4/8 GPUs): one fixed fleet cut into `world` node ranges.
+    Weak scaling: a fixed shard per GPU, `world` times the fleet.  Config 4 is always its
+    100k-node fleet split over the GPUs."""
     if config == 4:
         return nodes or 100_000
     per = nodes or {1: 40000, 2: 1000, 3: 10000, 5: 1000}[config]
-    return per * world
+    return per if scaling == "strong" else per * world
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+class Workload:
+    """One rank's node shard of a fleet, its per-step interval descriptors (inputs resident in
+    HBM), the engine context, the cluster (RCCL) and the namespace CSR."""
+
+    def __init__(self, args, total_nodes, split, shard_rank, rank, world, local, K, uid_fn):
+        import torch
+
+        from kepler_amd import accel, fleet
+        from kepler_amd.torch_batch import interval_from_tensors, to_device
+
+        t0 = time.time()
+        self.lo, self.hi, layout = fleet.config_shard(args.config, split, shard_rank, total_nodes,
+                                                      fragment_slots=args.fragment)
+        self.layout = layout
+        self.sizes = sizes = layout.sizes()
+        self.Z = Z = layout.zones
+        self.K = K
+        sim = fleet.FleetSim(layout, seed=fleet.SEED + self.lo)
+        n_steps = args.warmup + args.steps
+        n_ivs = n_steps * K  # every interval has its own node counters / clocks
+        n_distinct = max(1, min(args.distinct, n_ivs))
+        self.prime = sim.next_interval()  # first read (monitor.go:326-330), untimed
+        self.full = [sim.next_interval() for _ in range(n_distinct)]
+        self.node_steps = [self.full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_ivs)]
+        log(rank, f"[bench] rank 0 nodes [{self.lo}, {self.hi}) of {total_nodes} (split {split}): {sizes} Z={Z}, "
+                  f"inputs in {time.time() - t0:.1f}s")
+        self.acc = accel.Accel(Z, **layout.capacities(), device=local)
+        self.cluster = accel.Cluster.join(self.acc, exchange_unique_id(rank, world, uid_fn), world, rank)
+        statics = to_device(layout.static_arrays())
+        if args.fragment > 0:  # the slot join's per-node spans: rows moved in slot order
+            statics.update(to_device({"node_proc_span": layout.proc_span()}))
+        dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
+                    for a in self.full]
+        node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")
+        dev_nodes = [to_device({k: a[k] for k in node_keys}) for a in self.node_steps]
+        order = to_device({"o": layout.node_order_heaviest_first()})["o"] if args.node_order else None
+
+        def make(k):
+            t = dict(statics)
+            t.update(dev_full[k % n_distinct])
+            t.update(dev_nodes[k])
+            if order is not None:
+                t["node_order"] = order
+            return t
+
+        self.iv_tensors = [make(k) for k in range(n_ivs)]
+        # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
+        # runs K > 1 fast-node intervals as one launch
+        self.flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+        self.ivs = [interval_from_tensors(t, sizes, self.flags) for t in self.iv_tensors]
+        self.iv_arrays = [(accel.KaccInterval * K)(*self.ivs[k * K:(k + 1) * K]) for k in range(n_steps)]
+        ns_off, ns_slot = layout.namespace_csr()
+        self.ns_t = to_device({"off": ns_off, "slot": ns_slot})
+        self.n_ns = len(ns_off) - 1
+        # cluster totals double-buffered: step k's all-reduce (comm stream) overlaps step k+1's
+        # interval; buffer k % 2 is rewritten only after the all-reduce of step k-2 is done
+        self.ns_e = [torch.zeros(self.n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+        self.ns_p = [torch.zeros(self.n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+        self.nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+        self.nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+
+    def close(self):
+        self.cluster.close()
+        self.acc.close()
+
+
+def measure(args, w, rank, world, stream, comm_stream):
+    """W untimed warm-up steps, then exactly `steps` steps bracketed by barrier + synchronize;
+    returns (max wall seconds over ranks, per-interval kernel ms of the launch stream).  A step =
+    K intervals (one kacc_run_intervals call) + the cluster totals (partial sums on the compute
+    stream, the RCCL all-reduce on the comm stream overlapping the next step).  The host side of
+    a step is a handful of C calls with prebuilt arguments: at a 1/8 shard a step is ~60 us of
+    GPU work, so the issue path must stay far below that."""
+    import ctypes
 
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local)
-    # an explicit stream: the engine launches on it and the HIP events below
-    # time exactly that stream (a NULL handle would mean the context's stream)
-    torch.cuda.set_stream(torch.cuda.Stream())
-    comm_stream = torch.cuda.Stream()  # the cluster all-reduce overlaps the next interval
-    if world > 1:  # control plane only (unique id, barriers, max over ranks); data path: RCCL
-        dist.init_process_group("gloo")
+    from kepler_amd import accel
 
-    from kepler_amd import accel, fleet
-    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
-
-    t_setup = time.time()
-    total_nodes = bench_nodes(args.config, world, args.nodes)
-    lo, hi, layout = fleet.config_shard(args.config, world, rank, total_nodes, fragment_slots=args.fragment)
-    sim = fleet.FleetSim(layout, seed=fleet.SEED + lo)
-    Z = layout.zones
-    sizes = layout.sizes()
-    log(rank, f"[bench] rank 0 nodes [{lo}, {hi}) of {total_nodes}: {sizes} Z={Z} "
-              f"built in {time.time() - t_setup:.1f}s")
-
-    K = max(1, args.intervals)
-    n_steps = args.warmup + args.steps
-    n_ivs = n_steps * K  # every interval has its own node counters / clocks
-    n_distinct = max(1, min(args.distinct, n_ivs))
-    prime = sim.next_interval()  # first read (monitor.go:326-330), untimed
-    full = [sim.next_interval() for _ in range(n_distinct)]
-    node_steps = [full[k] if k < n_distinct else sim.next_node_inputs() for k in range(n_ivs)]
-    log(rank, f"[bench] inputs generated in {time.time() - t_setup:.1f}s")
-
-    acc = accel.Accel(Z, **layout.capacities(), device=local)
-    uid = exchange_unique_id(rank, world, accel.Cluster.unique_id)
-    cluster = accel.Cluster.join(acc, uid, world, rank)
-    stream = current_stream_handle()
-    assert stream != 0
-    statics = to_device(layout.static_arrays())
-    if args.fragment > 0:  # the slot join's per-node spans: rows moved in slot order
-        statics.update(to_device({"node_proc_span": layout.proc_span()}))
-    dev_full = [to_device({k: a[k] for k in ("proc_cpu_delta", "proc_slot", "ctr_slot", "vm_slot", "pod_slot")})
-                for a in full]
-    node_keys = ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")
-    dev_nodes = [to_device({k: a[k] for k in node_keys}) for a in node_steps]
-    order = to_device({"o": layout.node_order_heaviest_first()})["o"] if args.node_order else None
-
-    def make(k):
-        t = dict(statics)
-        t.update(dev_full[k % n_distinct])
-        t.update(dev_nodes[k])
-        if order is not None:
-            t["node_order"] = order
-        return t
-
-    iv_tensors = [make(k) for k in range(n_ivs)]
-    # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
-    # runs K > 1 fast-node intervals as one launch
-    ivs = [interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES) for t in iv_tensors]
-    prime_t = to_device(prime)
-    acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
-    acc.sync(stream)
-    del prime_t
-
-    ns_off, ns_slot = layout.namespace_csr()
-    ns_t = to_device({"off": ns_off, "slot": ns_slot})
-    n_ns = len(ns_off) - 1
-    # cluster totals double-buffered: step k's all-reduce (comm stream) overlaps step k+1's
-    # interval; buffer k % 2 is rewritten only after the all-reduce of step k-2 is done
-    ns_e = [torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
-    ns_p = [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
-    nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
-    nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
-    done = [None, None]
-    cs = comm_stream.cuda_stream
+    lib = accel.load()
+    K = w.K
+    acc, cl = w.acc, w.cluster
+    cstream = ctypes.c_void_p(stream)
+    P = lambda vals: (ctypes.c_void_p * 1)(*[ctypes.c_void_p(v) for v in vals])  # noqa: E731
+    ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
+                P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]), P([w.nd_p[b].data_ptr()]), P([stream]),
+                P([comm_stream.cuda_stream])) for b in range(2)]
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    used = [False, False]
+    compute = torch.cuda.current_stream()
 
     def step(k, ev=None):
         if ev is not None:
             ev[0].record()
-        if K == 1:
-            acc.run_interval(ivs[k], stream)
-        else:  # K consecutive intervals, back to back from C
-            acc.run_intervals(ivs[k * K:(k + 1) * K], stream)
+        rc = lib.kacc_run_intervals(acc.ctx, w.iv_arrays[k], K, cstream)
+        if rc != accel.KACC_OK:
+            acc._check(rc)
         if ev is not None:
             ev[1].record()
         b = k % 2
-        if done[b] is not None and not done[b].query():  # stream-level wait (no host sync) unless done
-            torch.cuda.current_stream().wait_event(done[b])
-        cluster.allreduce_namespaces(n_ns, [ns_t["off"].data_ptr()], [ns_t["slot"].data_ptr()],
-                                     [ns_e[b].data_ptr()], [ns_p[b].data_ptr()], [nd_e[b].data_ptr()],
-                                     [nd_p[b].data_ptr()], streams=[stream], comm_streams=[cs])
-        done[b] = torch.cuda.Event()
+        if used[b]:  # stream-level wait for the all-reduce of step k-2 (no host sync)
+            compute.wait_event(done[b])
+        rc = lib.kacc_allreduce_namespaces(cl.handle, w.n_ns, *ns_args[b])
+        if rc != accel.KACC_OK:
+            cl._check(rc)
         done[b].record(comm_stream)
+        used[b] = True
 
     for k in range(args.warmup):
         step(k)
     acc.sync(stream)
     torch.cuda.synchronize()
-    log(rank, f"[bench] warmup done, setup {time.time() - t_setup:.1f}s")
-
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
     if world > 1:
@@ -501,6 +523,50 @@ def main():
     wall = time.perf_counter() - t0
     acc.sync(stream)  # surfaces any device-detected range error
     kernel_ms = [a.elapsed_time(b) / K for a, b in events]  # per interval
+    wall_t = torch.tensor([wall], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+    return float(wall_t.item()), kernel_ms
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.shard_of > 1 and world > 1:
+        raise SystemExit("--shard-of emulates one rank's shard on ONE GPU (world 1 only)")
+    scaling = "strong" if args.config == 4 else args.scaling
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local)
+    # an explicit stream: the engine launches on it and the HIP events below
+    # time exactly that stream (a NULL handle would mean the context's stream)
+    torch.cuda.set_stream(torch.cuda.Stream())
+    comm_stream = torch.cuda.Stream()  # the cluster all-reduce overlaps the next interval
+    if world > 1:  # control plane only (unique id, barriers, max over ranks); data path: RCCL
+        dist.init_process_group("gloo")
+
+    from kepler_amd import accel
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+
+    t_setup = time.time()
+    total_nodes = bench_nodes(args.config, world, args.nodes, scaling)
+    split = world * args.shard_of
+    K = max(1, args.intervals)
+    w = Workload(args, total_nodes, split, rank, rank, world, local, K, accel.Cluster.unique_id)
+    stream = current_stream_handle()
+    assert stream != 0
+    layout, sizes, Z = w.layout, w.sizes, w.Z
+    prime_t = to_device(w.prime)
+    w.acc.run_interval(interval_from_tensors(prime_t, sizes), stream)
+    w.acc.sync(stream)
+    del prime_t
+    log(rank, f"[bench] setup {time.time() - t_setup:.1f}s")
+    wall_max, kernel_ms = measure(args, w, rank, world, stream, comm_stream)
+
     # same-box reference for the roofline: a 1.28 GB device-to-device copy
     src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
     dst = torch.empty_like(src)
@@ -515,32 +581,22 @@ def main():
     copy_gbps = 2 * src.numel() * 8 / (float(np.median(cps[1:])) * 1e-3) / 1e9
     del src, dst
 
-    wall_t = torch.tensor([wall], dtype=torch.float64)
     procs_t = torch.tensor([sizes["n_procs"], sizes["n_nodes"]], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(procs_t)
-    wall_max = float(wall_t.item())
     total_procs, total_nodes_done = (float(x) for x in procs_t.tolist())
 
     # roofline numerator per interval: the K-interval one-launch path reads the engine state
     # once and carries it on chip, so its algorithmic bytes are fewer (kacc_intervals_bytes)
-    fused = accel.fused_intervals(layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES, K, args.node_order, Z)
+    fused = accel.fused_intervals(w.flags, K, args.node_order, Z)
     bytes_per_launch = accel.intervals_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"], sizes["n_vms"],
                                              sizes["n_pods"], K, fused) / K
     k_avg_ms = float(np.mean(kernel_ms))
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
 
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        ent = pmc.get(f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else "")
-                      + (f"_k{K}" if fused else ""))
-        if ent and ent.get("n_procs") == sizes["n_procs"]:  # per interval, like `achieved`
-            traffic = ent.get("hbm_bytes_per_interval", ent.get("hbm_bytes_per_launch"))
-
+    traffic, traffic_source = pmc_traffic(args, sizes, K, fused)
+    rccl_version, rccl_path = accel.Cluster.rccl()
+    emulated = args.shard_of > 1
     result = {
         "metric": METRIC,
         "value": total_procs * K * args.steps / wall_max,
@@ -550,15 +606,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall_max * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "strong" if args.config == 4 else "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64+u64",
         "data": "synthetic (kepler_amd/fleet.py, seed 0x4B45504C; inputs resident in HBM)",
         "config": {
-            "workload": f"config{args.config}: {sizes['n_nodes']} nodes x "
-                        f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs, Z={Z} per GPU"
+            "workload": f"config{args.config}: {total_nodes}-node fleet"
+                        + (f" split {split} ways (plan_node_ranges), {sizes['n_nodes']} nodes x "
+                           f"{sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs on this GPU" if split > 1 else
+                           f" x {sizes['n_procs'] // max(sizes['n_nodes'], 1)} procs")
+                        + f", Z={Z}"
                         + (f", {K} intervals per step (kacc_run_intervals)" if K > 1 else "")
-                        + (f", fragmented slots ({args.fragment:g}, node_proc_span)" if args.fragment else ""),
+                        + (f", fragmented slots ({args.fragment:g}, node_proc_span)" if args.fragment else "")
+                        + (f" [EMULATED: rank 0's shard of a {split}-GPU split, run on one GPU]" if emulated else ""),
             "intervals_per_step": K,
             "fleet_nodes": total_nodes,
             "nodes_per_gpu": sizes["n_nodes"],
@@ -567,14 +627,16 @@ def main():
             "vms_per_gpu": sizes["n_vms"],
             "pods_per_gpu": sizes["n_pods"],
             "zones": Z,
-            "namespaces": n_ns,
+            "namespaces": w.n_ns,
             "fragment_slots": args.fragment,
+            "shard_of": args.shard_of,
             "parallelism": f"node-sharded x{world} (shard.plan_node_ranges); namespace + cluster node "
                            f"totals all-reduced over RCCL by kacc_allreduce_namespaces",
         },
         "node_snapshots_per_s": total_nodes_done * K * args.steps / wall_max,
         "kernel_ms": k_avg_ms,
         "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
+        "step_minus_kernel_ms": wall_max * 1e3 / args.steps - k_avg_ms * K,
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -582,26 +644,23 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            "traffic_source": traffic_source,
             "bytes_per_interval": bytes_per_launch,
             "bytes_per_interval_unfused": accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
                                                                sizes["n_vms"], sizes["n_pods"]),
-            "kernel": (f"kacc::intervals_carry_kernel<{Z},0,{256 if layout.fast_flag() & accel.KACC_F_MEDIUM_NODES else 512}>"
-                       f" ({K} intervals in one launch, state carried on chip; "
-                       f"achieved = kacc_intervals_bytes(carried) / K per interval)" if fused else
-                       f"kacc::small_kernel<{Z}> (one launch per step, one wavefront per node: every node "
-                       f"fits KACC_F_SMALL_NODES)" if layout.fast_flag() & accel.KACC_F_SMALL_NODES else
-                       f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, "
-                       f"KACC_F_FAST_NODES)" if layout.fast_flag() else
-                       f"kacc::interval_kernel<{Z},0> + chunk_kernel<{Z},0> + pod_kernel<{Z},0> (big nodes "
-                       f"chunked; HIP events bracket all three launches of the step)"),
+            "kernel": kernel_name(w.flags, K, fused, Z),
             "same_box_copy_GBps": copy_gbps,
             "frac_of_copy": achieved / copy_gbps,
         },
+        "rccl": {"version": rccl_version, "path": rccl_path},
         "cpu_baseline": None,
     }
+    if emulated:
+        result["note"] = (f"one GPU running rank 0's shard of the {split}-way split: the per-GPU step of an "
+                          f"{split}-GPU strong-scaling run without the cross-GPU all-reduce (one-rank communicator)")
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res, cs_ = cpu_baseline(layout, [prime] + full, node_steps, args.cpu_nodes, args.cpu_seconds,
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not emulated:
+        res, cs_ = cpu_baseline(layout, [w.prime] + w.full, w.node_steps, args.cpu_nodes, args.cpu_seconds,
                                 max_runs=args.cpu_runs)
         gf = res["gofaithful"]
         hc = host_cpu()
@@ -626,15 +685,35 @@ def main():
                                            f"{res['soa_mt']['runs']} runs"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
+    w.close()
+    del w
 
-    if world == 1 and args.frag_line > 0 and args.fragment == 0 and args.config in (1, 2, 3):
+    if world > 1 and scaling == "strong" and args.weak_line and args.config in (1, 2, 3, 5):
+        # extra key: every rank a full shard of its own (weak scaling), the same timed loop
+        wk = Workload(args, bench_nodes(args.config, world, args.nodes, "weak"), world, rank, rank, world, local, K,
+                      accel.Cluster.unique_id)
+        prime_t = to_device(wk.prime)
+        wk.acc.run_interval(interval_from_tensors(prime_t, wk.sizes), stream)
+        wk.acc.sync(stream)
+        del prime_t
+        wwall, wkms = measure(args, wk, rank, world, stream, comm_stream)
+        wp = torch.tensor([wk.sizes["n_procs"]], dtype=torch.float64)
+        dist.all_reduce(wp)
+        result["weak_scaling"] = {"value": float(wp.item()) * K * args.steps / wwall, "unit": "proc-attr/s",
+                                  "ms_per_step": wwall * 1e3 / args.steps, "kernel_ms": float(np.mean(wkms)),
+                                  "nodes_per_gpu": wk.sizes["n_nodes"],
+                                  "fleet_nodes": bench_nodes(args.config, world, args.nodes, "weak")}
+        wk.close()
+        del wk
+
+    if world == 1 and args.frag_line > 0 and args.fragment == 0 and args.config in (1, 2, 3) and not emulated:
         try:
             result["slot_layouts"] = slot_layout_lines(args, args.frag_line, K, min(args.steps, 10),
                                                        bytes_per_launch)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["slot_layouts"] = {"error": repr(e)}
 
-    if world == 1 and args.pipeline_line and args.fragment == 0 and args.config == 3 and K == 1:
+    if world == 1 and args.pipeline_line and args.fragment == 0 and args.config == 3 and K == 1 and not emulated:
         try:
             result["pipeline"] = pipeline_line(args)
         except Exception as e:  # a secondary line: report, never lose the headline
@@ -646,10 +725,55 @@ def main():
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
-    cluster.close()
-    acc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def kernel_name(flags, K, fused, Z):
+    from kepler_amd import accel
+
+    if fused:
+        return (f"kacc::intervals_carry_kernel<{Z},0,{256 if flags & accel.KACC_F_MEDIUM_NODES else 512}>"
+                f" ({K} intervals in one launch, state carried on chip; "
+                f"achieved = kacc_intervals_bytes(carried) / K per interval)")
+    if flags & accel.KACC_F_SMALL_NODES:
+        return (f"kacc::small_kernel<{Z}> (one launch per step, one wavefront per node: every node "
+                f"fits KACC_F_SMALL_NODES)")
+    if flags & accel.KACC_F_FAST_NODES:
+        return f"kacc::interval_kernel<{Z},0> (one launch per step: every node fits the fast path, KACC_F_FAST_NODES)"
+    return (f"kacc::interval_kernel<{Z},0> + chunk_kernel<{Z},0> + pod_kernel<{Z},0> (big nodes "
+            f"chunked; HIP events bracket all three launches of the step)")
+
+
+def lib_sha256():
+    import hashlib
+
+    from kepler_amd import accel
+
+    with open(accel.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(args, sizes, K, fused):
+    """roofline.traffic: HBM bytes per interval from profiles/pmc_traffic.json (rocprofv3 --pmc
+    FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_summary.py) ONLY when that entry was measured on this
+    very build (sha256 of libkepler_accel.so) and these sizes; otherwise null, with the reason."""
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    key = (f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else "")
+           + (f"_k{K}" if fused else ""))
+    if not os.path.exists(pmc_path):
+        return None, "no profiles/pmc_traffic.json"
+    with open(pmc_path) as f:
+        ent = json.load(f).get(key)
+    if not ent:
+        return None, f"no PMC entry {key}"
+    if ent.get("n_procs") != sizes["n_procs"]:
+        return None, f"PMC entry {key} is for {ent.get('n_procs')} procs, not {sizes['n_procs']}"
+    sha = lib_sha256()
+    if ent.get("lib_sha256") != sha:
+        return None, (f"PMC entry {key} was measured on build {str(ent.get('lib_sha256'))[:16]}, not this build "
+                      f"{sha[:16]}: no counters of this build")
+    return ent.get("hbm_bytes_per_interval", ent.get("hbm_bytes_per_launch")), ent.get("source")
 
 
 if __name__ == "__main__":

@@ -321,7 +321,9 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *ns_pod_o
  *   - cluster node totals per zone (monitor/types.go:27-40):
  *     node energy u64 [2*Z] = { Σ ActiveEnergyTotal[z] }, { Σ IdleEnergyTotal[z] }
  *     node power  f64 [3*Z] = { Σ Power[z] }, { Σ ActivePower[z] }, { Σ IdlePower[z] }
- *     over every node of each shard's node table;
+ *     over nodes [0, n_nodes) of the last interval run on each shard (a node
+ *     that left the batch stops exporting, so PromQL's sum no longer counts
+ *     it; a context with no interval run yet contributes zeros);
  *   - the pods themselves (a pod lives on one node: a gather, not a sum).
  * RCCL ranks are GPUs.  A process may hold several shards of one GPU (their
  * partial vectors are added on that GPU in shard order before the collective)
@@ -346,6 +348,15 @@ int kacc_cluster_unique_id(uint8_t id[KACC_UNIQUE_ID_BYTES]);
 int kacc_cluster_join(kacc_ctx *ctx, const uint8_t id[KACC_UNIQUE_ID_BYTES], int nranks, int rank,
                       kacc_cluster **out);
 void kacc_cluster_destroy(kacc_cluster *c);
+/* The RCCL the library runs its collectives with.  RCCL is loaded on first
+ * use (dlopen, not a link-time dependency): the copy the process already
+ * holds under the soname librccl.so.1 (e.g. a framework's), else the first one
+ * on the search path (/opt/rocm/lib), or the file named by KACC_RCCL_PATH.  A
+ * major version other than the headers' the library was built with (NCCL_MAJOR
+ * 2) is refused.  version: ncclGetVersion(); path: the loaded file (len bytes
+ * incl. the NUL, truncated).  KACC_EHIP (message via kacc_last_error(NULL))
+ * when no usable RCCL is found; the cluster entry points then fail the same. */
+int kacc_cluster_rccl(int *version, char *path, size_t len);
 /* nranks: GPUs in the cluster; rank: this process's first GPU; n_shards: local shards. */
 int kacc_cluster_info(const kacc_cluster *c, int *nranks, int *rank, int *n_shards);
 /* Cluster namespace totals (and, when out_node_* are non-NULL, cluster node
@@ -403,7 +414,9 @@ int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *co
  * uint64_t IDs (the packer's 64-bit IDs of the container / VM / pod ID
  * strings; the two top values reserved).  Errors (duplicate ID in a node, a
  * reserved key, more live IDs than the node's range) are raised as
- * KACC_ERANGE at kacc_sync; the affected rows get slot word 0xffffffff.      */
+ * KACC_ERANGE at kacc_sync; the affected rows get slot word 0xffffffff (of
+ * two rows carrying one ID, which one keeps a slot is unspecified: the whole
+ * call is reported as failed).                                               */
 typedef enum kacc_kind {
   KACC_KIND_PROC = 0, /* key: uint32_t PID — process.go:120 StringID        */
   KACC_KIND_CTR = 1,  /* key: uint64_t ID of the container ID string        */
@@ -473,7 +486,8 @@ typedef struct kacc_records {
   const uint64_t *ctr_key;   /* [R] key of Process.Container.ID (type CONTAINER)             */
   const uint64_t *vm_key;    /* [R] key of Process.VirtualMachine.ID (type VM)               */
   const uint64_t *pod_key;   /* [R] key of the container's Pod.ID per LookupByContainerID
-                                    (pod.go:209-239), KACC_KEY_EMPTY = not found; or NULL     */
+                                    (pod.go:209-239), KACC_KEY_EMPTY = not found (the container
+                                    goes to ContainersNoPod), KACC_KEY_TOMB rejected; or NULL */
   const uint32_t *pod_ns;    /* [R] the pod's namespace index (namespace totals); or NULL    */
 } kacc_records;
 typedef struct kacc_packed {
@@ -523,12 +537,14 @@ int kacc_unpack(kacc_ctx *ctx, kacc_kind kind, uint32_t n, const uint32_t *slot_
  * the boundary keep items already tracked first (Go's heap requires a strictly
  * higher energy to evict), then the batch order.  Tracked items are frozen
  * copies (energy and power per zone), as Add(prev.Clone()) keeps.  Nodes are
- * those of the context (kacc_config.nodes): the device holds nodes x max_size
- * items (x capacity for an unlimited tracker).                              */
+ * those of the context (kacc_config.nodes): the device holds, PER NODE,
+ * max_size items (capacity for an unlimited tracker), i.e.
+ * kacc_config.nodes x items x (8 + 16Z) bytes — 10k nodes x 500 x Z=4 is
+ * 360 MB; KACC_ENOMEM, with that figure in the message, when it does not fit. */
 typedef struct kacc_tracker kacc_tracker;
 #define KACC_TRACKER_MAX_BOUNDED 8192u /* largest max_size > 0 supported */
 /* max_size: > 0 top-N per node (<= KACC_TRACKER_MAX_BOUNDED), 0 disabled,
- * < 0 unlimited (at most `capacity` items per node, more raise ERANGE).
+ * < 0 unlimited (at most `capacity` items PER NODE, more raise ERANGE).
  * zone: target zone index in the kind's [slot*Z + z] tables.  min_energy:
  * minEnergyThreshold in µJ.                                                 */
 int kacc_tracker_create(kacc_ctx *ctx, kacc_kind kind, int64_t max_size, uint32_t capacity,

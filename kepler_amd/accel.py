@@ -125,6 +125,7 @@ EXPORTS = [
     "kacc_cluster_unique_id",
     "kacc_cluster_join",
     "kacc_cluster_destroy",
+    "kacc_cluster_rccl",
     "kacc_cluster_info",
     "kacc_allreduce_namespaces",
     "kacc_gather_pods",
@@ -274,6 +275,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_cluster_destroy.argtypes = [c_void_p]
     lib.kacc_cluster_destroy.restype = None
     lib.kacc_cluster_info.argtypes = [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]
+    lib.kacc_cluster_rccl.argtypes = [POINTER(c_int), c_char_p, ctypes.c_size_t]
     lib.kacc_allreduce_namespaces.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 8
     lib.kacc_gather_pods.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_void_p), c_uint64, POINTER(c_void_p),
                                      POINTER(c_void_p), POINTER(c_uint64), POINTER(c_uint64), POINTER(c_void_p)]
@@ -818,6 +820,18 @@ class Cluster:
         if rc != KACC_OK:
             raise AccelError(rc, last_error(None))
         return buf.raw
+
+    @staticmethod
+    def rccl():
+        """kacc_cluster_rccl: (ncclGetVersion(), path of the loaded librccl) the library's
+        collectives run with (raises AccelError when no usable RCCL is found)."""
+        lib = load()
+        v = c_int(0)
+        buf = ctypes.create_string_buffer(4096)
+        rc = lib.kacc_cluster_rccl(ctypes.byref(v), buf, len(buf))
+        if rc != KACC_OK:
+            raise AccelError(rc, last_error(None))
+        return v.value, buf.value.decode()
 
     @classmethod
     def join(cls, accel: Accel, uid: bytes, nranks: int, rank: int) -> "Cluster":

@@ -20,15 +20,98 @@
 // one shard per process (ncclCommInitRank, the one-process-per-GPU launch).
 // Every collective is enqueued on the shard's stream: nothing here blocks the
 // host except kacc_gather_pods' count exchange.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "kacc_internal.hpp"
+
+// RCCL is loaded on first use (dlopen), not linked: single-GPU users of the
+// library (and the C99 ABI client) need no librccl at load time.  The library
+// binds the RCCL that the process already holds under the soname librccl.so.1
+// (e.g. torch's), else the first on the search path (the build's RUNPATH,
+// /opt/rocm/lib); KACC_RCCL_PATH names another file.  The version is read with
+// ncclGetVersion and a major version other than the headers' (NCCL_MAJOR) is
+// refused; kacc_cluster_rccl() reports the version and the file in use.
+namespace {
+struct Rccl {
+  bool ok = false;
+  std::string err;
+  int version = 0;
+  std::string path;
+  decltype(&ncclGetVersion) GetVersion = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclAllReduce) AllReduce = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclBroadcast) Broadcast = nullptr;
+};
+
+const Rccl &rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char *env = std::getenv("KACC_RCCL_PATH");
+    const char *names[] = {env && *env ? env : "librccl.so.1", "librccl.so"};
+    void *h = nullptr;
+    for (const char *n : names)
+      if ((h = dlopen(n, RTLD_NOW | RTLD_LOCAL)) != nullptr) break;
+    if (!h) {
+      const char *e = dlerror();
+      r.err = std::string("dlopen(librccl.so.1): ") + (e ? e : "not found");
+      return;
+    }
+    bool all = true;
+    auto sym = [&](auto &fn, const char *name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn) {
+        all = false;
+        r.err += std::string(r.err.empty() ? "" : ", ") + "missing " + name;
+      }
+    };
+    sym(r.GetVersion, "ncclGetVersion");
+    sym(r.GetErrorString, "ncclGetErrorString");
+    sym(r.GetUniqueId, "ncclGetUniqueId");
+    sym(r.CommInitRank, "ncclCommInitRank");
+    sym(r.CommInitAll, "ncclCommInitAll");
+    sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.GroupStart, "ncclGroupStart");
+    sym(r.GroupEnd, "ncclGroupEnd");
+    sym(r.AllReduce, "ncclAllReduce");
+    sym(r.AllGather, "ncclAllGather");
+    sym(r.Broadcast, "ncclBroadcast");
+    if (!all) return;
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void *>(r.GetVersion), &info) && info.dli_fname) r.path = info.dli_fname;
+    if (r.GetVersion(&r.version) != ncclSuccess) {
+      r.err = "ncclGetVersion failed";
+      return;
+    }
+    // NCCL_VERSION(X,Y,Z) = X*10000 + Y*100 + Z since 2.9 (X*1000 + Y*100 + Z before)
+    const int major = r.version >= 10000 ? r.version / 10000 : r.version / 1000;
+    if (major != NCCL_MAJOR) {
+      r.err = "RCCL " + std::to_string(r.version) + " at " + r.path + ": major version " + std::to_string(major) +
+              " != " + std::to_string(NCCL_MAJOR) + " of the headers this library was built with";
+      return;
+    }
+    r.ok = true;
+  });
+  return r;
+}
+}  // namespace
 
 namespace kacc {
 namespace cluster {
@@ -88,7 +171,7 @@ struct kacc_cluster {
 namespace {
 
 int nccl_fail(kacc_ctx *ctx, ncclResult_t r, const char *what) {
-  return kacc_fail(ctx, KACC_EHIP, "%s: %s", what, ncclGetErrorString(r));
+  return kacc_fail(ctx, KACC_EHIP, "%s: %s", what, rccl().GetErrorString(r));
 }
 
 #define KACC_NCCL(ctx, call)                                  \
@@ -191,31 +274,47 @@ int local_broadcast(kacc_cluster *c, void *const *streams, uint64_t *const *e, u
   return KACC_OK;
 }
 
-// One in-place all-reduce (sum) of e [n_e] u64 and p [n_p] f64 per local GPU.
-int allreduce(kacc_cluster *c, void *const *streams, uint64_t *const *e, uint64_t n_e, double *const *p,
-              uint64_t n_p) {
+// In-place all-reduces (sum) of the vectors of `reqs` (u64 e [n_e], f64 p
+// [n_p] of each local GPU's first shard) as ONE RCCL group: one launch of
+// RCCL's kernels per step however many vectors cross the GPUs.
+struct ReduceReq {
+  uint64_t *const *e;
+  uint64_t n_e;
+  double *const *p;
+  uint64_t n_p;
+};
+int allreduce(kacc_cluster *c, void *const *streams, const ReduceReq *reqs, int n_reqs) {
   kacc_ctx *c0 = c->shards[0];
-  KACC_NCCL(c0, ncclGroupStart());
-  for (size_t d = 0; d < c->dev_first.size(); ++d) {
-    const int f = c->dev_first[d];
-    hipStream_t sf = shard_stream(c, streams, f);
-    if (n_e) {
-      const ncclResult_t r = ncclAllReduce(e[f], e[f], n_e, ncclUint64, ncclSum, c->comms[d], sf);
-      if (r != ncclSuccess) {
-        (void)ncclGroupEnd();
-        return nccl_fail(c0, r, "ncclAllReduce(u64)");
+  KACC_NCCL(c0, rccl().GroupStart());
+  for (int q = 0; q < n_reqs; ++q) {
+    const ReduceReq &rq = reqs[q];
+    for (size_t d = 0; d < c->dev_first.size(); ++d) {
+      const int f = c->dev_first[d];
+      hipStream_t sf = shard_stream(c, streams, f);
+      if (rq.n_e) {
+        const ncclResult_t r = rccl().AllReduce(rq.e[f], rq.e[f], rq.n_e, ncclUint64, ncclSum, c->comms[d], sf);
+        if (r != ncclSuccess) {
+          (void)rccl().GroupEnd();
+          return nccl_fail(c0, r, "ncclAllReduce(u64)");
+        }
       }
-    }
-    if (n_p) {
-      const ncclResult_t r = ncclAllReduce(p[f], p[f], n_p, ncclFloat64, ncclSum, c->comms[d], sf);
-      if (r != ncclSuccess) {
-        (void)ncclGroupEnd();
-        return nccl_fail(c0, r, "ncclAllReduce(f64)");
+      if (rq.n_p) {
+        const ncclResult_t r = rccl().AllReduce(rq.p[f], rq.p[f], rq.n_p, ncclFloat64, ncclSum, c->comms[d], sf);
+        if (r != ncclSuccess) {
+          (void)rccl().GroupEnd();
+          return nccl_fail(c0, r, "ncclAllReduce(f64)");
+        }
       }
     }
   }
-  KACC_NCCL(c0, ncclGroupEnd());
+  KACC_NCCL(c0, rccl().GroupEnd());
   return KACC_OK;
+}
+
+// RCCL loaded and usable, else the loader's message on ctx (or the create error).
+int need_rccl(kacc_ctx *ctx) {
+  const Rccl &r = rccl();
+  return r.ok ? KACC_OK : kacc_fail(ctx, KACC_EHIP, "RCCL unavailable: %s", r.err.c_str());
 }
 
 }  // namespace
@@ -232,6 +331,7 @@ int kacc_create_multi(const int *devices, int n, const kacc_config *cfgs, kacc_c
       if (devices[j] == devices[i] && devices[i - 1] != devices[i])
         return kacc_fail(nullptr, KACC_EINVAL, "shards of device %d are not contiguous", devices[i]);
   }
+  if (need_rccl(nullptr) != KACC_OK) return KACC_EHIP;
   auto *c = new kacc_cluster;
   c->owns_shards = true;
   c->zones = cfgs[0].zones;
@@ -255,12 +355,12 @@ int kacc_create_multi(const int *devices, int n, const kacc_config *cfgs, kacc_c
   c->nranks = static_cast<int>(devlist.size());
   c->rank0 = 0;
   c->comms.assign(devlist.size(), nullptr);
-  const ncclResult_t r = ncclCommInitAll(c->comms.data(), c->nranks, devlist.data());
+  const ncclResult_t r = rccl().CommInitAll(c->comms.data(), c->nranks, devlist.data());
   if (r != ncclSuccess) {
     c->comms.clear();
     kacc_cluster_destroy(c);
     return kacc_fail(nullptr, KACC_EHIP, "ncclCommInitAll over %d GPUs: %s", static_cast<int>(devlist.size()),
-                     ncclGetErrorString(r));
+                     rccl().GetErrorString(r));
   }
   if (cluster_scratch(c) != KACC_OK) {
     const std::string why = c->shards[0]->err;
@@ -275,9 +375,10 @@ int kacc_create_multi(const int *devices, int n, const kacc_config *cfgs, kacc_c
 int kacc_cluster_unique_id(uint8_t id[KACC_UNIQUE_ID_BYTES]) {
   if (!id) return kacc_fail(nullptr, KACC_EINVAL, "NULL argument");
   static_assert(sizeof(ncclUniqueId) == KACC_UNIQUE_ID_BYTES, "unique id size");
+  if (need_rccl(nullptr) != KACC_OK) return KACC_EHIP;
   ncclUniqueId u;
-  const ncclResult_t r = ncclGetUniqueId(&u);
-  if (r != ncclSuccess) return kacc_fail(nullptr, KACC_EHIP, "ncclGetUniqueId: %s", ncclGetErrorString(r));
+  const ncclResult_t r = rccl().GetUniqueId(&u);
+  if (r != ncclSuccess) return kacc_fail(nullptr, KACC_EHIP, "ncclGetUniqueId: %s", rccl().GetErrorString(r));
   std::memcpy(id, &u, sizeof(u));
   return KACC_OK;
 }
@@ -289,6 +390,7 @@ int kacc_cluster_join(kacc_ctx *ctx, const uint8_t id[KACC_UNIQUE_ID_BYTES], int
   if (nranks <= 0 || rank < 0 || rank >= nranks)
     return kacc_fail(ctx, KACC_EINVAL, "rank %d of %d", rank, nranks);
   KACC_HIP(ctx, hipSetDevice(ctx->device));
+  if (need_rccl(ctx) != KACC_OK) return KACC_EHIP;
   auto *c = new kacc_cluster;
   c->owns_shards = false;
   c->zones = ctx->cfg.zones;
@@ -300,11 +402,11 @@ int kacc_cluster_join(kacc_ctx *ctx, const uint8_t id[KACC_UNIQUE_ID_BYTES], int
   c->comms.assign(1, nullptr);
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
-  const ncclResult_t r = ncclCommInitRank(&c->comms[0], nranks, u, rank);
+  const ncclResult_t r = rccl().CommInitRank(&c->comms[0], nranks, u, rank);
   if (r != ncclSuccess) {
     c->comms.clear();
     kacc_cluster_destroy(c);
-    return kacc_fail(ctx, KACC_EHIP, "ncclCommInitRank(%d of %d): %s", rank, nranks, ncclGetErrorString(r));
+    return kacc_fail(ctx, KACC_EHIP, "ncclCommInitRank(%d of %d): %s", rank, nranks, rccl().GetErrorString(r));
   }
   const int rc = cluster_scratch(c);
   if (rc != KACC_OK) {
@@ -321,7 +423,7 @@ void kacc_cluster_destroy(kacc_cluster *c) {
     if (!c->comms[d]) continue;
     (void)hipSetDevice(c->shards[c->dev_first[d]]->device);
     (void)hipDeviceSynchronize();
-    (void)ncclCommDestroy(c->comms[d]);
+    if (rccl().CommDestroy) (void)rccl().CommDestroy(c->comms[d]);
   }
   for (size_t d = 0; d < c->d_count.size(); ++d)
     if (c->d_count[d]) {
@@ -336,6 +438,17 @@ void kacc_cluster_destroy(kacc_cluster *c) {
   if (c->owns_shards)
     for (kacc_ctx *x : c->shards) kacc_destroy(x);
   delete c;
+}
+
+int kacc_cluster_rccl(int *version, char *path, size_t len) {
+  const Rccl &r = rccl();
+  if (version) *version = r.version;
+  if (path && len) {
+    const size_t n = std::min(len - 1, r.path.size());
+    std::memcpy(path, r.path.data(), n);
+    path[n] = '\0';
+  }
+  return r.ok ? KACC_OK : kacc_fail(nullptr, KACC_EHIP, "RCCL unavailable: %s", r.err.c_str());
 }
 
 int kacc_cluster_info(const kacc_cluster *c, int *nranks, int *rank, int *n_shards) {
@@ -394,9 +507,12 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
       KACC_HIP(c0, hipEventRecord(c->events[s], a));
       KACC_HIP(c0, hipStreamWaitEvent(b, c->events[s], 0));
     }
-  // 3. across GPUs (RCCL), 4. back to every shard
-  if (n_ns && (rc = allreduce(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
-  if (nodes && (rc = allreduce(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
+  // 3. across GPUs (RCCL: every vector in one group), 4. back to every shard
+  ReduceReq reqs[2];
+  int n_reqs = 0;
+  if (n_ns) reqs[n_reqs++] = ReduceReq{out_energy, n_ns * Z, out_power, n_ns * Z};
+  if (nodes) reqs[n_reqs++] = ReduceReq{out_node_energy, 2 * Z, out_node_power, 3 * Z};
+  if (n_reqs && (rc = allreduce(c, cs, reqs, n_reqs)) != KACC_OK) return rc;
   if (n_ns && (rc = local_broadcast(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
   if (nodes && (rc = local_broadcast(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK)
     return rc;
@@ -420,16 +536,16 @@ int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *co
     KACC_HIP(c0, hipMemcpyAsync(c->d_count[d], &local[d], 8, hipMemcpyHostToDevice,
                                 shard_stream(c, streams, c->dev_first[d])));
   }
-  KACC_NCCL(c0, ncclGroupStart());
+  KACC_NCCL(c0, rccl().GroupStart());
   for (size_t d = 0; d < nd; ++d) {
-    const ncclResult_t r = ncclAllGather(c->d_count[d], c->d_count[d] + 1, 1, ncclUint64, c->comms[d],
+    const ncclResult_t r = rccl().AllGather(c->d_count[d], c->d_count[d] + 1, 1, ncclUint64, c->comms[d],
                                          shard_stream(c, streams, c->dev_first[d]));
     if (r != ncclSuccess) {
-      (void)ncclGroupEnd();
+      (void)rccl().GroupEnd();
       return nccl_fail(c0, r, "ncclAllGather(counts)");
     }
   }
-  KACC_NCCL(c0, ncclGroupEnd());
+  KACC_NCCL(c0, rccl().GroupEnd());
   std::vector<uint64_t> counts(c->nranks, 0);
   {
     const int f = c->dev_first[0];
@@ -467,7 +583,7 @@ int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *co
     }
   }
   // 3. all-gather-v: one in-place broadcast per rank, its exact block
-  KACC_NCCL(c0, ncclGroupStart());
+  KACC_NCCL(c0, rccl().GroupStart());
   for (int r = 0; r < c->nranks; ++r) {
     if (!counts[r]) continue;
     for (size_t d = 0; d < nd; ++d) {
@@ -475,15 +591,15 @@ int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *co
       hipStream_t sf = shard_stream(c, streams, f);
       uint64_t *e = out_energy[f] + off[r] * Z;
       double *p = out_power[f] + off[r] * Z;
-      ncclResult_t rr = ncclBroadcast(e, e, counts[r] * Z, ncclUint64, r, c->comms[d], sf);
-      if (rr == ncclSuccess) rr = ncclBroadcast(p, p, counts[r] * Z, ncclFloat64, r, c->comms[d], sf);
+      ncclResult_t rr = rccl().Broadcast(e, e, counts[r] * Z, ncclUint64, r, c->comms[d], sf);
+      if (rr == ncclSuccess) rr = rccl().Broadcast(p, p, counts[r] * Z, ncclFloat64, r, c->comms[d], sf);
       if (rr != ncclSuccess) {
-        (void)ncclGroupEnd();
+        (void)rccl().GroupEnd();
         return nccl_fail(c0, rr, "ncclBroadcast(pods)");
       }
     }
   }
-  KACC_NCCL(c0, ncclGroupEnd());
+  KACC_NCCL(c0, rccl().GroupEnd());
   return local_broadcast(c, streams, out_energy, off[c->nranks] * Z, out_power, off[c->nranks] * Z);
 }
 

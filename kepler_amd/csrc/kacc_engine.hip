@@ -3158,6 +3158,7 @@ int kacc_reset(kacc_ctx *ctx) {
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->live_nodes = 0;
   return KACC_OK;
 }
 
@@ -3171,6 +3172,7 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   (void)hipGetLastError();  // clear a stale error of an earlier call
   launch(ctx->cfg.zones, *b, dev_state(ctx), st);
   KACC_HIP(ctx, hipGetLastError());
+  ctx->live_nodes = b->n_nodes;
   return KACC_OK;
 }
 
@@ -3209,11 +3211,13 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
     launch_intervals(ctx->cfg.zones, all_medium(dev_batches, count), ctx->d_batches, count, dev_batches[0].n_nodes,
                      ds, st);
     KACC_HIP(ctx, hipGetLastError());
+    ctx->live_nodes = dev_batches[count - 1].n_nodes;
     return KACC_OK;
   }
   for (uint32_t k = 0; k < count; ++k)
     if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
   KACC_HIP(ctx, hipGetLastError());
+  if (count) ctx->live_nodes = dev_batches[count - 1].n_nodes;
   return KACC_OK;
 }
 
@@ -3469,6 +3473,7 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   KACC_HIP(ctx, hipMemcpyAsync(bt->h_err, ctx->d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
   KACC_HIP(ctx, hipEventRecord(bt->done, ctx->stream));
   bt->submitted = true;
+  ctx->live_nodes = bt->host[K - 1].n_nodes;
   return KACC_OK;
 }
 
@@ -3571,11 +3576,15 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint64_t Z = ctx->cfg.zones;
+  // the nodes of the last interval run on the context (a node that left the
+  // batch stops exporting, so PromQL's sum drops it; a fresh context sums none)
+  const uint64_t live = std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
   // at most kNodeBlocksMax blocks of a multiple of kBlock nodes each
-  const uint64_t groups = (ctx->cfg.nodes + kacc::kBlock - 1) / kacc::kBlock;
-  const uint32_t npb = static_cast<uint32_t>(kacc::kBlock * ((groups + kacc::kNodeBlocksMax - 1) / kacc::kNodeBlocksMax));
-  const uint32_t node_blocks =
-      node_energy && ctx->cfg.nodes ? static_cast<uint32_t>((ctx->cfg.nodes + npb - 1) / npb) : 0u;
+  const uint64_t groups = (live + kacc::kBlock - 1) / kacc::kBlock;
+  const uint32_t npb = static_cast<uint32_t>(
+      kacc::kBlock * std::max<uint64_t>(1, (groups + kacc::kNodeBlocksMax - 1) / kacc::kNodeBlocksMax));
+  // no live node: one block that writes zero totals
+  const uint32_t node_blocks = node_energy ? std::max<uint32_t>(1, static_cast<uint32_t>((live + npb - 1) / npb)) : 0u;
   if (node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
     KACC_HIP(ctx, hipStreamSynchronize(st));
     if (ctx->d_node_part) KACC_HIP(ctx, hipFree(ctx->d_node_part));
@@ -3586,7 +3595,7 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
     ctx->node_part_cap = node_blocks;
   }
   kacc::NodeTotalsArgs na{};
-  na.n_nodes = ctx->cfg.nodes;
+  na.n_nodes = live;
   na.npb = npb;
   na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
   na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];

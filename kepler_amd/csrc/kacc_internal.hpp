@@ -34,6 +34,7 @@ struct kacc_ctx {
   kacc_interval *h_batches = nullptr;  //   and their pinned staging copy
   uint32_t batch_cap = 0;
   hipEvent_t batch_copied = nullptr;
+  uint32_t live_nodes = 0;  // n_nodes of the last interval run: the nodes the cluster totals sum
   std::string err;
 };
 

@@ -116,6 +116,8 @@ int pack_node(const kacc_records &in, uint32_t n, Scratch &s, Counts *cnt, kacc_
     if (t == KACC_PROC_CONTAINER) {
       const uint64_t k = in.ctr_key[r];
       if (k >= KACC_KEY_TOMB) return -1;
+      // KACC_KEY_EMPTY = the pod lookup found none (ContainersNoPod); the other reserved key is an error
+      if (in.pod_key && in.pod_key[r] == KACC_KEY_TOMB) return -1;
       const uint32_t i = s.cmap.get(k, static_cast<uint32_t>(s.ctrs.size()), &added);
       if (added)
         s.ctrs.push_back(Agg{k, in.pod_key ? in.pod_key[r] : KACC_KEY_EMPTY, in.pod_ns ? in.pod_ns[r] : 0u, 0,
@@ -138,7 +140,7 @@ int pack_node(const kacc_records &in, uint32_t n, Scratch &s, Counts *cnt, kacc_
   // pods in the order of their containers' first appearance (informer.go:284-310)
   s.pmap.reset(s.ctrs.size());
   for (Agg &c : s.ctrs) {
-    if (c.pod >= KACC_KEY_TOMB) continue;  // ContainersNoPod (KACC_KEY_EMPTY), or a reserved key
+    if (c.pod == KACC_KEY_EMPTY) continue;  // ContainersNoPod
     bool added = false;
     const uint32_t q = s.pmap.get(c.pod, static_cast<uint32_t>(s.pods.size()), &added);
     if (added) s.pods.push_back(Agg{c.pod, 0, c.ns, 0, 0, 0, 0});
@@ -282,7 +284,7 @@ int kacc_pack(const kacc_records *in, kacc_packed *out, uint32_t threads) {
     }
   });
   if (bad == -1)
-    return kacc_fail(nullptr, KACC_EINVAL, "kacc_pack: node %u: a container / VM key is a reserved value",
+    return kacc_fail(nullptr, KACC_EINVAL, "kacc_pack: node %u: a container / VM key, or a pod key other than KACC_KEY_EMPTY, is a reserved value",
                      bad_node.load());
   if (bad == -2) return kacc_fail(nullptr, KACC_EINVAL, "kacc_pack: node %u: unknown process type", bad_node.load());
   // offsets

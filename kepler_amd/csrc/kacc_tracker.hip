@@ -336,6 +336,18 @@ int kacc_tracker_create(kacc_ctx *ctx, kacc_kind kind, int64_t max_size, uint32_
   t->nodes = static_cast<uint32_t>(std::max<uint64_t>(ctx->cfg.nodes, 1));
   t->min_e = min_energy;
   const size_t items = static_cast<size_t>(t->nodes) * t->cap, Z = t->Z;
+  // nodes x per-node items x (key 8 + energy 8Z + power 8Z): refuse before the
+  // allocation when it cannot fit (e.g. an unlimited tracker with a large
+  // per-node capacity over a big fleet), with the cost in the message
+  const size_t need = items * (8 + 16 * Z) + 4ull * t->nodes;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && need > free_b) {
+    const uint32_t nodes = t->nodes, per = t->cap;
+    delete t;
+    return kacc_fail(ctx, KACC_ENOMEM,
+                     "tracker needs %zu B = %u nodes x %u items per node x %zu B, %zu B of device memory free",
+                     need, nodes, per, static_cast<size_t>(8 + 16 * Z), free_b);
+  }
   hipError_t e = hipSuccess;
   auto A = [&](void **p, size_t bytes) {
     if (e == hipSuccess) e = hipMalloc(p, std::max<size_t>(bytes, 8));

@@ -264,21 +264,24 @@ def layout_from_sizes(zones: int, nodes, seed: int = SEED, shuffle_slots: bool =
 
 
 def config_layout(config: int, seed: int = SEED, nodes: Optional[int] = None,
-                  fragment_slots: float = 0.0, fragment_sorted: bool = False) -> FleetLayout:
+                  fragment_slots: float = 0.0, fragment_sorted: bool = False,
+                  n_namespaces: Optional[int] = None) -> FleetLayout:
     """Layouts of BASELINE.json configs (2: 1k×1k Z=2, 3: 10k×2k Z=4, 5: skewed).
 
     ``fragment_slots`` > 0 places each node's processes on a random subset of
-    its own slot range (the slot join's steady state under churn)."""
+    its own slot range (the slot join's steady state under churn).
+    ``n_namespaces``: the fleet's namespace count (default: one per node; a
+    shard of a bigger fleet passes the whole fleet's, config_shard)."""
     if config == 1:  # single node, 500 procs -> 50 containers -> 20 pods, package+dram
         # (``nodes``: a fleet of such nodes — the small-node kernel's workload)
         return make_layout(nodes or 1, 500, 2, seed, ctr_frac=0.8, procs_per_ctr=8, ctrs_per_pod=2.5,
-                           pod_frac=1.0, n_namespaces=4 if not nodes else None,
+                           pod_frac=1.0, n_namespaces=n_namespaces or (4 if not nodes else None),
                            fragment_slots=fragment_slots)
     if config == 2:
-        return make_layout(nodes or 1000, 1000, 2, seed, fragment_slots=fragment_slots)
+        return make_layout(nodes or 1000, 1000, 2, seed, fragment_slots=fragment_slots, n_namespaces=n_namespaces)
     if config in (3, 4):
         return make_layout(nodes or 10000, 2000, 4, seed, fragment_slots=fragment_slots,
-                           fragment_sorted=fragment_sorted)
+                           fragment_sorted=fragment_sorted, n_namespaces=n_namespaces)
     if config == 5:
         p = config_procs_per_node(5, nodes or 1000, seed)
         return make_layout(len(p), p, 4, seed, procs_per_vm=2, vm_frac=0.02)
@@ -308,10 +311,13 @@ def config_shard(config: int, world: int, rank: int, nodes: int, seed: int = SEE
     b = plan_node_ranges(config_procs_per_node(config, nodes, seed), world)
     lo, hi = int(b[rank]), int(b[rank + 1])
     s = seed + lo
+    # every shard indexes the whole fleet's namespaces (one per node, as an unsharded fleet)
     if config == 5:
         p = config_procs_per_node(5, nodes, seed)[lo:hi]
-        return lo, hi, make_layout(hi - lo, p, 4, s, procs_per_vm=2, vm_frac=0.02, fragment_slots=fragment_slots)
-    return lo, hi, config_layout(config, seed=s, nodes=hi - lo, fragment_slots=fragment_slots)
+        return lo, hi, make_layout(hi - lo, p, 4, s, procs_per_vm=2, vm_frac=0.02, fragment_slots=fragment_slots,
+                                   n_namespaces=max(nodes, 1))
+    return lo, hi, config_layout(config, seed=s, nodes=hi - lo, fragment_slots=fragment_slots,
+                                 n_namespaces=max(nodes, 1))
 
 
 @dataclass

@@ -36,6 +36,17 @@ def test_exports_every_declared_symbol(lib):
     assert set(decl) <= exported
 
 
+def test_rccl_is_loaded_lazily_and_reported(lib):
+    """RCCL is not a link-time dependency (single-GPU users and the C client need no
+    librccl); kacc_cluster_rccl names the RCCL the collectives would run with."""
+    out = subprocess.run(["readelf", "-d", accel.LIB_PATH], capture_output=True, text=True).stdout
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out)
+    assert needed and not any("rccl" in n for n in needed), needed
+    version, path = accel.Cluster.rccl()
+    assert version // 10000 == 2, version  # NCCL_MAJOR of the headers the library was built with
+    assert os.path.exists(path), path
+
+
 def test_abi_version(lib):
     assert lib.kacc_abi_version() == accel.KACC_ABI_VERSION
 

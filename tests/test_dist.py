@@ -77,6 +77,7 @@ def _bench_worker(rank, world, port, out_dir):
     for config in (3, 4, 5):
         total = bench.bench_nodes(config, world, nodes=60 if config != 4 else 90)
         lo, hi, L = fleet.config_shard(config, world, rank, total)
+        assert L.n_namespaces == total  # every shard indexes the whole fleet's namespaces
         res[config] = (lo, hi, L.n_nodes, L.n_procs, total)
     np.save(os.path.join(out_dir, f"r{rank}.npy"), np.array([uid == bytes(range(128))] +
                                                             [x for c in (3, 4, 5) for x in res[c]], dtype=np.int64))
@@ -101,5 +102,8 @@ def test_bench_control_plane_two_ranks(tmp_path):
             assert (lo, hi) == (b[r], b[r + 1]) and n_nodes == hi - lo
             assert n_procs == fleet.config_procs_per_node(config, int(total))[lo:hi].sum()
         assert got[0][0] == 0 and got[-1][1] == total  # the ranks tile the fleet
-    # weak scaling for configs 3 / 5, strong for config 4
-    assert rows[0][1 + 4] == 120 and rows[0][6 + 4] == 90
+    # strong scaling by default (one fixed fleet cut N ways); weak = N x the fleet
+    assert rows[0][1 + 4] == 60 and rows[0][6 + 4] == 90 and rows[0][11 + 4] == 60
+    import bench
+
+    assert bench.bench_nodes(3, 2, 60, "weak") == 120 and bench.bench_nodes(4, 2, 90, "weak") == 90

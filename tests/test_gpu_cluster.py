@@ -164,6 +164,11 @@ def test_cluster_join_one_rank():
     acc.sync(s)
     cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
     assert cl.info() == (1, 0, 1)
+    # the RCCL the collectives run with: major version of the build's headers, a real file
+    import os
+    version, path = accel.Cluster.rccl()
+    print(f"RCCL {version} at {path}", flush=True)
+    assert version // 10000 == 2 and os.path.exists(path)
     off, slots = L.namespace_csr()
     d = to_device({"o": off, "s": slots})
     Z = L.zones
@@ -256,3 +261,54 @@ def test_config4_full_size_sharded_8_ways():
         np.testing.assert_allclose(op[r].cpu().numpy(), fp.cpu().numpy(), rtol=1e-12, atol=0)
     cl.close()
     full.close()
+
+
+def test_cluster_node_totals_follow_the_live_nodes():
+    """Cluster node totals sum the nodes of the LAST interval run on the context: when a
+    shard's batch shrinks, the nodes that left stop counting (Kepler: a node that is gone
+    stops exporting, so PromQL's sum drops it), although their state rows are kept."""
+    L = fleet.make_layout(12, [300, 40, 900, 5] * 3, 2, seed=9, n_namespaces=3)
+    acc = accel.Accel(L.zones, **L.capacities())
+    sim = fleet.FleetSim(L, seed=9)
+    s = current_stream_handle()
+    cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
+    Z = L.zones
+    ne = torch.zeros(2 * Z, dtype=torch.int64, device="cuda")
+    npw = torch.zeros(3 * Z, dtype=torch.float64, device="cuda")
+
+    def totals():
+        cl.allreduce_namespaces(0, None, None, None, None, [ne.data_ptr()], [npw.data_ptr()], streams=[s])
+        torch.cuda.synchronize()
+        return ne.cpu().numpy().view(np.uint64).copy(), npw.cpu().numpy().copy()
+
+    e0, p0 = totals()  # nothing run yet: zero
+    assert not e0.any() and not p0.any()
+
+    def want(n):
+        st = {t: acc.download(t).reshape(-1, Z)[:n] for t in ("node_active_total", "node_idle_total", "node_power",
+                                                            "node_active_power", "node_idle_power")}
+        return (np.concatenate([st[t].sum(axis=0, dtype=np.uint64) for t in ("node_active_total", "node_idle_total")]),
+                np.concatenate([st[t].sum(axis=0) for t in ("node_power", "node_active_power", "node_idle_power")]))
+
+    for _ in range(3):
+        t = to_device(sim.next_interval())
+        acc.run_interval(interval_from_tensors(t, L.sizes(), L.fast_flag()), s)
+    acc.sync(s)
+    e, p = totals()
+    we, wp = want(L.n_nodes)
+    np.testing.assert_array_equal(e, we)
+    np.testing.assert_allclose(p, wp, rtol=1e-12, atol=0)
+    assert we.any()
+    # the batch shrinks to its first 9 nodes
+    keep = np.arange(9)
+    sub, sizes, _ = fleet.subset_interval(sim.next_interval(), keep, Z)
+    t = to_device(sub)
+    acc.run_interval(interval_from_tensors(t, sizes, L.fast_flag()), s)
+    acc.sync(s)
+    e, p = totals()
+    we, wp = want(9)
+    np.testing.assert_array_equal(e, we)
+    np.testing.assert_allclose(p, wp, rtol=1e-12, atol=0)
+    assert not np.array_equal(we, want(L.n_nodes)[0])  # the 3 nodes that left counted before
+    cl.close()
+    acc.close()

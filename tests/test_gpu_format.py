@@ -177,7 +177,9 @@ def test_format_lines_hipcub_fault_regression_multi_tile_past_4gib():
     zone_names = ["package", "core", "uncore", "dram"]
     rng = np.random.default_rng(23)
     acc = accel.Accel(Z, nodes=1, proc_slots=count, ctr_slots=1, vm_slots=1, pod_slots=1)
-    vals = (rng.lognormal(20, 5, size=count * Z)).astype(np.uint64)
+    # finite energies over the whole u64 range (lognormal's tail is clipped below 2^64, so no
+    # inf / NaN reaches the cast): µJ values from 1 to ~1.8e19
+    vals = np.minimum(rng.lognormal(20, 5, size=count * Z), 1.8e19).astype(np.uint64)
     acc.upload("proc_energy", vals)
     # fixed-width label pairs: pid="00001234",comm="xxxx...x" (L bytes per row)
     head = b'comm="'

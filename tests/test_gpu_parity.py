@@ -387,6 +387,69 @@ def test_run_intervals_matches_sequential(name, kw):
     acc.close()
 
 
+@pytest.mark.parametrize("flags_mask", [~0, ~accel.KACC_F_SMALL_NODES], ids=["small_kernel", "interval_kernel"])
+@pytest.mark.parametrize("nodes", [None, 96], ids=["single-node", "fleet-96"])
+def test_config1_exact_layout_bit_exact(nodes, flags_mask):
+    """BASELINE config 1 exactly: fleet.config_layout(1) — package + dram (Z = 2), the fake CPU
+    power meter's MaxEnergy 1e6 (counters wrap), 500 processes -> 50 containers -> 20 pods per
+    node — over 8 intervals with churn, every table bit-exact against the oracle; one node (the
+    reference's own case) and a fleet of such nodes, through the one-wavefront-per-node kernel
+    and the workgroup-per-node kernel."""
+    from oracle.oracle import Oracle
+
+    layout = fleet.config_layout(1, nodes=nodes)
+    assert layout.zones == 2 and np.all(np.diff(layout.proc_off.astype(np.int64)) == 500)
+    assert np.all(np.diff(layout.ctr_off.astype(np.int64)) == 50) and np.all(np.diff(layout.pod_off.astype(np.int64)) == 20)
+    flags = layout.fast_flag() & flags_mask
+    assert flags & accel.KACC_F_FAST_NODES
+    sim = fleet.FleetSim(layout, seed=31, churn=0.03, max_energy=fleet.MAX_ENERGY_FAKE, read_error_frac=0.05)
+    eng = EngineBackend(layout.zones, layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    wrapped = 0
+    prev = None
+    for k in range(8):
+        a = sim.next_interval()
+        wrapped += 0 if prev is None else int(np.count_nonzero(a["zone_energy"] < prev))
+        prev = a["zone_energy"].copy()
+        eng.interval(a, layout.sizes(), flags)
+        ora.interval(a, layout.sizes())
+        for name, _ in accel.TABLES:
+            assert_table_equal(eng.table(name), ora.state[name], f"interval {k} {name}")
+    assert wrapped > 0  # the fake meter's counters wrapped at least once
+
+
+@pytest.mark.timeout(300)
+def test_config5_shape_60_intervals_one_call_bit_exact():
+    """BASELINE config 5's shape: heavy-tailed nodes of 10k-50k processes, Z = 4, VMs +
+    containers + pods, 60 intervals in ONE kacc_run_intervals call with counter wraparound
+    (fake-meter MaxEnergy 1e6), churn, read errors and adversarial inputs: every table
+    bit-exact against the oracle after the call (and after the first-read call before it)."""
+    from oracle.oracle import Oracle
+
+    procs = [10000, 50000, 23000, 12000, 31000, 10000, 17500]
+    layout = fleet.make_layout(len(procs), procs, 4, seed=55, procs_per_vm=2, vm_frac=0.02)
+    assert layout.fast_flag() == 0  # big nodes: the chunked path
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=55, churn=0.02, read_error_frac=0.03, max_energy=fleet.MAX_ENERGY_FAKE,
+                         adversarial=0.05)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    s = current_stream_handle()
+    first = sim.next_interval()
+    t0 = to_device(first)
+    acc.run_intervals([interval_from_tensors(t0, sizes)], s)
+    ora.interval(first, sizes)
+    ivs = [sim.next_interval() for _ in range(60)]
+    dev = [to_device(a) for a in ivs]
+    acc.run_intervals([interval_from_tensors(t, sizes) for t in dev], s)
+    acc.sync(s)
+    for a in ivs:
+        ora.interval(a, sizes)
+    for tname, _ in accel.TABLES:
+        assert_table_equal(acc.download(tname), ora.state[tname], tname)
+    acc.close()
+
+
 @pytest.mark.parametrize("name,kw,K", [
     ("z2-config2-like", dict(n_nodes=64, procs_per_node=[1000, 700, 1, 0, 2048, 513] * 10 + [9] * 4, zones=2), 12),
     ("z2-fragmented", dict(n_nodes=16, procs_per_node=[2000, 900, 64, 3] * 4, zones=2, fragment_slots=0.05), 9),

@@ -13,6 +13,7 @@ reads at 64 B); both counters are KiB.  Per launch of kacc::interval_kernel<Z,0>
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import statistics
@@ -65,6 +66,8 @@ def main():
             "hbm_bytes_per_interval": (2.0 * fm + wm) * 1024.0 / K,
             "algorithmic_bytes_per_interval": alg / K,
             "source": label,
+            # the build the counters belong to: bench.py reports them only for this very library
+            "lib_sha256": hashlib.sha256(open(accel.LIB_PATH, "rb").read()).hexdigest(),
             "raw_kib": {"FETCH_SIZE": fv, "WRITE_SIZE": wv},
         }
     })
