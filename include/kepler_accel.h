@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define KACC_ABI_VERSION 2u
+#define KACC_ABI_VERSION 3u
 #define KACC_MAX_ZONES 8u
 
 /* Status codes. */
@@ -195,7 +195,21 @@ typedef struct kacc_interval {
 /* Device-resident state / result tables.  [n*Z+z] tables are node-major or
  * slot-major with the zone innermost.  After kacc_run_interval they hold the
  * new snapshot: node zones = monitor.NodeUsage (types.go:27-40), workload
- * zones = monitor.Usage (types.go:44-47).                                     */
+ * zones = monitor.Usage (types.go:44-47).
+ *
+ * KACC_T_PROC_POWER is DERIVED, not stored (ABI 3): a process's power is
+ * cpuTimeRatio · NodeUsage.ActivePower for a zone that passed the guard
+ * (process.go:124, 142), and 0 otherwise, so the engine keeps per slot the
+ * ratio (KACC_T_PROC_RATIO) and the node (KACC_T_PROC_NODE) of the slot's
+ * last attribution and multiplies on read, bit-identical to a stored value
+ * (8Z - 12 bytes less per process row and interval).  kacc_table_download,
+ * kacc_unpack, kacc_format_*, and the trackers' frozen copies derive it; it
+ * has no device pointer (kacc_table_device_ptr: KACC_EINVAL) and cannot be
+ * uploaded.  The derived value is Usage.Power for every slot its node
+ * attributed in the node's LAST processed interval (the snapshot's running
+ * processes); for a slot that left its node's batch it is defined only until
+ * that node's next interval (a terminated process's final power is read by
+ * kacc_tracker_add before then).                                             */
 typedef enum kacc_table {
   KACC_T_NODE_ENERGY_TOTAL = 0, /* u64 [N*Z] NodeUsage.EnergyTotal          */
   KACC_T_NODE_ACTIVE_ENERGY,    /* u64 [N*Z] NodeUsage.activeEnergy (interval) */
@@ -210,7 +224,7 @@ typedef enum kacc_table {
   KACC_T_NODE_CPU_DELTA,        /* f64 [N]   ProcessTotalCPUTimeDelta used   */
   KACC_T_NODE_STATUS,           /* u32 [N]   KACC_NODE_OK/FIRST_READ/SKIPPED */
   KACC_T_PROC_ENERGY,           /* u64 [Sp*Z] Process Usage.EnergyTotal      */
-  KACC_T_PROC_POWER,            /* f64 [Sp*Z] Process Usage.Power            */
+  KACC_T_PROC_POWER,            /* f64 [Sp*Z] Process Usage.Power (DERIVED)  */
   KACC_T_CTR_ENERGY,            /* u64 [Sc*Z]                                */
   KACC_T_CTR_POWER,             /* f64 [Sc*Z]                                */
   KACC_T_CTR_CPU_DELTA,         /* f64 [Sc]  resource.Container.CPUTimeDelta */
@@ -222,6 +236,9 @@ typedef enum kacc_table {
   KACC_T_POD_POWER,             /* f64 [Sq*Z]                                */
   KACC_T_POD_CPU_DELTA,         /* f64 [Sq]  resource.Pod.CPUTimeDelta       */
   KACC_T_POD_CPU_TOTAL,         /* f64 [Sq]  resource.Pod.CPUTotalTime       */
+  KACC_T_PROC_RATIO,            /* f64 [Sp]  cpuTimeRatio of the slot's last attribution
+                                              (process.go:128; Δ / ProcessTotalCPUTimeDelta) */
+  KACC_T_PROC_NODE,             /* u32 [Sp]  the node of that attribution     */
   KACC_T_COUNT
 } kacc_table;
 

@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KACC_LIB", os.path.join(_HERE, "lib", "libkepler_accel.so"))  # KACC_LIB: A/B builds
 
-KACC_ABI_VERSION = 2
+KACC_ABI_VERSION = 3
 KACC_MAX_ZONES = 8
 KACC_OK = 0
 KACC_EINVAL = -1
@@ -80,7 +80,15 @@ TABLES = [
     ("pod_power", np.float64),
     ("pod_cpu_delta", np.float64),
     ("pod_cpu_total", np.float64),
+    ("proc_ratio", np.float64),
+    ("proc_node", np.uint32),
 ]
+# derived on read (no device storage, no upload / device pointer): a process's power is
+# cpuTimeRatio x its node's ActivePower (process.go:124-142; kacc_derive.hpp)
+DERIVED_TABLES = {"proc_power"}
+# engine storage behind a derived table (not a Go quantity): the CPU restatements keep them
+# only to check the engine's layout
+ENGINE_TABLES = {"proc_ratio", "proc_node"}
 TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)

@@ -33,6 +33,7 @@
 
 #include "../../include/kepler_accel.h"
 #include "kacc_debug.h"
+#include "kacc_derive.hpp"
 #include "kacc_device.hpp"
 #include "kacc_internal.hpp"
 
@@ -124,7 +125,8 @@ struct DevState {
   double *node_usage_ratio, *node_cpu_delta;
   uint32_t *node_status;
   uint64_t *proc_energy;
-  double *proc_power;
+  double *proc_ratio;   // [Sp] cpuTimeRatio of the slot's last attribution (power is derived)
+  uint32_t *proc_node;  // [Sp] the node that attribution belonged to
   uint64_t *ctr_energy;
   double *ctr_power, *ctr_cpu_delta, *ctr_cpu_total;
   uint64_t *vm_energy;
@@ -274,6 +276,42 @@ __device__ __forceinline__ void attribute_row(const Attr<Z> &a, uint32_t live, d
   }
 }
 
+// process.go:118-148 for one process row: the energy totals, and the row's
+// cpuTimeRatio (returned), which the state keeps INSTEAD of the Z powers: a
+// process's Power is ratio · the node's ActivePower when the zone passes the
+// guard (process.go:124, 142) — a function of the node's own tables of the same
+// interval (kacc_derive.hpp), derived wherever it is read.  8 + 4 bytes per row
+// (ratio, node) instead of 8Z.
+template <int Z>
+__device__ __forceinline__ double attribute_proc(const Attr<Z> &a, double delta, bool is_new,
+                                                 const uint64_t (&prev)[Z], uint64_t (&E)[Z]) {
+  const double ratio = delta / a.nd;  // one IEEE division per row, never a reciprocal
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    if (a.live & (1u << z)) {
+      const uint64_t e = go_f64_to_u64(ratio * u2f(a.aE[z]));
+      E[z] = a.first ? e : e + (is_new ? 0ull : prev[z]);
+    } else {  // skipped zone keeps the zero Usage of newProcess (process.go:58-63)
+      E[z] = 0;
+    }
+  }
+  return ratio;
+}
+
+// A process row's outputs at slot s: energy totals, ratio and node.
+template <int Z, bool NT>
+__device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const uint64_t (&E)[Z], double ratio,
+                                           uint32_t node) {
+  store_row<Z, NT, uint64_t>(st.proc_energy, s, E);
+  if constexpr (NT) {
+    __builtin_nontemporal_store(ratio, st.proc_ratio + s);
+    __builtin_nontemporal_store(node, st.proc_node + s);
+  } else {
+    st.proc_ratio[s] = ratio;
+    st.proc_node[s] = node;
+  }
+}
+
 // One aggregate row (container / VM / pod): read-modify-write of its slot.
 template <int Z, bool NT>
 __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, double delta,
@@ -360,13 +398,12 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
                                                        uint32_t row0, uint64_t s0, uint32_t len,
                                                        const uint64_t (&prev)[Z],
                                                        uint64_t *__restrict__ energy,
-                                                       double *__restrict__ power) {
+                                                       double *__restrict__ ratio_tab,
+                                                       uint32_t *__restrict__ node_tab, uint32_t node) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
-  using f64x2 = __attribute__((ext_vector_type(2))) double;
   constexpr int kHalf = Z / 2;
   const uint32_t lane = threadIdx.x & 63u;
   u64x2 *pe = reinterpret_cast<u64x2 *>(energy + s0 * Z);
-  f64x2 *pp = reinterpret_cast<f64x2 *>(power + s0 * Z);
 #pragma unroll
   for (int j = 0; j < kHalf; ++j) {
     const uint32_t piece = lane + 64u * j;
@@ -382,35 +419,34 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
     const bool is_new = (wr & KACC_SLOT_NEW) != 0;
     const double ratio = s_d[row] / a.nd;  // the row's own IEEE division
     uint64_t E[2];
-    double P[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       // zone 2*zp+h: lane-dependent, so read from LDS (a register array
       // indexed by a lane value would be demoted to scratch)
       const uint32_t z = 2 * zp + h;
       const uint64_t aE = sh.active_energy[z];
-      const double aP = sh.active_power[z];
       if (a.live & (1u << z)) {
         const uint64_t e = go_f64_to_u64(ratio * u2f(aE));
         E[h] = a.first ? e : e + (is_new ? 0ull : prev[2 * j + h]);
-        P[h] = a.first ? 0.0 : ratio * aP;
       } else {
         E[h] = 0;
-        P[h] = 0.0;
       }
     }
     u64x2 ev;
     ev.x = E[0];
     ev.y = E[1];
-    f64x2 pv;
-    pv.x = P[0];
-    pv.y = P[1];
-    if constexpr (NT) {
+    if constexpr (NT)
       __builtin_nontemporal_store(ev, pe + piece);
-      __builtin_nontemporal_store(pv, pp + piece);
-    } else {
+    else
       pe[piece] = ev;
-      pp[piece] = pv;
+    if (zp == 0) {  // the slot's ratio and node: contiguous across the group's lanes
+      if constexpr (NT) {
+        __builtin_nontemporal_store(ratio, ratio_tab + s0 + idx);
+        __builtin_nontemporal_store(node, node_tab + s0 + idx);
+      } else {
+        ratio_tab[s0 + idx] = ratio;
+        node_tab[s0 + idx] = node;
+      }
     }
   }
 }
@@ -826,10 +862,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
         if (r == 0xffffu) continue;  // a free slot of the node's range
         const uint32_t wk = s_w[r];
         uint64_t E[Z];
-        double P[Z];
-        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E, P);
-        store_row<Z, kNT, uint64_t>(st.proc_energy, static_cast<uint64_t>(smin) + pos, E);
-        store_row<Z, kNT, double>(st.proc_power, static_cast<uint64_t>(smin) + pos, P);
+        const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E);
+        store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n);
       }
     }
     if constexpr (kSweepable) {
@@ -839,7 +873,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
         const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
         attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0,
                                              static_cast<uint64_t>(smin) + pos0, len, prev[k],
-                                             st.proc_energy, st.proc_power);
+                                             st.proc_energy, st.proc_ratio, st.proc_node, n);
       }
     }
   } else if constexpr ((V & kVarSkipProcs) == 0) {  // process.go:118-148
@@ -851,7 +885,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
           const uint32_t pos0 = r - (tid & 63);
           attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
                                                 uniform_u32(s_w[pos0] & KACC_SLOT_MASK), 64u, prev[k],
-                                                st.proc_energy, st.proc_power);
+                                                st.proc_energy, st.proc_ratio, st.proc_node, n);
           continue;
         }
       }
@@ -863,10 +897,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
         continue;
       }
       uint64_t E[Z];
-      double P[Z];
-      attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E, P);
-      store_row<Z, kNtScat, uint64_t>(st.proc_energy, sl, E);
-      store_row<Z, kNtScat, double>(st.proc_power, sl, P);
+      const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E);
+      store_proc<Z, kNtScat>(st, sl, E, ratio, n);
     }
   }
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
@@ -1430,13 +1462,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           s_inv[pos] = 0xffffu;        // the map starts empty next interval (this lane's entry)
           const uint32_t wk = s_w[r];
           uint64_t pv[Z], E[Z];
-          double P[Z];
 #pragma unroll
           for (int z = 0; z < Z; ++z) pv[z] = s_cE[pos * Z + z];
-          attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E, P);
+          const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E);
           if constexpr ((V & kCarryNoRowStores) == 0) {
-            store_row<Z, true, uint64_t>(st.proc_energy, static_cast<uint64_t>(s_lo) + pos, E);
-            store_row<Z, true, double>(st.proc_power, static_cast<uint64_t>(s_lo) + pos, P);
+            store_proc<Z, true>(st, static_cast<uint64_t>(s_lo) + pos, E, ratio, n);
           }
 #pragma unroll
           for (int z = 0; z < Z; ++z) s_cE[pos * Z + z] = E[z];
@@ -1457,13 +1487,11 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           continue;
         }
         uint64_t pv[Z], E[Z];
-        double P[Z];
 #pragma unroll
         for (int z = 0; z < Z; ++z) pv[z] = s_cE[r * Z + z];
-        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E, P);
+        const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E);
         if constexpr ((V & kCarryNoRowStores) == 0) {
-          store_row<Z, kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
-          store_row<Z, kNtScatterStores, double>(st.proc_power, sl, P);
+          store_proc<Z, kNtScatterStores>(st, sl, E, ratio, n);
         }
 #pragma unroll
         for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = E[z];
@@ -1837,10 +1865,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
           const uint32_t e = s_inv[pos];
           if (e == 0xffffu) continue;
           uint64_t E[Z];
-          double P[Z];
-          attribute_row<Z>(a, a.live, s_d[e & 0x7fffu], (e & 0x8000u) != 0, prev[g], E, P);
-          store_row<Z, kNT, uint64_t>(st.proc_energy, static_cast<uint64_t>(smin) + pos, E);
-          store_row<Z, kNT, double>(st.proc_power, static_cast<uint64_t>(smin) + pos, P);
+          const double ratio = attribute_proc<Z>(a, s_d[e & 0x7fffu], (e & 0x8000u) != 0, prev[g], E);
+          store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n);
           continue;
         }
       }
@@ -1848,13 +1874,13 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
         if (swept) {
           const uint32_t len = pos0 < span ? min(span - pos0, 64u) : 0u;
           attribute_group_masked<Z, kNT, true>(a, sh, s_d, s_w, s_inv, pos0, static_cast<uint64_t>(smin) + pos0,
-                                               len, prev[g], st.proc_energy, st.proc_power);
+                                               len, prev[g], st.proc_energy, st.proc_ratio, st.proc_node, n);
           continue;
         }
         if (contig & (1u << g)) {
           attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, s_inv, pos0,
                                                 uniform_u32(s_w[pos0] & KACC_SLOT_MASK), 64u, prev[g],
-                                                st.proc_energy, st.proc_power);
+                                                st.proc_energy, st.proc_ratio, st.proc_node, n);
           continue;
         }
       }
@@ -1871,10 +1897,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
         continue;
       }
       uint64_t E[Z];
-      double P[Z];
-      attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[g], E, P);
-      store_row<Z, kNT && kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
-      store_row<Z, kNT && kNtScatterStores, double>(st.proc_power, sl, P);
+      const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[g], E);
+      store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n);
     }
   };
   attr_batch(0);
@@ -2343,7 +2367,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
             const uint32_t g = r - (tid & 63);
             attribute_group_masked<Z, kNT, false>(a, sh, s_d, s_w, nullptr, g,
                                            uniform_u32(s_w[g] & KACC_SLOT_MASK), 64u, prev[u],
-                                           st.proc_energy, st.proc_power);
+                                           st.proc_energy, st.proc_ratio, st.proc_node, n);
             continue;
           }
         }
@@ -2355,10 +2379,8 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
           continue;
         }
         uint64_t E[Z];
-        double P[Z];
-        attribute_row<Z>(a, a.live, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E, P);
-        store_row<Z, kNT && kNtScatterStores, uint64_t>(st.proc_energy, sl, E);
-        store_row<Z, kNT && kNtScatterStores, double>(st.proc_power, sl, P);
+        const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E);
+        store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n);
       }
     }
     // aggregates beyond one per lane (chunks of mostly empty containers):
@@ -2635,6 +2657,17 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
   if (tid == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
 }
 
+// Elements [first, first + count) of the derived process power table
+// ([slot*Z + z], kacc_derive.hpp), grid-stride.
+__global__ __launch_bounds__(kBlock) void proc_power_kernel(const ProcDerive d, uint64_t first, uint64_t count,
+                                                            double *out) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < count;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint64_t e = first + i;
+    out[i] = proc_power(d, e / d.zones, static_cast<uint32_t>(e % d.zones));
+  }
+}
+
 }  // namespace kacc
 
 // =============================================================================
@@ -2653,15 +2686,20 @@ struct TableDesc {
   uint32_t elem;   // bytes
   int per;         // 0 = per node, 1 = per proc slot, 2 ctr, 3 vm, 4 pod
   bool zoned;      // × Z
+  bool derived;    // no storage: computed on read (KACC_T_PROC_POWER, kacc_derive.hpp)
 };
 
 const TableDesc kTables[KACC_T_COUNT] = {
-    {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},  {8, 0, true},
-    {8, 0, true},  {8, 0, false}, {4, 0, false}, {8, 0, false}, {8, 0, false}, {4, 0, false},
-    {8, 1, true},  {8, 1, true},  {8, 2, true},  {8, 2, true},  {8, 2, false}, {8, 2, false},
-    {8, 3, true},  {8, 3, true},  {8, 3, false}, {8, 4, true},  {8, 4, true},  {8, 4, false},
-    {8, 4, false},
+    {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},
+    {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},  {8, 0, false, false},
+    {4, 0, false, false}, {8, 0, false, false}, {8, 0, false, false}, {4, 0, false, false},
+    {8, 1, true, false},  {8, 1, true, true},   {8, 2, true, false},  {8, 2, true, false},
+    {8, 2, false, false}, {8, 2, false, false}, {8, 3, true, false},  {8, 3, true, false},
+    {8, 3, false, false}, {8, 4, true, false},  {8, 4, true, false},  {8, 4, false, false},
+    {8, 4, false, false}, {8, 1, false, false}, {4, 1, false, false},
 };
+static_assert(KACC_T_PROC_POWER == 13 && KACC_T_PROC_RATIO == 25 && KACC_T_PROC_NODE == 26 && KACC_T_COUNT == 27,
+              "kTables rows follow the kacc_table enum");
 
 }  // namespace
 
@@ -2713,7 +2751,8 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.node_cpu_delta = (double *)T(KACC_T_NODE_CPU_DELTA);
   s.node_status = (uint32_t *)T(KACC_T_NODE_STATUS);
   s.proc_energy = (uint64_t *)T(KACC_T_PROC_ENERGY);
-  s.proc_power = (double *)T(KACC_T_PROC_POWER);
+  s.proc_ratio = (double *)T(KACC_T_PROC_RATIO);
+  s.proc_node = (uint32_t *)T(KACC_T_PROC_NODE);
   s.ctr_energy = (uint64_t *)T(KACC_T_CTR_ENERGY);
   s.ctr_power = (double *)T(KACC_T_CTR_POWER);
   s.ctr_cpu_delta = (double *)T(KACC_T_CTR_CPU_DELTA);
@@ -3100,6 +3139,7 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
   }
   for (int t = 0; t < KACC_T_COUNT; ++t) {
     ctx->counts[t] = table_count(ctx->cfg, t);
+    if (kTables[t].derived) continue;  // computed on read
     const size_t bytes = std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem;
     if ((e = hipMalloc(&ctx->tables[t], bytes)) != hipSuccess) {
       fail(ctx, KACC_ENOMEM, "hipMalloc table %d (%zu B): %s", t, bytes, hipGetErrorString(e));
@@ -3152,9 +3192,9 @@ int kacc_reset(kacc_ctx *ctx) {
   if (!ctx) return KACC_EINVAL;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   for (int t = 0; t < KACC_T_COUNT; ++t)
-    KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0,
-                                 std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
-                                 ctx->stream));
+    if (!kTables[t].derived)
+      KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0, std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
+                                   ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -3514,6 +3554,10 @@ int kacc_table_info(const kacc_ctx *ctx, kacc_table t, uint64_t *elem_bytes, uin
 
 int kacc_table_device_ptr(kacc_ctx *ctx, kacc_table t, void **dev_ptr) {
   if (!ctx || t < 0 || t >= KACC_T_COUNT || !dev_ptr) return KACC_EINVAL;
+  if (kTables[t].derived) {
+    *dev_ptr = nullptr;
+    return fail(ctx, KACC_EINVAL, "table %d is derived on read (no device storage): see kacc_table_download", (int)t);
+  }
   *dev_ptr = ctx->tables[t];
   return KACC_OK;
 }
@@ -3525,9 +3569,22 @@ static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
     return fail(ctx, KACC_EINVAL, "table %d range [%llu,+%llu) outside %llu", (int)t,
                 (unsigned long long)first, (unsigned long long)count,
                 (unsigned long long)ctx->counts[t]);
+  if (kTables[t].derived && !down)
+    return fail(ctx, KACC_EINVAL, "table %d is derived on read and cannot be uploaded", (int)t);
   if (!count) return KACC_OK;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (kTables[t].derived) {  // KACC_T_PROC_POWER: derived into a scratch buffer, then copied
+    double *tmp = nullptr;
+    KACC_HIP(ctx, hipMalloc(&tmp, count * sizeof(double)));
+    int rc = kacc_internal_proc_power(ctx, first, count, tmp, ctx->stream);
+    hipError_t e = rc == KACC_OK ? hipStreamSynchronize(ctx->stream) : hipSuccess;
+    if (rc == KACC_OK && e == hipSuccess) e = hipMemcpy(host, tmp, count * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(tmp);
+    if (rc != KACC_OK) return rc;
+    if (e != hipSuccess) return fail(ctx, KACC_EHIP, "derived table %d: %s", (int)t, hipGetErrorString(e));
+    return KACC_OK;
+  }
   char *dev = static_cast<char *>(ctx->tables[t]) + first * kTables[t].elem;
   const size_t bytes = count * kTables[t].elem;
   if (down)
@@ -3622,6 +3679,20 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
   return KACC_OK;
 }
 
+int kacc_internal_proc_power(kacc_ctx *ctx, uint64_t first, uint64_t count, double *out, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (!count) return KACC_OK;
+  if (!out) return fail(ctx, KACC_EINVAL, "NULL argument");
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const uint64_t blocks = (count + kacc::kBlock - 1) / kacc::kBlock;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(kacc::proc_power_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
+                     dim3(kacc::kBlock), 0, st, kacc_proc_derive(ctx), first, count, out);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
 uint64_t kacc_intervals_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V, uint64_t Q, uint32_t K,
                               int carried) {
   // K intervals of these sizes.  Carried (intervals_carry_kernel,
@@ -3640,7 +3711,8 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
                              uint64_t Q) {
   // minimal HBM bytes of one interval_kernel launch.
   const uint64_t node = 76 + 96ull * Z;
-  const uint64_t proc = 12 + 24ull * Z;
+  // Δ 8 + slot 4 in, previous totals 8Z in; totals 8Z + ratio 8 + node 4 out
+  const uint64_t proc = 24 + 16ull * Z;
   const uint64_t ctr = 32 + 24ull * Z;
   const uint64_t vm = 16 + 24ull * Z;
   const uint64_t pod = 32 + 24ull * Z;

@@ -29,6 +29,7 @@
 #include <string>
 #include <vector>
 
+#include "kacc_derive.hpp"
 #include "kacc_internal.hpp"
 #include "kacc_pow5_tables.h"
 
@@ -403,6 +404,7 @@ constexpr uint32_t kConstCap = 1024;
 constexpr int kLineWaves = 2;  // line_write_kernel: waves per workgroup (16 KiB of LDS each)
 
 struct LineArgs {
+  uint64_t src_first;  // element index of src[0] (a derived table materialised from its row `first`)
   const void *src;       // table base
   uint32_t Z;            // table zones
   uint32_t is_energy;
@@ -433,9 +435,9 @@ __device__ __forceinline__ uint64_t line_row(const LineArgs &a, uint64_t r) {
 // of reading a stored copy: the formatting is cheaper than 2 x 24 B of traffic).
 __device__ __forceinline__ void line_value(const LineArgs &a, uint64_t e, Text &o) {
   if (a.is_energy)
-    write_joules(static_cast<const uint64_t *>(a.src)[e], o);  // energy.go:30-32
+    write_joules(static_cast<const uint64_t *>(a.src)[e - a.src_first], o);  // energy.go:30-32
   else
-    write_float(static_cast<const double *>(a.src)[e] / 1e6, o);  // energy.go:57-59
+    write_float(static_cast<const double *>(a.src)[e - a.src_first] / 1e6, o);  // energy.go:57-59
 }
 
 // Pass 1: the length of every line.
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(64 * kLineWaves) void line_write_kernel(const LineA
     p.l1 = a.label_off[r + 1];
     p.o0 = a.line_off[i];
     p.o1 = a.line_off[i + 1];
-    p.raw = static_cast<const uint64_t *>(a.src)[(a.first + r) * a.Z + a.zone_table[p.j]];
+    p.raw = static_cast<const uint64_t *>(a.src)[(a.first + r) * a.Z + a.zone_table[p.j] - a.src_first];
     return p;
   };
   const uint64_t base0 = (static_cast<uint64_t>(blockIdx.x) * kLineWaves + (threadIdx.x >> 6)) * 64;
@@ -779,15 +781,29 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   kacc::fmt::Args a{};
   a.src = static_cast<const char *>(ctx->tables[t]) + first * 8;
+  double *derived = nullptr;  // KACC_T_PROC_POWER: the range derived first (kacc_derive.hpp)
+  if (t == KACC_T_PROC_POWER) {
+    KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&derived), count * 8, st));
+    const int rc = kacc_internal_proc_power(ctx, first, count, derived, st);
+    if (rc != KACC_OK) {
+      (void)hipFreeAsync(derived, st);
+      return rc;
+    }
+    a.src = derived;
+  }
   a.count = count;
   a.is_energy = energy ? 1u : 0u;
   a.out = out;
   a.len = len;
   (void)hipGetLastError();  // clear a stale error of an earlier call
   const uint64_t grid = (count + kacc::fmt::kThreads - 1) / kacc::fmt::kThreads;
-  if (grid > 0x7fffffffull) return kacc_fail(ctx, KACC_EINVAL, "format: count too large for one launch");
+  if (grid > 0x7fffffffull) {
+    if (derived) (void)hipFreeAsync(derived, st);
+    return kacc_fail(ctx, KACC_EINVAL, "format: count too large for one launch");
+  }
   hipLaunchKernelGGL(kacc::fmt::format_kernel, dim3(static_cast<uint32_t>(grid)), dim3(kacc::fmt::kThreads), 0,
                      st, a);
+  if (derived) (void)hipFreeAsync(derived, st);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
@@ -846,7 +862,8 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   a.out = out;
   a.out_cap = out_cap;
   a.err = ctx->d_err;
-  // temporaries, stream ordered: consts, lengths, tile sums
+  // temporaries, stream ordered: consts, lengths, tile sums (+ the derived rows of
+  // KACC_T_PROC_POWER, rows [first, first + count), kacc_derive.hpp)
   const uint64_t tiles = (lines + 1 + kacc::fmt::kTile - 1) / kacc::fmt::kTile;
   if (tiles > 0x7fffffffull) return kacc_fail(ctx, KACC_EINVAL, "format_lines: too many lines");
   const size_t scan_bytes = 8 * tiles;
@@ -854,7 +871,10 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   // every sub-buffer 256-B aligned (the scan's look-back state needs aligned storage)
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
   const uint64_t off_len = 1024, off_scan = al(off_len + 8 * (lines + 1));
-  KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), off_scan + scan_bytes, st));
+  const bool derived = t == KACC_T_PROC_POWER;
+  const uint64_t off_derived = al(off_scan + scan_bytes);
+  KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), derived ? off_derived + 8 * count * Z : off_scan + scan_bytes,
+                               st));
   a.consts = tmp;
   a.len = reinterpret_cast<uint64_t *>(tmp + off_len);
   int rc = KACC_OK;
@@ -862,6 +882,13 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
     (void)hipFreeAsync(tmp, st);
     return code;
   };
+  if (derived) {
+    a.src = tmp + off_derived;
+    a.src_first = first * Z;
+    if ((rc = kacc_internal_proc_power(ctx, first * Z, count * Z, reinterpret_cast<double *>(tmp + off_derived), st)) !=
+        KACC_OK)
+      return done(rc);
+  }
   if (hipMemcpyAsync(tmp, consts.data(), consts.size(), hipMemcpyHostToDevice, st) != hipSuccess)
     return done(kacc_fail(ctx, KACC_EHIP, "format_lines: constants upload"));
   (void)hipGetLastError();

@@ -33,6 +33,7 @@
 #include <thread>
 #include <vector>
 
+#include "kacc_derive.hpp"
 #include "kacc_internal.hpp"
 
 namespace {
@@ -232,10 +233,13 @@ namespace unpack {
 constexpr int kThreads = 256;
 
 // out[dest ? dest[i] : i] = the tables' row of slot word w[i] (energy, power per zone).
+// Processes (tp NULL): power derived from the slot's ratio and its node's tables
+// (kacc_derive.hpp).
 template <int Z>
 __global__ __launch_bounds__(kThreads) void unpack_kernel(uint32_t n, const uint32_t *w, const uint32_t *dest,
                                                           uint64_t cap, const uint64_t *te, const double *tp,
-                                                          uint64_t *oe, double *op, uint32_t *err) {
+                                                          const ProcDerive pd, uint64_t *oe, double *op,
+                                                          uint32_t *err) {
   const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint64_t s = w[i] & KACC_SLOT_MASK;
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(kThreads) void unpack_kernel(uint32_t n, const uint
 #pragma unroll
   for (int z = 0; z < Z; ++z) {
     oe[o + z] = te[s * Z + z];
-    op[o + z] = tp[s * Z + z];
+    op[o + z] = tp ? tp[s * Z + z] : proc_power(pd, s, z);
   }
 }
 
@@ -343,12 +347,13 @@ int kacc_unpack(kacc_ctx *ctx, kacc_kind kind, uint32_t n, const uint32_t *slot_
                        : kind == KACC_KIND_VM ? ctx->cfg.vm_slots
                                               : ctx->cfg.pod_slots;
   const uint64_t *e = static_cast<const uint64_t *>(ctx->tables[te]);
-  const double *p = static_cast<const double *>(ctx->tables[te + 1]);
+  const double *p = kind == KACC_KIND_PROC ? nullptr : static_cast<const double *>(ctx->tables[te + 1]);
+  const kacc::ProcDerive pd = kacc_proc_derive(ctx);
   const uint32_t grid = (n + kacc::unpack::kThreads - 1) / kacc::unpack::kThreads;
   (void)hipGetLastError();
 #define KACC_UNPACK(Z)                                                                                          \
   hipLaunchKernelGGL((kacc::unpack::unpack_kernel<Z>), dim3(grid), dim3(kacc::unpack::kThreads), 0, st, n,   \
-                     slot_words, dest, cap, e, p, out_energy, out_power, ctx->d_err)
+                     slot_words, dest, cap, e, p, pd, out_energy, out_power, ctx->d_err)
   switch (ctx->cfg.zones) {
     case 1: KACC_UNPACK(1); break;
     case 2: KACC_UNPACK(2); break;

@@ -32,6 +32,7 @@
 #include <cstring>
 #include <vector>
 
+#include "kacc_derive.hpp"
 #include "kacc_internal.hpp"
 
 namespace kacc {
@@ -43,7 +44,8 @@ constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node c
 
 struct Args {
   const uint64_t *tab_e;
-  const double *tab_p;
+  const double *tab_p;  // NULL for processes: power derived (kacc_derive.hpp) from pd
+  ProcDerive pd;
   uint64_t min_e;
   int64_t max_size;
   uint32_t Z, z0, cap, n_nodes;
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       a.set_key[base + r] = s_key[src];
       for (uint32_t z = 0; z < Z; ++z) {
         a.set_e[(base + r) * Z + z] = a.tab_e[sl * Z + z];
-        a.set_p[(base + r) * Z + z] = a.tab_p[sl * Z + z];
+        a.set_p[(base + r) * Z + z] = a.tab_p ? a.tab_p[sl * Z + z] : proc_power(a.pd, sl, z);
       }
     }
     size = new_size;
@@ -290,12 +292,15 @@ void kind_tables(const kacc_ctx *ctx, kacc_kind k, const uint64_t **e, const dou
                    : k == KACC_KIND_VM ? KACC_T_VM_ENERGY
                                        : KACC_T_POD_ENERGY;
   *e = static_cast<const uint64_t *>(ctx->tables[base]);
-  *p = static_cast<const double *>(ctx->tables[base + 1]);
+  // a process's power is derived (kacc_derive.hpp) from its ratio and its node's
+  // tables of the same interval: the tracker must run before that node's next one
+  *p = k == KACC_KIND_PROC ? nullptr : static_cast<const double *>(ctx->tables[base + 1]);
 }
 
 kacc::trk::Args tracker_args(const kacc_tracker *t) {
   kacc::trk::Args a{};
   kind_tables(t->ctx, t->kind, &a.tab_e, &a.tab_p);
+  a.pd = kacc_proc_derive(t->ctx);
   a.min_e = t->min_e;
   a.max_size = t->max_size;
   a.Z = t->Z;

@@ -227,6 +227,8 @@ static void node_interval(kor_state *st, const kacc_interval *b, uint32_t n, int
     const uint64_t s = w & KACC_SLOT_MASK;
     attribute(Z, d[i], node_delta, nz, false, first_read, (w & KACC_SLOT_NEW) != 0,
               st->proc_energy + s * Z, st->proc_power + s * Z);
+    if (st->proc_ratio) st->proc_ratio[s] = d[i] / node_delta;  // process.go:128
+    if (st->proc_node) st->proc_node[s] = n;
   }
   for (uint32_t c = r.c0; c < r.c1; ++c) {
     const uint32_t w = b->ctr_slot[c];

@@ -51,6 +51,10 @@ typedef struct kor_state {
   double *vm_power, *vm_cpu_delta;
   uint64_t *pod_energy;
   double *pod_power, *pod_cpu_delta, *pod_cpu_total;
+  /* the engine's process storage behind the derived power (kacc_derive.hpp):
+   * the row's cpuTimeRatio (process.go:128) and its node, per slot */
+  double *proc_ratio;
+  uint32_t *proc_node;
 } kor_state;
 
 /* Scalar Go-semantics helpers (exported so the KATs can pin them directly). */

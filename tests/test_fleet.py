@@ -67,7 +67,10 @@ def test_subset_matches_full_fleet(oracle_lib):
         f = full.state[name]
         per = len(f) // (L.n_nodes if kind == "node" else L.capacities()[f"{kind}_slots"])
         got = f.reshape(-1, per)[maps[kind]].reshape(-1)
-        np.testing.assert_array_equal(got, sub.state[name][: len(got)], err_msg=name)
+        want = sub.state[name][: len(got)]
+        if name == "proc_node":  # node indices of the subset -> the fleet's
+            want = maps["node"][want]
+        np.testing.assert_array_equal(got, want, err_msg=name)
 
 
 def test_plan_node_ranges_balanced():

@@ -55,7 +55,10 @@ def _check_shard_tables(shard_acc, sl, lo, hi, maps, want_state, zones, nodes_to
         if len(idx) == 0:
             continue
         want = full.reshape(-1, per)[idx]
-        np.testing.assert_array_equal(got.reshape(-1, per)[: len(idx)], want, err_msg=f"shard [{lo},{hi}) {name}")
+        g = got.reshape(-1, per)[: len(idx)]
+        if name == "proc_node":  # shard-local node indices -> the fleet's
+            g = g + lo
+        np.testing.assert_array_equal(g, want, err_msg=f"shard [{lo},{hi}) {name}")
 
 
 def _namespace_csr_device(layouts):
@@ -235,6 +238,8 @@ def test_config4_full_size_sharded_8_ways():
             n_rows = (hi - lo) if kind == "node" else sl.capacities()[f"{kind}_slots"]
             per = len(got) // n_rows
             want = full.download(name, base[kind] * per, len(got))
+            if name == "proc_node":  # shard-local node indices -> the fleet's
+                got = got + lo
             np.testing.assert_array_equal(got, want, err_msg=f"shard [{lo},{hi}) {name}")
     # sampled oracle parity of the unsharded context
     for name, _ in accel.TABLES:
@@ -242,7 +247,10 @@ def test_config4_full_size_sharded_8_ways():
         cap = L.n_nodes if kind == "node" else L.capacities()[f"{kind}_slots"]
         per = full.table_info(name)[1] // cap
         got = _gather_rows(full, name, omaps[kind], per)
-        np.testing.assert_array_equal(got, ora.state[name], err_msg=name)
+        want = ora.state[name]
+        if name == "proc_node":  # the sample's node indices -> the fleet's
+            want = omaps["node"][want]
+        np.testing.assert_array_equal(got, want, err_msg=name)
     # cluster namespace totals (RCCL path) == one context's namespace kernel
     n_ns = L.n_namespaces
     csr = _namespace_csr_device([sl for _, _, sl in shards])

@@ -61,10 +61,11 @@ def edge_powers():
 def test_format_edges():
     e, p = edge_energies(), edge_powers()
     n = max(e.size, p.size)
-    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=1)
+    # power values through a stored power table (KACC_T_PROC_POWER is derived: not uploadable)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=n, vm_slots=1, pod_slots=1)
     acc.upload("proc_energy", np.resize(e, n))
-    acc.upload("proc_power", np.resize(p, n))
-    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "proc_power", n)
+    acc.upload("ctr_power", np.resize(p, n))
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "ctr_power", n)
     for i in range(n):
         ev, pv = int(np.resize(e, n)[i]), float(np.resize(p, n)[i])
         assert got_e[i] == write_float(joules(ev)), (ev, got_e[i])
@@ -82,10 +83,10 @@ def test_format_random(kind):
     else:  # attribution-like: µJ totals and µW powers
         e = (rng.lognormal(18, 4, size=n)).astype(np.uint64)
         p = rng.lognormal(12, 3, size=n) * rng.choice([1.0, 1.0, 1.0, 0.0], size=n)
-    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=1)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=n, vm_slots=1, pod_slots=1)
     acc.upload("proc_energy", e)
-    acc.upload("proc_power", p)
-    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "proc_power", n)
+    acc.upload("ctr_power", p)
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "ctr_power", n)
     bad = []
     for i in range(n):
         we = write_float(joules(int(e[i])))
@@ -214,4 +215,60 @@ def test_format_lines_hipcub_fault_regression_multi_tile_past_4gib():
         want = sample_line(metric, bytes(labels[r]).decode(), zone_names[z], joules(int(vals[r * Z + z]))).encode()
         assert got == want, (i, got[:120], want[:120])
     del out
+    acc.close()
+
+
+def test_format_derived_process_power():
+    """KACC_T_PROC_POWER is derived on read (ratio x the node's ActivePower, kacc_derive.hpp):
+    format_values and format_lines of it == the downloaded (derived) values written as Go
+    writes them, after real intervals (guarded zones, NaN / Inf ratios of adversarial nodes)."""
+    from kepler_amd import fleet
+    from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
+    from oracle.gofmt import sample_line
+
+    L = fleet.make_layout(24, [300, 2000, 1, 0, 700, 64] * 4, 4, seed=8)
+    acc = accel.Accel(L.zones, **L.capacities())
+    sim = fleet.FleetSim(L, seed=8, adversarial=0.2, zero_ratio_frac=0.1)
+    s = current_stream_handle()
+    for _ in range(3):
+        t = to_device(sim.next_interval())
+        acc.run_interval(interval_from_tensors(t, L.sizes(), L.fast_flag()), s)
+    acc.sync(s)
+    with pytest.raises(accel.AccelError):  # no device storage
+        acc.device_ptr("proc_power")
+    with pytest.raises(accel.AccelError):  # not uploadable
+        acc.upload("proc_power", np.zeros(4), 0)
+    pp = acc.download("proc_power")
+    n = pp.size
+    got = device_text(acc, "proc_power", n)
+    for i in range(n):
+        want = write_float(watts(float(pp[i])))
+        assert got[i] == want or (math.isnan(pp[i]) and got[i] == "NaN"), (i, pp[i], got[i], want)
+    # a range not starting at 0 (the derived range is materialised from `first`)
+    first, cnt = 1000 * L.zones + 3, 5000
+    d_out = torch.zeros(cnt * accel.KACC_FMT_WIDTH, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(cnt, dtype=torch.uint8, device="cuda")
+    acc.format_values("proc_power", first, cnt, d_out.data_ptr(), d_len.data_ptr(), s)
+    acc.sync(s)
+    raw, ln = d_out.cpu().numpy().reshape(cnt, -1), d_len.cpu().numpy()
+    for i in range(0, cnt, 7):
+        assert bytes(raw[i, :ln[i]]).decode() == got[first + i]
+    # whole lines over a slot range of the derived table, a zone subset
+    Z, rows0, rows = L.zones, 17, 4000
+    label = 'comm="x",pid="1"'
+    labels = np.frombuffer((label * rows).encode(), np.uint8)
+    d_labels = torch.from_numpy(labels.copy()).cuda()
+    d_loff = torch.from_numpy(np.arange(rows + 1, dtype=np.int64) * len(label)).cuda()
+    zn, zo = ["package", "dram"], [0, 3]
+    d_line_off = torch.zeros(rows * 2 + 1, dtype=torch.int64, device="cuda")
+    args = ("proc_power", "kepler_process_cpu_watts", rows0, rows, zn, d_labels.data_ptr(), d_loff.data_ptr(),
+            d_line_off.data_ptr())
+    total = acc.format_lines(*args, zone_order=zo, stream=s)
+    out = torch.empty(total, dtype=torch.uint8, device="cuda")
+    acc.format_lines(*args, out_ptr=out.data_ptr(), out_cap=total, zone_order=zo, stream=s)
+    acc.sync(s)
+    text = bytes(out.cpu().numpy()).decode()
+    want = "".join(sample_line("kepler_process_cpu_watts", label, zn[j], watts(float(pp[(rows0 + r) * Z + zo[j]])))
+                   for r in range(rows) for j in range(2))
+    assert text == want
     acc.close()

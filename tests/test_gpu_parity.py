@@ -285,7 +285,10 @@ def test_config3_full_size_properties_and_sampled_parity():
         per = len(full) // (layout.n_nodes if kind == "node" else layout.capacities()[f"{kind}_slots"])
         idx = maps[kind]
         got = full.reshape(-1, per)[idx].reshape(-1)
-        np.testing.assert_array_equal(got, ora.state[name], err_msg=name)
+        want = ora.state[name]
+        if name == "proc_node":  # the sample's node indices -> the fleet's
+            want = maps["node"][want]
+        np.testing.assert_array_equal(got, want, err_msg=name)
     # conservation on every node: sum of process power == ActivePower (rel 1e-9),
     # sum of process interval energy within [aE - rows, aE]
     ap = eng.table("node_active_power").reshape(-1, Z)

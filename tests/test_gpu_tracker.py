@@ -72,16 +72,17 @@ FLEETS = [
 
 
 @pytest.mark.parametrize("concurrent", [False, True, "reuse"],
-                         ids=["one-stream", "tracker-beside-interval", "reuse-tracker-first"])
+                         ids=["one-stream", "tracker-second-stream", "reuse-tracker-first"])
 @pytest.mark.parametrize("name,sizes,Z,churn,max_size", FLEETS, ids=[f[0] for f in FLEETS])
 def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurrent):
     """One tracker per node (every node's PowerMonitor owns one): each node keeps its own top
-    max_size, against one Go heap per node.  concurrent: the tracker runs on a second stream
-    beside the interval kernel (it reads only terminated slots, which the interval never
-    writes) and clears only the odd nodes (a per-node export); otherwise every node.
-    "reuse": the join hands terminated slots to new rows at once (KACC_JOIN_REUSE_TERMINATED),
-    so the tracker adds the terminated batch right after the join, before the interval
-    kernel overwrites those slots."""
+    max_size, against one Go heap per node.  The tracker adds an interval's terminated batch
+    after the join and BEFORE the interval kernel, as calculateProcessPower does
+    (process.go:87-99 precede :118-148): a process's power is derived from its ratio and its
+    node's tables (kacc_derive.hpp), which the interval rewrites.  concurrent: the tracker
+    runs on a second stream (the interval waits for it) and clears only the odd nodes (a
+    per-node export); otherwise every node.  "reuse": the join hands terminated slots to new
+    rows at once (KACC_JOIN_REUSE_TERMINATED)."""
     reuse = concurrent == "reuse"
     concurrent = concurrent is True
     layout = fleet.make_layout(len(sizes), sizes, Z, seed=31)
@@ -125,8 +126,6 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
             joined = torch.cuda.Event()
             joined.record(torch.cuda.current_stream())
             s2.wait_event(joined)
-        if not reuse:
-            acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         if it == 3:  # an export happened: Clear() before this interval's adds (process.go:80-84)
             if concurrent:  # only the odd nodes exported
                 mask = (np.arange(layout.n_nodes) % 2).astype(np.int32)
@@ -137,13 +136,12 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
                 tr.clear(ts2)
                 otr.clear()
         tr.add(sm, tk.data_ptr(), ts.data_ptr(), tc.data_ptr(), ts2)
-        if concurrent:  # the next join rewrites the terminated lists the tracker reads
+        if concurrent:  # the interval (and the next join) after the tracker's reads
             torch.cuda.current_stream().wait_stream(s2)
-        if reuse:  # after the tracker read the terminated slots' final values
-            acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
+        acc.run_interval(interval_from_tensors(t, sizes_d, layout.fast_flag()), s)
         acc.sync(s)
-        if reuse:  # the oracle tracker reads the same final values: the tables before this interval
-            pre_e, pre_p = ora.state["proc_energy"].copy(), ora.state["proc_power"].copy()
+        # the oracle tracker reads the same final values: the tables before this interval
+        pre_e, pre_p = ora.state["proc_energy"].copy(), ora.state["proc_power"].copy()
         ora.interval(a_ora, sizes_d)
         # oracle: the same terminated batch (per-node segments), values from the oracle tables
         nodes, kk, ss = [], [], []
@@ -152,8 +150,7 @@ def test_tracker_fleet_matches_go_heap(name, sizes, Z, churn, max_size, concurre
             nodes += [n] * c
             kk += otk[s0:s0 + c].tolist()
             ss += ots[s0:s0 + c].tolist()
-        otr.add_batch(nodes, kk, ss, pre_e if reuse else ora.state["proc_energy"],
-                      pre_p if reuse else ora.state["proc_power"])
+        otr.add_batch(nodes, kk, ss, pre_e, pre_p)
         gk, gn, ge, gp = tr.items()
         order = np.lexsort((gk, gn))
         ok_, on_, oe_, op_ = otr.items()

@@ -90,7 +90,7 @@ def main():
                 torch.cuda.synchronize()
                 per[i].append(round(float(np.mean([x.elapsed_time(y) for x, y in ev])), 4))
         print(json.dumps({"per_context_round_means_ms": per,
-                          "tables": {i: [hex(a2.device_ptr(n)) for n in ("proc_energy", "proc_power")]
+                          "tables": {i: [hex(a2.device_ptr(n)) for n in ("proc_energy", "proc_ratio")]
                                      for i, a2 in enumerate(accs)}}, indent=1))
         return
     modes = ["headline", "b2b", "sync", "partials_before"]
