@@ -79,6 +79,10 @@ def parse():
                          "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
     ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
                     help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
+    ap.add_argument("--totals", choices=["exports", "tables"], default="exports",
+                    help="cluster totals from the interval's exports, reduced on the comm stream while the next "
+                         "interval runs (kacc_allreduce_exports), or from the state tables with the partial sums on "
+                         "the compute stream (kacc_allreduce_namespaces)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -442,13 +446,24 @@ class Workload:
             return t
 
         self.iv_tensors = [make(k) for k in range(n_ivs)]
+        # cluster-total exports (kacc_interval.pod_export / node_export) of each step's last
+        # interval, double-buffered by step parity: step k's totals are reduced on the comm
+        # stream while step k+1 runs (kacc_allreduce_exports)
+        self.exports = args.totals == "exports"
+        self.pex = [torch.zeros(max(sizes["n_pods"], 1) * 2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+        self.nex = [torch.zeros(max(sizes["n_nodes"], 1) * 5 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+        if self.exports:
+            for st in range(n_steps):
+                t = self.iv_tensors[st * K + K - 1]
+                t["pod_export"], t["node_export"] = self.pex[st % 2], self.nex[st % 2]
         # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
         # runs K > 1 fast-node intervals as one launch
         self.flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
         self.ivs = [interval_from_tensors(t, sizes, self.flags) for t in self.iv_tensors]
         self.iv_arrays = [(accel.KaccInterval * K)(*self.ivs[k * K:(k + 1) * K]) for k in range(n_steps)]
         ns_off, ns_slot = layout.namespace_csr()
-        self.ns_t = to_device({"off": ns_off, "slot": ns_slot})
+        _, ns_row = layout.namespace_csr_rows()
+        self.ns_t = to_device({"off": ns_off, "slot": ns_slot, "row": ns_row})
         self.n_ns = len(ns_off) - 1
         # cluster totals double-buffered: step k's all-reduce (comm stream) overlaps step k+1's
         # interval; buffer k % 2 is rewritten only after the all-reduce of step k-2 is done
@@ -481,14 +496,26 @@ def measure(args, w, rank, world, stream, comm_stream):
     acc, cl = w.acc, w.cluster
     cstream = ctypes.c_void_p(stream)
     P = lambda vals: (ctypes.c_void_p * 1)(*[ctypes.c_void_p(v) for v in vals])  # noqa: E731
-    ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
-                P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]), P([w.nd_p[b].data_ptr()]), P([stream]),
-                P([comm_stream.cuda_stream])) for b in range(2)]
+    U = lambda v: (ctypes.c_uint32 * 1)(v)  # noqa: E731
+    if w.exports:  # everything after the interval on the comm stream, from the step's exports
+        ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["row"].data_ptr()]), U(w.sizes["n_pods"]),
+                    P([w.pex[b].data_ptr()]), U(w.sizes["n_nodes"]), P([w.nex[b].data_ptr()]),
+                    P([w.ns_e[b].data_ptr()]), P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]),
+                    P([w.nd_p[b].data_ptr()]), P([stream]), P([comm_stream.cuda_stream])) for b in range(2)]
+        reduce_fn = lib.kacc_allreduce_exports
+    else:  # partial sums from the state tables on the compute stream, the all-reduce on the comm stream
+        ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
+                    P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]), P([w.nd_p[b].data_ptr()]), P([stream]),
+                    P([comm_stream.cuda_stream])) for b in range(2)]
+        reduce_fn = lib.kacc_allreduce_namespaces
     done = [torch.cuda.Event(), torch.cuda.Event()]
     used = [False, False]
     compute = torch.cuda.current_stream()
 
     def step(k, ev=None):
+        b = k % 2
+        if used[b]:  # stream-level wait for step k-2's totals (its buffers are reused; no host sync)
+            compute.wait_event(done[b])
         if ev is not None:
             ev[0].record()
         rc = lib.kacc_run_intervals(acc.ctx, w.iv_arrays[k], K, cstream)
@@ -496,10 +523,7 @@ def measure(args, w, rank, world, stream, comm_stream):
             acc._check(rc)
         if ev is not None:
             ev[1].record()
-        b = k % 2
-        if used[b]:  # stream-level wait for the all-reduce of step k-2 (no host sync)
-            compute.wait_event(done[b])
-        rc = lib.kacc_allreduce_namespaces(cl.handle, w.n_ns, *ns_args[b])
+        rc = reduce_fn(cl.handle, w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
         done[b].record(comm_stream)
@@ -630,6 +654,9 @@ def main():
             "namespaces": w.n_ns,
             "fragment_slots": args.fragment,
             "shard_of": args.shard_of,
+            "cluster_totals": ("kacc_allreduce_exports (interval exports; partial sums + RCCL on the comm stream)"
+                               if args.totals == "exports" else
+                               "kacc_allreduce_namespaces (partial sums from the tables on the compute stream)"),
             "parallelism": f"node-sharded x{world} (shard.plan_node_ranges); namespace + cluster node "
                            f"totals all-reduced over RCCL by kacc_allreduce_namespaces",
         },

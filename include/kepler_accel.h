@@ -190,6 +190,21 @@ typedef struct kacc_interval {
   /* pods [n_pods] */
   const uint32_t *pod_ctr_end;
   const uint32_t *pod_slot;
+  /* Optional OUTPUTS (device pointers, NULL = off): this interval's values for
+   * the cluster totals, written in batch order by the interval's own kernels
+   * (coalesced), so kacc_allreduce_exports reduces them on another stream
+   * while the next interval runs (double-buffer them across intervals):
+   *   pod_export  [n_pods * 2Z] u64 words: batch pod q's EnergyTotal[Z], then
+   *               the bits of its Power[Z] (zeros for a pod whose slot is out
+   *               of range);
+   *   node_export [n_nodes * 5Z] u64 words: node n's ActiveEnergyTotal[Z],
+   *               IdleEnergyTotal[Z], then the bits of Power[Z], ActivePower[Z],
+   *               IdlePower[Z] (monitor/types.go:27-40).
+   * Every node of the batch is exported, a skipped node (read error) with its
+   * unchanged values.  The pinned batch path passes the view's pointers
+   * through as device pointers.                                             */
+  uint64_t *pod_export;
+  uint64_t *node_export;
 } kacc_interval;
 
 /* Device-resident state / result tables.  [n*Z+z] tables are node-major or
@@ -392,6 +407,24 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
                               double *const *out_power, uint64_t *const *out_node_energy,
                               double *const *out_node_power, void *const *streams,
                               void *const *comm_streams);
+/* The same cluster totals from the interval's exports (kacc_interval.pod_export
+ * / node_export) instead of the state tables: nothing runs on streams[s]
+ * except an event record — the partial sums run on comm_streams[s] after the
+ * work queued on streams[s] so far (the interval that wrote the exports),
+ * then the all-reduce, so the next interval on streams[s] overlaps all of it.
+ * ns_pod_off[s] / ns_pod_row[s]: namespace k owns the shard's batch pod ROWS
+ * ns_pod_row[ns_pod_off[k] .. ns_pod_off[k+1]) (the CSR of
+ * kacc_namespace_totals with pod rows for slots: the same sum order, so the
+ * results are bit-identical to kacc_allreduce_namespaces); n_pods[s] / n_nodes[s]
+ * (HOST): rows of the exports.  The exports must stay untouched until
+ * comm_streams[s] has passed this call (kacc_allreduce_exports reads them
+ * asynchronously): a caller alternates two export buffers.                  */
+int kacc_allreduce_exports(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                           const uint32_t *const *ns_pod_row, const uint32_t *n_pods,
+                           const uint64_t *const *pod_export, const uint32_t *n_nodes,
+                           const uint64_t *const *node_export, uint64_t *const *out_energy,
+                           double *const *out_power, uint64_t *const *out_node_energy,
+                           double *const *out_node_power, void *const *streams, void *const *comm_streams);
 /* Cluster pod gather: shard s contributes n_pods[s] (HOST) pods, its slots
  * pod_slot[s] (device), in that order; every local shard receives all pods of
  * the cluster in (rank, shard) order — energy u64 / power f64 [total*Z] into

@@ -136,6 +136,7 @@ EXPORTS = [
     "kacc_cluster_rccl",
     "kacc_cluster_info",
     "kacc_allreduce_namespaces",
+    "kacc_allreduce_exports",
     "kacc_gather_pods",
     "kacc_last_error_copy",
     "kacc_intervals_bytes",
@@ -224,6 +225,10 @@ class KaccShape(ctypes.Structure):
     _fields_ = [(n, c_uint32) for n in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods", "intervals")]
 
 
+# optional per-interval OUTPUT arrays (device): the cluster-total exports
+INTERVAL_OUTPUTS = ["pod_export", "node_export"]
+
+
 class KaccInterval(ctypes.Structure):
     _fields_ = [
         ("n_nodes", c_uint32),
@@ -232,7 +237,7 @@ class KaccInterval(ctypes.Structure):
         ("n_vms", c_uint32),
         ("n_pods", c_uint32),
         ("flags", c_uint32),
-    ] + [(name, c_void_p) for name in INTERVAL_ARRAYS]
+    ] + [(name, c_void_p) for name in INTERVAL_ARRAYS + INTERVAL_OUTPUTS]
 
 
 class AccelError(RuntimeError):
@@ -285,6 +290,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_cluster_info.argtypes = [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]
     lib.kacc_cluster_rccl.argtypes = [POINTER(c_int), c_char_p, ctypes.c_size_t]
     lib.kacc_allreduce_namespaces.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 8
+    lib.kacc_allreduce_exports.argtypes = [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_uint32),
+                                           POINTER(c_void_p), POINTER(c_uint32)] + [POINTER(c_void_p)] * 7
     lib.kacc_gather_pods.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_void_p), c_uint64, POINTER(c_void_p),
                                      POINTER(c_void_p), POINTER(c_uint64), POINTER(c_uint64), POINTER(c_void_p)]
     lib.kacc_batch_submit.argtypes = [c_void_p, c_void_p]
@@ -424,6 +431,9 @@ def make_interval(arrays: dict, sizes: dict, flags: int = 0, ptr=None) -> KaccIn
             setattr(it, name, None)
         else:
             setattr(it, name, ptr(a) or None)  # empty torch tensors give 0 -> NULL
+    for name in INTERVAL_OUTPUTS:
+        a = arrays.get(name)
+        setattr(it, name, (ptr(a) or None) if a is not None else None)
     return it
 
 
@@ -867,6 +877,22 @@ class Cluster:
         node = out_node_energy is not None
         self._check(self.lib.kacc_allreduce_namespaces(
             self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_slot) if n_ns else None,
+            _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
+            _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
+            _ptrs(streams) if streams else None, _ptrs(comm_streams) if comm_streams else None))
+
+    def allreduce_exports(self, n_ns: int, ns_pod_off, ns_pod_row, n_pods, pod_export, out_energy, out_power,
+                          n_nodes=None, node_export=None, out_node_energy=None, out_node_power=None, streams=None,
+                          comm_streams=None) -> None:
+        """kacc_allreduce_exports: per-shard lists of device pointers (n_pods / n_nodes: ints);
+        everything runs on comm_streams after the work queued on streams."""
+        n = len(self.shards)
+        node = out_node_energy is not None
+        u32 = lambda v: (c_uint32 * n)(*v)  # noqa: E731
+        self._check(self.lib.kacc_allreduce_exports(
+            self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_row) if n_ns else None,
+            u32(n_pods) if n_ns else None, _ptrs(pod_export) if n_ns else None,
+            u32(n_nodes) if node else None, _ptrs(node_export) if node else None,
             _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
             _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
             _ptrs(streams) if streams else None, _ptrs(comm_streams) if comm_streams else None))

@@ -519,6 +519,60 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
   return KACC_OK;
 }
 
+int kacc_allreduce_exports(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                           const uint32_t *const *ns_pod_row, const uint32_t *n_pods,
+                           const uint64_t *const *pod_export, const uint32_t *n_nodes,
+                           const uint64_t *const *node_export, uint64_t *const *out_energy,
+                           double *const *out_power, uint64_t *const *out_node_energy,
+                           double *const *out_node_power, void *const *streams, void *const *comm_streams) {
+  if (!c) return KACC_EINVAL;
+  kacc_ctx *c0 = c->shards[0];
+  const size_t ns = c->shards.size();
+  const uint64_t Z = c->zones;
+  const bool nodes = out_node_energy && out_node_power;
+  if ((out_node_energy != nullptr) != (out_node_power != nullptr))
+    return kacc_fail(c0, KACC_EINVAL, "node totals need both output arrays");
+  if (n_ns && (!ns_pod_off || !ns_pod_row || !n_pods || !pod_export || !out_energy || !out_power))
+    return kacc_fail(c0, KACC_EINVAL, "NULL argument");
+  if (nodes && (!n_nodes || !node_export)) return kacc_fail(c0, KACC_EINVAL, "node totals need node exports");
+  for (size_t s = 0; s < ns; ++s) {
+    if (n_ns && (!ns_pod_off[s] || !ns_pod_row[s] || !out_energy[s] || !out_power[s] || (n_pods[s] && !pod_export[s])))
+      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL namespace / pod export array", s);
+    if (nodes && (!out_node_energy[s] || !out_node_power[s] || (n_nodes[s] && !node_export[s])))
+      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL node-total / node export array", s);
+  }
+  // everything on the comm streams, after the work queued on the compute streams
+  void *const *cs = comm_streams ? comm_streams : streams;
+  for (size_t s = 0; s < ns; ++s) {
+    kacc_ctx *x = c->shards[s];
+    hipStream_t a = shard_stream(c, streams, s), b = shard_stream(c, cs, s);
+    KACC_HIP(c0, hipSetDevice(x->device));
+    if (a != b) {
+      KACC_HIP(c0, hipEventRecord(c->events[s], a));
+      KACC_HIP(c0, hipStreamWaitEvent(b, c->events[s], 0));
+    }
+    // 1. partial vectors of every shard from its exports
+    const int rc = kacc_internal_export_partials(
+        x, n_ns, n_ns ? ns_pod_off[s] : nullptr, n_ns ? ns_pod_row[s] : nullptr, n_ns ? pod_export[s] : nullptr,
+        n_ns ? n_pods[s] : 0, nodes ? node_export[s] : nullptr, nodes ? n_nodes[s] : 0, n_ns ? out_energy[s] : nullptr,
+        n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr, b);
+    if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
+  }
+  if (c->nranks == 1 && ns == 1) return KACC_OK;
+  // 2. shards of one GPU, 3. across GPUs, 4. back to every shard — all on the comm streams
+  int rc = KACC_OK;
+  if (n_ns && (rc = local_combine(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
+  if (nodes && (rc = local_combine(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
+  ReduceReq reqs[2];
+  int n_reqs = 0;
+  if (n_ns) reqs[n_reqs++] = ReduceReq{out_energy, n_ns * Z, out_power, n_ns * Z};
+  if (nodes) reqs[n_reqs++] = ReduceReq{out_node_energy, 2 * Z, out_node_power, 3 * Z};
+  if (n_reqs && (rc = allreduce(c, cs, reqs, n_reqs)) != KACC_OK) return rc;
+  if (n_ns && (rc = local_broadcast(c, cs, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
+  if (nodes && (rc = local_broadcast(c, cs, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
+  return KACC_OK;
+}
+
 int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *const *pod_slot, uint64_t out_cap,
                      uint64_t *const *out_energy, double *const *out_power, uint64_t *total, uint64_t *first,
                      void *const *streams) {

@@ -312,6 +312,43 @@ __device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const
   }
 }
 
+// Cluster-total exports (kacc_interval.pod_export / node_export): what a pod /
+// node contributes to the cluster totals, in batch order, written by the
+// interval's own kernels so that kacc_allreduce_exports reduces them on
+// another stream while the next interval runs.  Pod row q: EnergyTotal[Z] then
+// the bits of Power[Z] (zeros for a pod whose slot is out of range).
+template <int Z>
+__device__ __forceinline__ void export_pod(const kacc_interval &b, uint32_t q, const uint64_t (&E)[Z],
+                                           const double (&P)[Z]) {
+  if (!b.pod_export) return;
+  uint64_t *o = b.pod_export + static_cast<uint64_t>(q) * (2 * Z);
+  store_row<Z, true, uint64_t>(o, 0, E);
+  store_row<Z, true, double>(reinterpret_cast<double *>(o), 1, P);
+}
+template <int Z>
+__device__ __forceinline__ void export_pod_zero(const kacc_interval &b, uint32_t q) {
+  uint64_t E[Z];
+  double P[Z];
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    E[z] = 0;
+    P[z] = 0.0;
+  }
+  export_pod<Z>(b, q, E, P);
+}
+// Node n, zone z: ActiveEnergyTotal, IdleEnergyTotal, Power, ActivePower, IdlePower.
+template <int Z>
+__device__ __forceinline__ void export_node_zone(const kacc_interval &b, uint32_t n, uint32_t z, uint64_t at,
+                                                 uint64_t it, double p, double ap, double ip) {
+  if (!b.node_export) return;
+  uint64_t *o = b.node_export + static_cast<uint64_t>(n) * (5 * Z) + z;
+  o[0] = at;
+  o[Z] = it;
+  o[2 * Z] = static_cast<uint64_t>(__double_as_longlong(p));
+  o[3 * Z] = static_cast<uint64_t>(__double_as_longlong(ap));
+  o[4 * Z] = static_cast<uint64_t>(__double_as_longlong(ip));
+}
+
 // One aggregate row (container / VM / pod): read-modify-write of its slot.
 template <int Z, bool NT>
 __device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, double delta,
@@ -461,20 +498,24 @@ __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState
   const uint64_t abs_e = b.zone_energy[i];
   uint64_t active;
   double p = 0.0, ap = 0.0, ip = 0.0;
+  uint64_t at, it;
   if (first) {  // firstNodeRead, node.go:111-128
     active = go_f64_to_u64(u2f(abs_e) * ratio);
-    st.node_active_total[i] = active;
-    st.node_idle_total[i] = abs_e - active;
+    at = active;
+    it = abs_e - active;
   } else {  // calculateNodePower, node.go:50-68
     const double dt = go_duration_seconds(go_sub_mono(b.node_ts_ns[n], st.node_ts[n]));
     const uint64_t delta = energy_delta(abs_e, st.node_energy_total[i], b.zone_max[i]);
     active = go_f64_to_u64(u2f(delta) * ratio);
-    st.node_active_total[i] = st.node_active_total[i] + active;
-    st.node_idle_total[i] = st.node_idle_total[i] + (delta - active);
+    at = st.node_active_total[i] + active;
+    it = st.node_idle_total[i] + (delta - active);
     p = u2f(delta) / dt;
     ap = p * ratio;
     ip = p - ap;
   }
+  st.node_active_total[i] = at;
+  st.node_idle_total[i] = it;
+  export_node_zone<Z>(b, n, static_cast<uint32_t>(z), at, it, p, ap, ip);
   st.node_energy_total[i] = abs_e;
   st.node_active_energy[i] = active;
   st.node_power[i] = p;
@@ -489,6 +530,34 @@ __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState
 struct NodeRanges {
   uint32_t p0, p1, c0, c1, v0, v1, q0, q1;
 };
+
+// A skipped node (read error) keeps its snapshot (node.go:39-44): its exports
+// are its unchanged table values, lanes [lane, +nlanes) of the node's workers.
+template <int Z>
+__device__ __forceinline__ void export_skipped(const kacc_interval &b, const DevState &st, uint32_t n,
+                                               const NodeRanges &r, uint32_t lane, uint32_t nlanes) {
+  if (b.node_export) {
+    for (uint32_t z = lane; z < static_cast<uint32_t>(Z); z += nlanes) {
+      const uint64_t i = static_cast<uint64_t>(n) * Z + z;
+      export_node_zone<Z>(b, n, z, st.node_active_total[i], st.node_idle_total[i], st.node_power[i],
+                          st.node_active_power[i], st.node_idle_power[i]);
+    }
+  }
+  if (b.pod_export) {
+    for (uint32_t q = r.q0 + lane; q < r.q1; q += nlanes) {
+      const uint64_t sl = b.pod_slot[q] & KACC_SLOT_MASK;
+      if (sl >= st.pod_slots) {
+        export_pod_zero<Z>(b, q);
+        continue;
+      }
+      uint64_t E[Z];
+      double P[Z];
+      load_row<Z>(st.pod_energy, sl, E);
+      load_row_f64<Z>(st.pod_power, sl, P);
+      export_pod<Z>(b, q, E, P);
+    }
+  }
+}
 
 // Row ranges of node n, clamped so a malformed batch cannot fault.
 __device__ __forceinline__ NodeRanges clamp_ranges(const kacc_interval &b, const DevState &st, NodeRanges r,
@@ -583,6 +652,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   if (status & KACC_NODE_READ_ERROR) {
     // node.go:39-44 -> calculatePower fails, previous snapshot kept.
     if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+    if (b.pod_export || b.node_export)
+      export_skipped<Z>(b, st, n, clamp_ranges(b, st, raw, tid), static_cast<uint32_t>(tid), kThreads);
     return;
   }
   const NodeRanges rg = clamp_ranges(b, st, raw, tid);
@@ -842,7 +913,10 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
   auto aggregate_out = [&]() {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
-    if (!a_ok) return;
+    if (!a_ok) {
+      if (role == 3) export_pod_zero<Z>(b, q0 + j);
+      return;
+    }
     if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), a_s, a_prev);
     uint64_t E[Z];
     double P[Z];
@@ -850,6 +924,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
                      a_prev, E, P);
     store_row<Z, kNtAgg, uint64_t>(a_energy(), a_s, E);
     store_row<Z, kNtAgg, double>(a_power(), a_s, P);
+    if (role == 3) export_pod<Z>(b, q0 + j, E, P);
   };
   if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
@@ -1257,6 +1332,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     }
     if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44: previous snapshot kept
       if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+      if (b.pod_export || b.node_export) export_skipped<Z>(b, st, n, rg, tid, kThreads);
     } else if (!fits) {  // the caller's KACC_F_FAST_NODES promise was wrong
       if (tid == 0) raise_err(st.err, kErrBigNode);
     } else {
@@ -1420,6 +1496,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         st.node_power[zi] = z_p;
         st.node_active_power[zi] = z_ap;
         st.node_idle_power[zi] = z_ip;
+        export_node_zone<Z>(b, n, tid, c_atot, c_itot, z_p, z_ap, z_ip);
       }
       const Attr<Z> a = make_attr<Z>(sh);
       if (tid == 0) {
@@ -1446,9 +1523,12 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         double *ap = role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
         store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, uint64_t>(ae, a_s, E);
         store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, double>(ap, a_s, P);
+        if (role == 3) export_pod<Z>(b, rg.q0 + (tid - nc - nv), E, P);
 #pragma unroll
         for (int z = 0; z < Z; ++z) c_aE[z] = E[z];
         c_atotal = a_total;
+      } else if (role == 3) {
+        export_pod_zero<Z>(b, rg.q0 + (tid - nc - nv));
       }
       c_role = a_ok ? role : 0u;
       c_aw = a_ok ? a_w : 0xffffffffu;
@@ -1585,6 +1665,8 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   node_words(b, n, status, raw);
   if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44
     if (lane == 0) st.node_status[n] = KACC_NODE_SKIPPED;
+    if (b.pod_export || b.node_export)
+      export_skipped<Z>(b, st, n, clamp_ranges(b, st, raw, static_cast<int>(lane)), lane, 64u);
     return;
   }
   const NodeRanges rg = clamp_ranges(b, st, raw, static_cast<int>(lane));
@@ -1844,15 +1926,20 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
-    const uint32_t role = role_of(lane + 64u * h);
+    const uint32_t i = lane + 64u * h, role = role_of(i);
     const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
-    if (role == 0 || a_s >= cap_of(role)) continue;
+    if (role == 0) continue;
+    if (a_s >= cap_of(role)) {
+      if (role == 3) export_pod_zero<Z>(b, q0 + index_of(i));
+      continue;
+    }
     uint64_t E[Z];
     double P[Z];
     attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h], (a_w[h] & KACC_SLOT_NEW) != 0,
                      a_prev[h], E, P);
     store_row<Z, kNT && kNtAggStores, uint64_t>(energy_of(role), a_s, E);
     store_row<Z, kNT && kNtAggStores, double>(power_of(role), a_s, P);
+    if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P);
   }
   auto attr_batch = [&](int kb) {  // process.go:118-148
 #pragma unroll
@@ -2350,7 +2437,17 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
       }
     }
     // ---- E: aggregates, then process rows (process.go:118-148) ------------------
-    if (a_ok && !defer) agg_out(a_role, a_w, a_delta, a_prev);
+    if (a_ok && !defer) {
+      const uint64_t s = a_w & KACC_SLOT_MASK;
+      uint64_t E[Z];
+      double P[Z];
+      attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
+      store_row<Z, kNT, uint64_t>(energy_of(a_role), s, E);
+      store_row<Z, kNT, double>(power_of(a_role), s, P);
+      if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P);
+    } else if (a_role == 3 && !a_ok) {
+      export_pod_zero<Z>(b, qb + (utid - ncv));
+    }
     if (defer && a_ok) {
       const uint32_t i = atomicAdd(st.defer_ctr, 1u);
       if (i < st.defer_cap)
@@ -2392,6 +2489,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
       const bool ok = s < cap_of(role);
       if (!ok) {
         raise_err(st.err, kErrSlot);
+        if (role == 3) export_pod_zero<Z>(b, qb + (j - ncv));
         continue;
       }
       if (role == 3) {
@@ -2474,6 +2572,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     attribute_row<Z>(a, a.live_pod, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
     store_row<Z, kNT, uint64_t>(st.pod_energy, sl, E);
     store_row<Z, kNT, double>(st.pod_power, sl, P);
+    export_pod<Z>(b, q, E, P);
   }
 }
 
@@ -2482,7 +2581,10 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
 // kNsUnroll at a time, adds in order), then the 16 lane sums are halved
 // pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
 // f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
-template <int Z>
+// kW: 8-byte words between consecutive rows — Z for the state tables (rows =
+// pod slots, energy and power tables apart), 2Z for an interval's pod export
+// (rows = batch pod rows, energy then power bits in one record).
+template <int Z, int kW = Z>
 __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
                                                 const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
                                                 const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
@@ -2509,8 +2611,8 @@ __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, con
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
       const uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
-      load_row<Z>(pe, at, er[u]);
-      load_row_f64<Z>(pp, at, pr[u]);
+      load_row<Z>(pe + at * kW, 0, er[u]);
+      load_row_f64<Z>(pp + at * kW, 0, pr[u]);
     }
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
@@ -2561,13 +2663,14 @@ struct NodeTotalsArgs {
   uint32_t npb;       // nodes per block (a multiple of kBlock)
   const uint64_t *active_total, *idle_total;
   const double *power, *active_power, *idle_power;
+  const uint64_t *node_export;  // else the five tables: an interval's node export [n_nodes][5Z]
   uint64_t *part;     // [blocks][5Z] raw 8-byte words: 2Z u64 then 3Z f64
   uint32_t *done;     // block counter, re-armed by the last block
   uint64_t *out_e;
   double *out_p;
 };
 
-template <int Z>
+template <int Z, int kW = Z>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
                                                                   const uint32_t *__restrict__ slots,
@@ -2576,7 +2679,7 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
                                                                   uint64_t *out_e, double *out_p, uint32_t *err,
                                                                   const NodeTotalsArgs na) {
   if (blockIdx.x < ns_blocks) {
-    namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+    namespace_block<Z, kW>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
     return;
   }
   constexpr int kV = 5 * Z;
@@ -2594,11 +2697,21 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
   for (uint64_t n = static_cast<uint64_t>(b) * na.npb + tid; n < n_end; n += kBlock) {
     uint64_t a[Z], i[Z];
     double pw[Z], ap[Z], ip[Z];
-    load_row<Z>(na.active_total, n, a);
-    load_row<Z>(na.idle_total, n, i);
-    load_row_f64<Z>(na.power, n, pw);
-    load_row_f64<Z>(na.active_power, n, ap);
-    load_row_f64<Z>(na.idle_power, n, ip);
+    if (na.node_export) {  // the same values, from the interval's node export
+      const uint64_t *x = na.node_export + n * (5 * Z);
+      const double *xd = reinterpret_cast<const double *>(x);
+      load_row<Z>(x, 0, a);
+      load_row<Z>(x, 1, i);
+      load_row_f64<Z>(xd, 2, pw);
+      load_row_f64<Z>(xd, 3, ap);
+      load_row_f64<Z>(xd, 4, ip);
+    } else {
+      load_row<Z>(na.active_total, n, a);
+      load_row<Z>(na.idle_total, n, i);
+      load_row_f64<Z>(na.power, n, pw);
+      load_row_f64<Z>(na.active_power, n, ap);
+      load_row_f64<Z>(na.idle_power, n, ip);
+    }
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
       ve[z] += a[z];
@@ -2854,15 +2967,23 @@ void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const 
                      ctx->d_err);
 }
 
+// pod_export NULL: the namespace sums gather the state tables by pod slot;
+// else the interval's pod export by batch pod row (n_pods rows)
 template <int Z>
 void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, kacc_ctx *ctx,
                              uint64_t *out_e, double *out_p, const kacc::NodeTotalsArgs &na, uint32_t node_blocks,
-                             hipStream_t st) {
+                             hipStream_t st, const uint64_t *pod_export = nullptr, uint64_t n_pods = 0) {
   const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
   const uint32_t ns_blocks = (n_ns + per_block - 1) / per_block;
-  hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
-                     ns_blocks, n_ns, off, slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
-                     (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p, ctx->d_err, na);
+  if (pod_export)
+    hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z, 2 * Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0,
+                       st, ns_blocks, n_ns, off, slots, pod_export, reinterpret_cast<const double *>(pod_export + Z),
+                       n_pods, out_e, out_p, ctx->d_err, na);
+  else
+    hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
+                       ns_blocks, n_ns, off, slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
+                       (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p, ctx->d_err,
+                       na);
 }
 
 // Chunk-item list sized for the worst case of a batch (every node oversized,
@@ -3483,6 +3604,8 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
     dv[k].n_vms = h.n_vms;
     dv[k].n_pods = h.n_pods;
     dv[k].flags = (h.flags & ~KACC_F_TRUSTED_LAYOUT) | (h.n_nodes ? node_size_flags(h) : 0u);
+    dv[k].pod_export = h.pod_export;  // device outputs the caller owns, passed through
+    dv[k].node_export = h.node_export;
     for (const BatchField &f : kBatchFields)  // honour optional arrays the caller switched off
       if (!field_ptr(h, f)) field_ptr(dv[k], f) = nullptr;
     max_nodes = std::max<uint64_t>(max_nodes, h.n_nodes);
@@ -3628,14 +3751,24 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, con
 int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
                                    uint64_t *out_energy, double *out_power, uint64_t *node_energy, double *node_power,
                                    void *stream) {
+  return kacc_internal_export_partials(ctx, n_ns, off, slots, nullptr, 0, nullptr, 0, out_energy, out_power,
+                                       node_energy, node_power, stream);
+}
+
+int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *rows,
+                                  const uint64_t *pod_export, uint64_t n_pods, const uint64_t *node_export,
+                                  uint64_t n_nodes, uint64_t *out_energy, double *out_power, uint64_t *node_energy,
+                                  double *node_power, void *stream) {
   if (!ctx) return KACC_EINVAL;
-  if (n_ns && (!off || !slots || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
+  if (n_ns && (!off || !rows || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint64_t Z = ctx->cfg.zones;
   // the nodes of the last interval run on the context (a node that left the
-  // batch stops exporting, so PromQL's sum drops it; a fresh context sums none)
-  const uint64_t live = std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
+  // batch stops exporting, so PromQL's sum drops it; a fresh context sums none);
+  // from an export: its n_nodes rows
+  const uint64_t live = node_export ? n_nodes : std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
+  const uint32_t *slots = rows;
   // at most kNodeBlocksMax blocks of a multiple of kBlock nodes each
   const uint64_t groups = (live + kacc::kBlock - 1) / kacc::kBlock;
   const uint32_t npb = static_cast<uint32_t>(
@@ -3663,18 +3796,23 @@ int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t 
   na.part = reinterpret_cast<uint64_t *>(static_cast<char *>(ctx->d_node_part) + 16);
   na.out_e = node_energy;
   na.out_p = node_power;
+  na.node_export = node_export;
   if (!n_ns && !node_blocks) return KACC_OK;
   (void)hipGetLastError();
+#define KACC_PARTIALS(Z_)                                                                                  \
+  launch_cluster_partials<Z_>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st, pod_export, \
+                              n_pods)
   switch (ctx->cfg.zones) {
-    case 1: launch_cluster_partials<1>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 2: launch_cluster_partials<2>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 3: launch_cluster_partials<3>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 4: launch_cluster_partials<4>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 5: launch_cluster_partials<5>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 6: launch_cluster_partials<6>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    case 7: launch_cluster_partials<7>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
-    default: launch_cluster_partials<8>(n_ns, off, slots, ctx, out_energy, out_power, na, node_blocks, st); break;
+    case 1: KACC_PARTIALS(1); break;
+    case 2: KACC_PARTIALS(2); break;
+    case 3: KACC_PARTIALS(3); break;
+    case 4: KACC_PARTIALS(4); break;
+    case 5: KACC_PARTIALS(5); break;
+    case 6: KACC_PARTIALS(6); break;
+    case 7: KACC_PARTIALS(7); break;
+    default: KACC_PARTIALS(8); break;
   }
+#undef KACC_PARTIALS
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }

@@ -131,6 +131,13 @@ class FleetLayout:
         np.cumsum(counts, out=off[1:])
         return off, self.pod_slot[order].astype(np.uint32)
 
+    def namespace_csr_rows(self):
+        """ns_pod_off [n_ns+1], ns_pod_row [Q]: the same grouping over batch pod ROWS (the
+        index space of an interval's pod export, kacc_allreduce_exports): the same order."""
+        order = np.argsort(self.pod_ns, kind="stable")
+        off, _ = self.namespace_csr()
+        return off, order.astype(np.uint32)
+
     def node_order_heaviest_first(self) -> np.ndarray:
         rows = np.diff(self.proc_off.astype(np.int64))
         return np.argsort(-rows, kind="stable").astype(np.uint32)

@@ -53,7 +53,7 @@ def test_abi_version(lib):
 
 def test_struct_layout_matches_header(tmp_path):
     c = tmp_path / "layout.c"
-    fields = ["n_nodes", "flags"] + accel.INTERVAL_ARRAYS
+    fields = ["n_nodes", "flags"] + accel.INTERVAL_ARRAYS + accel.INTERVAL_OUTPUTS
     body = "\n".join(f'printf("%zu\\n", offsetof(kacc_interval, {f}));' for f in fields)
     c.write_text(f"""
 #include <stddef.h>

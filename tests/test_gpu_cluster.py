@@ -320,3 +320,125 @@ def test_cluster_node_totals_follow_the_live_nodes():
     assert not np.array_equal(we, want(L.n_nodes)[0])  # the 3 nodes that left counted before
     cl.close()
     acc.close()
+
+
+EXPORT_FLEETS = [
+    ("fast-z4", dict(n_nodes=40, procs_per_node=[2000, 300, 1, 0, 1500] * 8, zones=4, shuffle_slots=True), 0),
+    ("small-z2", dict(n_nodes=64, procs_per_node=[500, 64, 3, 0] * 16, zones=2), 0),
+    ("big-z4", dict(n_nodes=6, procs_per_node=[10000, 3000, 12, 0, 2049, 700], zones=4, vm_frac=0.02,
+                    procs_per_vm=2), 0),
+    ("carry-z2", dict(n_nodes=48, procs_per_node=[1000, 700, 1, 0, 1024, 513] * 8, zones=2), 5),
+]
+
+
+@pytest.mark.parametrize("name,kw,K", EXPORT_FLEETS, ids=[f[0] for f in EXPORT_FLEETS])
+def test_interval_exports_match_tables_and_totals(name, kw, K):
+    """kacc_interval.pod_export / node_export, written by every kernel shape (workgroup per
+    node, wavefront per node, big-node chunks + deferred pods, the K-interval carry kernel)
+    == the state tables after the interval (a skipped node: its unchanged values; a pod with
+    an out-of-range slot: zeros); kacc_allreduce_exports on the comm stream ==
+    kacc_allreduce_namespaces from the tables, bit for bit (same sum order)."""
+    L = fleet.make_layout(seed=19, **kw)
+    Z = L.zones
+    acc = accel.Accel(Z, **L.capacities())
+    sim = fleet.FleetSim(L, seed=19, churn=0.03, read_error_frac=0.15, adversarial=0.1,
+                         max_energy=fleet.MAX_ENERGY_FAKE)
+    s = current_stream_handle()
+    flags = L.fast_flag()
+    if K:
+        flags = (flags & ~accel.KACC_F_SMALL_NODES) | accel.KACC_F_NODE_SLOT_RANGES
+    pex = [torch.zeros(max(L.n_pods, 1) * 2 * Z, dtype=torch.int64, device="cuda") for _ in range(max(K, 1))]
+    nex = [torch.zeros(L.n_nodes * 5 * Z, dtype=torch.int64, device="cuda") for _ in range(max(K, 1))]
+    keep = []
+    for it in range(3):
+        ivs = [sim.next_interval() for _ in range(max(K, 1))]
+        descs = []
+        for k, a in enumerate(ivs):
+            t = to_device(a)
+            t["pod_export"], t["node_export"] = pex[k], nex[k]
+            keep.append(t)
+            descs.append(interval_from_tensors(t, L.sizes(), flags))
+        acc.run_intervals(descs, s)
+        acc.sync(s)
+    # the last interval's exports against the tables
+    last = ivs[-1]
+    pe = pex[-1].cpu().numpy().view(np.uint64).reshape(-1, 2 * Z)[: L.n_pods]
+    ne = nex[-1].cpu().numpy().view(np.uint64).reshape(-1, 5 * Z)
+    st = {t: acc.download(t) for t in ("pod_energy", "pod_power", "node_active_total", "node_idle_total",
+                                       "node_power", "node_active_power", "node_idle_power")}
+    slots = (last["pod_slot"] & np.uint32(accel.KACC_SLOT_MASK)).astype(np.int64)
+    np.testing.assert_array_equal(pe[:, :Z], st["pod_energy"].reshape(-1, Z)[slots])
+    np.testing.assert_array_equal(pe[:, Z:], st["pod_power"].reshape(-1, Z)[slots].view(np.uint64))
+    want_ne = np.concatenate([st["node_active_total"].reshape(-1, Z), st["node_idle_total"].reshape(-1, Z)]
+                             + [st[t].reshape(-1, Z).view(np.uint64) for t in ("node_power", "node_active_power",
+                                                                                "node_idle_power")], axis=1)
+    np.testing.assert_array_equal(ne, want_ne)
+    assert (last["node_status"] & accel.KACC_NODE_READ_ERROR).any()  # skipped nodes were exported too
+    # cluster totals from the exports (comm stream) == from the tables
+    cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
+    n_ns = L.n_namespaces
+    off, slots_ns = L.namespace_csr()
+    _, rows_ns = L.namespace_csr_rows()
+    d = to_device({"o": off, "s": slots_ns, "r": rows_ns})
+    outs = [[torch.zeros(n, dtype=dt, device="cuda") for n, dt in ((n_ns * Z, torch.int64), (n_ns * Z, torch.float64),
+                                                                  (2 * Z, torch.int64), (3 * Z, torch.float64))]
+            for _ in range(2)]
+    cl.allreduce_namespaces(n_ns, [d["o"].data_ptr()], [d["s"].data_ptr()], [outs[0][0].data_ptr()],
+                            [outs[0][1].data_ptr()], [outs[0][2].data_ptr()], [outs[0][3].data_ptr()], streams=[s])
+    comm = torch.cuda.Stream()
+    cl.allreduce_exports(n_ns, [d["o"].data_ptr()], [d["r"].data_ptr()], [L.n_pods], [pex[-1].data_ptr()],
+                         [outs[1][0].data_ptr()], [outs[1][1].data_ptr()], n_nodes=[L.n_nodes],
+                         node_export=[nex[-1].data_ptr()], out_node_energy=[outs[1][2].data_ptr()],
+                         out_node_power=[outs[1][3].data_ptr()], streams=[s], comm_streams=[comm.cuda_stream])
+    torch.cuda.synchronize()
+    acc.sync(s)
+    for a_, b_ in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a_.cpu().numpy().view(np.uint64), b_.cpu().numpy().view(np.uint64))
+    assert outs[0][0].abs().sum().item() > 0
+    cl.close()
+    acc.close()
+
+
+def test_allreduce_exports_sharded_matches_tables():
+    """Several shards on one GPU (kacc_create_multi): kacc_allreduce_exports (partials of
+    every shard on the comm streams, combined, all-reduced) == kacc_allreduce_namespaces."""
+    L = fleet.make_layout(48, [2000, 300, 1, 0, 700, 64] * 8, 4, seed=23, n_namespaces=11)
+    world = 3
+    shards = shard.shard(L, world)
+    cl = accel.Cluster.create_multi([0] * world, L.zones, [sl.capacities() for _, _, sl in shards])
+    Z = L.zones
+    sim = fleet.FleetSim(L, seed=23, read_error_frac=0.1)
+    s = current_stream_handle()
+    comm = torch.cuda.Stream()
+    pex = [torch.zeros(max(sl.n_pods, 1) * 2 * Z, dtype=torch.int64, device="cuda") for _, _, sl in shards]
+    nex = [torch.zeros(sl.n_nodes * 5 * Z, dtype=torch.int64, device="cuda") for _, _, sl in shards]
+    keep = []
+    for _ in range(3):
+        a = sim.next_interval()
+        for r, ((lo, hi, sl), acc) in enumerate(zip(shards, cl.shards)):
+            sub, sizes, _ = fleet.subset_interval(a, np.arange(lo, hi), Z)
+            t = to_device(sub)
+            t["pod_export"], t["node_export"] = pex[r], nex[r]
+            keep.append(t)
+            acc.run_interval(interval_from_tensors(t, sizes, sl.fast_flag()), s)
+    n_ns = L.n_namespaces
+    csr = [to_device({"o": sl.namespace_csr()[0], "s": sl.namespace_csr()[1], "r": sl.namespace_csr_rows()[1]})
+           for _, _, sl in shards]
+    mk = lambda n, dt: [torch.zeros(n, dtype=dt, device="cuda") for _ in range(world)]  # noqa: E731
+    o_tab = [mk(n_ns * Z, torch.int64), mk(n_ns * Z, torch.float64), mk(2 * Z, torch.int64), mk(3 * Z, torch.float64)]
+    o_exp = [mk(n_ns * Z, torch.int64), mk(n_ns * Z, torch.float64), mk(2 * Z, torch.int64), mk(3 * Z, torch.float64)]
+    P = lambda xs: [x.data_ptr() for x in xs]  # noqa: E731
+    cl.allreduce_namespaces(n_ns, [c["o"].data_ptr() for c in csr], [c["s"].data_ptr() for c in csr], *map(P, o_tab),
+                            streams=[s] * world)
+    cl.allreduce_exports(n_ns, [c["o"].data_ptr() for c in csr], [c["r"].data_ptr() for c in csr],
+                         [sl.n_pods for _, _, sl in shards], P(pex), P(o_exp[0]), P(o_exp[1]),
+                         n_nodes=[sl.n_nodes for _, _, sl in shards], node_export=P(nex),
+                         out_node_energy=P(o_exp[2]), out_node_power=P(o_exp[3]), streams=[s] * world,
+                         comm_streams=[comm.cuda_stream] * world)
+    torch.cuda.synchronize()
+    for acc in cl.shards:
+        acc.sync(s)
+    for a_, b_ in zip(o_tab, o_exp):
+        for r in range(world):
+            np.testing.assert_array_equal(a_[r].cpu().numpy().view(np.uint64), b_[r].cpu().numpy().view(np.uint64))
+    cl.close()
