@@ -317,13 +317,16 @@ __device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const
 // interval's own kernels so that kacc_allreduce_exports reduces them on
 // another stream while the next interval runs.  Pod row q: EnergyTotal[Z] then
 // the bits of Power[Z] (zeros for a pod whose slot is out of range).
+// Plain stores: a lane's record leaves as Z/2 + Z/2 16-B pieces, so each wave
+// instruction writes every 2Z-th 16 B of the wave's span; L2 merges the pieces
+// into full lines (non-temporal, each piece would reach HBM as a partial line).
 template <int Z>
 __device__ __forceinline__ void export_pod(const kacc_interval &b, uint32_t q, const uint64_t (&E)[Z],
                                            const double (&P)[Z]) {
   if (!b.pod_export) return;
   uint64_t *o = b.pod_export + static_cast<uint64_t>(q) * (2 * Z);
-  store_row<Z, true, uint64_t>(o, 0, E);
-  store_row<Z, true, double>(reinterpret_cast<double *>(o), 1, P);
+  store_row<Z, false, uint64_t>(o, 0, E);
+  store_row<Z, false, double>(reinterpret_cast<double *>(o), 1, P);
 }
 template <int Z>
 __device__ __forceinline__ void export_pod_zero(const kacc_interval &b, uint32_t q) {
