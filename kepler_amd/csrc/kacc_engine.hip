@@ -93,7 +93,12 @@ constexpr int kChunkRows = kRowsLds;   // big-node rows per chunk item
 constexpr int kChunkThreads = 512;     // chunk kernel workgroup
 constexpr int kChunkRpt = kChunkRows / kChunkThreads;
 constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node CPU total)
-constexpr uint32_t kChunkGrid = 512;   // persistent chunk-kernel workgroups (2 per CU resident)
+// KACC_CHUNK_WAVES: waves per SIMD the chunk kernel is compiled for at Z <= 4
+// (4 = two workgroups per CU, 121 VGPRs; 6 = three, 80 VGPRs with spills)
+#ifndef KACC_CHUNK_WAVES
+#define KACC_CHUNK_WAVES 4
+#endif
+constexpr uint32_t kChunkGrid = 128 * KACC_CHUNK_WAVES;  // persistent chunk-kernel workgroups (all resident)
 
 template <int V>
 constexpr int kTpb = 512;  // threads per workgroup (fast path)
@@ -141,6 +146,10 @@ struct DevState {
   ChunkItem *items;    // [item_cap] big-node chunks this launch
   uint32_t *item_ctr;  // [0] length, [1] dequeue head; cleared by pod_kernel
   uint32_t item_cap;
+  // kacc_run_intervals over intervals of ONE layout (the same offset arrays):
+  // the chunk items are generated once (items_kernel) and reused, so the node
+  // phase skips them; pod_kernel keeps the list for the next interval
+  uint32_t items_given, keep_items;
 };
 
 struct NodeShared {
@@ -2018,21 +2027,123 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
 //                    visible across XCDs: no cross-workgroup wait anywhere).
 // Every sum keeps its sequential / canonical-tree order, so results are
 // bit-identical to one workgroup handling the whole node.
+// Chunk items of big node n (see big_node_prepare): items [base, base + nch)
+// with the first container / VM / pod each chunk owns.  A segment belongs to
+// the chunk holding its first row (rows are [containers][VMs][rest]); a pod to
+// the chunk owning its first container.  Segment i is the first one owned by
+// chunks (key(i-1), key(i)].  Lanes g < kGen of the caller generate.
+template <int V, uint32_t kGen>
+__device__ __forceinline__ void gen_items(const kacc_interval &b, const DevState &st, uint32_t n,
+                                          const NodeRanges &rg, uint32_t base, uint32_t nch, uint32_t g) {
+  constexpr int kScan = 4;  // segments per generating lane per step
+  const uint32_t p0 = rg.p0, p1 = rg.p1;
+  ChunkItem *__restrict__ items = st.items + base;
+  const uint32_t c0 = rg.c0, c1 = rg.c1, v0 = rg.v0, v1 = rg.v1, q0 = rg.q0, q1 = rg.q1;
+  auto clampr = [&](uint32_t x) { return min(max(x, p0), p1); };
+  auto clampc = [&](uint32_t x) { return min(max(x, c0), c1); };
+  auto chunk_of = [&](uint32_t start) -> int {
+    return static_cast<int>(min((start - p0) / kChunkRows, nch - 1));
+  };
+  // first row of container c given ctr_proc_end[c - 1] (p0 for c0)
+  const uint32_t ctr_rows_end = c1 > c0 ? clampr(b.ctr_proc_end[c1 - 1]) : p0;
+  // segment i (owner chunk kc, its predecessor's kp) begins chunks kp+1..kc
+  auto mark = [&](uint32_t i, int kc, int kp, uint32_t ChunkItem::*field) {
+    if (kc < kp) raise_err(st.err, kErrOffsets);
+    for (int k = kp + 1; k <= kc; ++k) items[k].*field = i;
+  };
+  // containers: start(c) = c == c0 ? p0 : end[c-1]
+  for (uint32_t cb = c0 + g; cb < ((V & kVarBigNoScan) ? c0 : c1); cb += kGen * kScan) {
+    uint32_t e1[kScan], e2[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      const uint32_t c = cb + u * kGen;
+      e1[u] = (c < c1 && c > c0) ? b.ctr_proc_end[c - 1] : p0;
+      e2[u] = (c < c1 && c > c0 + 1) ? b.ctr_proc_end[c - 2] : p0;
+    }
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      const uint32_t c = cb + u * kGen;
+      if (c >= c1) continue;
+      mark(c, chunk_of(clampr(e1[u])), c > c0 ? chunk_of(clampr(e2[u])) : -1,
+           &ChunkItem::ctr_begin);
+    }
+  }
+  // VMs: start(v) = v == v0 ? ctr_rows_end : vm_end[v-1]
+  for (uint32_t vb = v0 + g; vb < ((V & kVarBigNoScan) ? v0 : v1); vb += kGen * kScan) {
+    uint32_t e1[kScan], e2[kScan];
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      const uint32_t v = vb + u * kGen;
+      e1[u] = (v < v1 && v > v0) ? b.vm_proc_end[v - 1] : ctr_rows_end;
+      e2[u] = (v < v1 && v > v0 + 1) ? b.vm_proc_end[v - 2] : ctr_rows_end;
+    }
+#pragma unroll
+    for (int u = 0; u < kScan; ++u) {
+      const uint32_t v = vb + u * kGen;
+      if (v >= v1) continue;
+      mark(v, chunk_of(clampr(e1[u])), v > v0 ? chunk_of(clampr(e2[u])) : -1,
+           &ChunkItem::vm_begin);
+    }
+  }
+  // pods: first container f(q) = q == q0 ? c0 : pod_end[q-1]; key = key of
+  // container f(q), or the last chunk when the pod starts past the containers
+  if constexpr ((V & (kVarSkipAggregates | kVarBigNoScan)) == 0) {
+    for (uint32_t qb = q0 + g; qb < q1; qb += kGen * kScan) {
+      uint32_t f1[kScan], f2[kScan], s1[kScan], s2[kScan];
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t q = qb + u * kGen;
+        f1[u] = (q < q1 && q > q0) ? clampc(b.pod_ctr_end[q - 1]) : c0;
+        f2[u] = (q < q1 && q > q0 + 1) ? clampc(b.pod_ctr_end[q - 2]) : c0;
+      }
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        s1[u] = (f1[u] > c0 && f1[u] < c1) ? b.ctr_proc_end[f1[u] - 1] : p0;
+        s2[u] = (f2[u] > c0 && f2[u] < c1) ? b.ctr_proc_end[f2[u] - 1] : p0;
+      }
+#pragma unroll
+      for (int u = 0; u < kScan; ++u) {
+        const uint32_t q = qb + u * kGen;
+        if (q >= q1) continue;
+        const int kc = f1[u] < c1 ? chunk_of(clampr(s1[u])) : static_cast<int>(nch - 1);
+        const int kp = q == q0 ? -1 : f2[u] < c1 ? chunk_of(clampr(s2[u])) : static_cast<int>(nch - 1);
+        mark(q, kc, kp, &ChunkItem::pod_begin);
+      }
+    }
+  }
+  // chunks after the last segment's owner own none of that kind
+  const int kl_ctr = c1 > c0 ? chunk_of(c1 - 1 > c0 ? clampr(b.ctr_proc_end[c1 - 2]) : p0) : -1;
+  const int kl_vm = v1 > v0 ? chunk_of(v1 - 1 > v0 ? clampr(b.vm_proc_end[v1 - 2]) : ctr_rows_end) : -1;
+  int kl_pod = -1;
+  if (q1 > q0) {
+    const uint32_t f = q1 - 1 > q0 ? clampc(b.pod_ctr_end[q1 - 2]) : c0;
+    kl_pod = f < c1 ? chunk_of(f > c0 ? clampr(b.ctr_proc_end[f - 1]) : p0) : static_cast<int>(nch - 1);
+  }
+  for (uint32_t k = g; k < nch; k += kGen) {
+    items[k].node = n;
+    items[k].chunk = k;
+    items[k].nchunks = nch;
+    if (static_cast<int>(k) > kl_ctr) items[k].ctr_begin = c1;
+    if (static_cast<int>(k) > kl_vm) items[k].vm_begin = v1;
+    if (static_cast<int>(k) > kl_pod) items[k].pod_begin = q1;
+  }
+}
+
 template <int Z, int V>
 __device__ void big_node_prepare(const kacc_interval &b, const DevState &st, const uint32_t n,
                                  const NodeRanges &rg, double *red, NodeShared &sh,
                                  uint32_t &s_base) {
   constexpr int kThreads = kTpb<V>;
   constexpr uint32_t kGen = kThreads - kTree;  // lanes generating chunk items
-  constexpr int kScan = 4;                     // segments per generating lane per step
   const int tid = threadIdx.x;
   const uint32_t p0 = rg.p0, p1 = rg.p1, rows = p1 - p0;
   const uint32_t nch = rows ? (rows + kChunkRows - 1) / kChunkRows : 1u;
-  if (tid == 0) s_base = (V & kVarBigNoAtomic) ? n + p0 / kChunkRows : atomicAdd(st.item_ctr, nch);
+  if (tid == 0 && !st.items_given)
+    s_base = (V & kVarBigNoAtomic) ? n + p0 / kChunkRows : atomicAdd(st.item_ctr, nch);
   if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
   __syncthreads();
-  const uint32_t base = s_base;
-  const bool fits = base + nch <= st.item_cap && base + nch >= base;  // host sizes the list
+  const uint32_t base = st.items_given ? 0u : s_base;
+  const bool fits = st.items_given || (base + nch <= st.item_cap && base + nch >= base);  // host sizes the list
   if (!fits && tid == 0) raise_err(st.err, kErrCapacity);
   const bool given = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) != 0;
   if (tid < kTree) {
@@ -2063,102 +2174,9 @@ __device__ void big_node_prepare(const kacc_interval &b, const DevState &st, con
       }
       red[tid] = s;
     }
-  } else if (fits) {
+  } else if (fits && !st.items_given) {
     // ---- chunk items, concurrently with the sum (the other kGen lanes) --------
-    // A segment belongs to the chunk holding its first row (rows are
-    // [containers][VMs][rest]); a pod to the chunk owning its first container.
-    // Segment i is the first one owned by chunks (key(i-1), key(i)].
-    const uint32_t g = static_cast<uint32_t>(tid) - kTree;
-    ChunkItem *__restrict__ items = st.items + base;
-    const uint32_t c0 = rg.c0, c1 = rg.c1, v0 = rg.v0, v1 = rg.v1, q0 = rg.q0, q1 = rg.q1;
-    auto clampr = [&](uint32_t x) { return min(max(x, p0), p1); };
-    auto clampc = [&](uint32_t x) { return min(max(x, c0), c1); };
-    auto chunk_of = [&](uint32_t start) -> int {
-      return static_cast<int>(min((start - p0) / kChunkRows, nch - 1));
-    };
-    // first row of container c given ctr_proc_end[c - 1] (p0 for c0)
-    const uint32_t ctr_rows_end = c1 > c0 ? clampr(b.ctr_proc_end[c1 - 1]) : p0;
-    // segment i (owner chunk kc, its predecessor's kp) begins chunks kp+1..kc
-    auto mark = [&](uint32_t i, int kc, int kp, uint32_t ChunkItem::*field) {
-      if (kc < kp) raise_err(st.err, kErrOffsets);
-      for (int k = kp + 1; k <= kc; ++k) items[k].*field = i;
-    };
-    // containers: start(c) = c == c0 ? p0 : end[c-1]
-    for (uint32_t cb = c0 + g; cb < ((V & kVarBigNoScan) ? c0 : c1); cb += kGen * kScan) {
-      uint32_t e1[kScan], e2[kScan];
-#pragma unroll
-      for (int u = 0; u < kScan; ++u) {
-        const uint32_t c = cb + u * kGen;
-        e1[u] = (c < c1 && c > c0) ? b.ctr_proc_end[c - 1] : p0;
-        e2[u] = (c < c1 && c > c0 + 1) ? b.ctr_proc_end[c - 2] : p0;
-      }
-#pragma unroll
-      for (int u = 0; u < kScan; ++u) {
-        const uint32_t c = cb + u * kGen;
-        if (c >= c1) continue;
-        mark(c, chunk_of(clampr(e1[u])), c > c0 ? chunk_of(clampr(e2[u])) : -1,
-             &ChunkItem::ctr_begin);
-      }
-    }
-    // VMs: start(v) = v == v0 ? ctr_rows_end : vm_end[v-1]
-    for (uint32_t vb = v0 + g; vb < ((V & kVarBigNoScan) ? v0 : v1); vb += kGen * kScan) {
-      uint32_t e1[kScan], e2[kScan];
-#pragma unroll
-      for (int u = 0; u < kScan; ++u) {
-        const uint32_t v = vb + u * kGen;
-        e1[u] = (v < v1 && v > v0) ? b.vm_proc_end[v - 1] : ctr_rows_end;
-        e2[u] = (v < v1 && v > v0 + 1) ? b.vm_proc_end[v - 2] : ctr_rows_end;
-      }
-#pragma unroll
-      for (int u = 0; u < kScan; ++u) {
-        const uint32_t v = vb + u * kGen;
-        if (v >= v1) continue;
-        mark(v, chunk_of(clampr(e1[u])), v > v0 ? chunk_of(clampr(e2[u])) : -1,
-             &ChunkItem::vm_begin);
-      }
-    }
-    // pods: first container f(q) = q == q0 ? c0 : pod_end[q-1]; key = key of
-    // container f(q), or the last chunk when the pod starts past the containers
-    if constexpr ((V & (kVarSkipAggregates | kVarBigNoScan)) == 0) {
-      for (uint32_t qb = q0 + g; qb < q1; qb += kGen * kScan) {
-        uint32_t f1[kScan], f2[kScan], s1[kScan], s2[kScan];
-#pragma unroll
-        for (int u = 0; u < kScan; ++u) {
-          const uint32_t q = qb + u * kGen;
-          f1[u] = (q < q1 && q > q0) ? clampc(b.pod_ctr_end[q - 1]) : c0;
-          f2[u] = (q < q1 && q > q0 + 1) ? clampc(b.pod_ctr_end[q - 2]) : c0;
-        }
-#pragma unroll
-        for (int u = 0; u < kScan; ++u) {
-          s1[u] = (f1[u] > c0 && f1[u] < c1) ? b.ctr_proc_end[f1[u] - 1] : p0;
-          s2[u] = (f2[u] > c0 && f2[u] < c1) ? b.ctr_proc_end[f2[u] - 1] : p0;
-        }
-#pragma unroll
-        for (int u = 0; u < kScan; ++u) {
-          const uint32_t q = qb + u * kGen;
-          if (q >= q1) continue;
-          const int kc = f1[u] < c1 ? chunk_of(clampr(s1[u])) : static_cast<int>(nch - 1);
-          const int kp = q == q0 ? -1 : f2[u] < c1 ? chunk_of(clampr(s2[u])) : static_cast<int>(nch - 1);
-          mark(q, kc, kp, &ChunkItem::pod_begin);
-        }
-      }
-    }
-    // chunks after the last segment's owner own none of that kind
-    const int kl_ctr = c1 > c0 ? chunk_of(c1 - 1 > c0 ? clampr(b.ctr_proc_end[c1 - 2]) : p0) : -1;
-    const int kl_vm = v1 > v0 ? chunk_of(v1 - 1 > v0 ? clampr(b.vm_proc_end[v1 - 2]) : ctr_rows_end) : -1;
-    int kl_pod = -1;
-    if (q1 > q0) {
-      const uint32_t f = q1 - 1 > q0 ? clampc(b.pod_ctr_end[q1 - 2]) : c0;
-      kl_pod = f < c1 ? chunk_of(f > c0 ? clampr(b.ctr_proc_end[f - 1]) : p0) : static_cast<int>(nch - 1);
-    }
-    for (uint32_t k = g; k < nch; k += kGen) {
-      items[k].node = n;
-      items[k].chunk = k;
-      items[k].nchunks = nch;
-      if (static_cast<int>(k) > kl_ctr) items[k].ctr_begin = c1;
-      if (static_cast<int>(k) > kl_vm) items[k].vm_begin = v1;
-      if (static_cast<int>(k) > kl_pod) items[k].pod_begin = q1;
-    }
+    gen_items<V, kGen>(b, st, n, rg, base, nch, static_cast<uint32_t>(tid) - kTree);
   }
   __syncthreads();
   if (given) {
@@ -2184,6 +2202,34 @@ __device__ void big_node_prepare(const kacc_interval &b, const DevState &st, con
   }
 }
 
+// The chunk items of every big node of a layout, once for all the intervals of a
+// kacc_run_intervals call over that layout (every descriptor the same offset
+// arrays): one workgroup per node, all lanes generating.  Items exist for
+// every big node whatever its status; chunk_kernel skips the items of a node
+// that is skipped in its interval.
+template <int V>
+__global__ __launch_bounds__(kTpb<V>) void items_kernel(const kacc_interval b, const DevState st) {
+  constexpr int kThreads = kTpb<V>;
+  __shared__ uint32_t s_base;
+  const uint32_t n = blockIdx.x;
+  if (n >= b.n_nodes) return;
+  uint32_t status_unused;
+  NodeRanges raw;
+  node_words(b, n, status_unused, raw);
+  const NodeRanges rg = clamp_ranges(b, st, raw, threadIdx.x);
+  if (fits_fast<V>(rg)) return;  // block-uniform: the fast path takes this node
+  const uint32_t rows = rg.p1 - rg.p0;
+  const uint32_t nch = rows ? (rows + kChunkRows - 1) / kChunkRows : 1u;
+  if (threadIdx.x == 0) s_base = atomicAdd(st.item_ctr, nch);
+  __syncthreads();
+  const uint32_t base = s_base;
+  if (base + nch > st.item_cap || base + nch < base) {
+    if (threadIdx.x == 0) raise_err(st.err, kErrCapacity);
+    return;
+  }
+  gen_items<V, kThreads>(b, st, n, rg, base, nch, threadIdx.x);
+}
+
 // Node-uniform attribution parameters written by the node phase, back into LDS.
 template <int Z>
 __device__ __forceinline__ void node_params_to_lds(const DevState &st, uint32_t n, int tid,
@@ -2201,7 +2247,7 @@ __device__ __forceinline__ void node_params_to_lds(const DevState &st, uint32_t 
 }
 
 template <int Z, int V>
-__global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(const kacc_interval b,
+__global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void chunk_kernel(const kacc_interval b,
                                                                            const DevState st) {
   constexpr int kThreads = kChunkThreads;
   constexpr int kR = kChunkRpt;
@@ -2255,9 +2301,14 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : 4)) void chunk_kernel(c
       idx = uniform_u32(s_next[parity]);
       continue;
     }
-    uint32_t status_unused;
+    uint32_t status;
     NodeRanges raw;
-    node_words(b, n, status_unused, raw);
+    node_words(b, n, status, raw);
+    if (status & KACC_NODE_READ_ERROR) {  // reused items (items_given) of a node skipped now
+      __syncthreads();
+      idx = uniform_u32(s_next[parity]);
+      continue;
+    }
     const NodeRanges rg = clamp_ranges(b, st, raw, tid);
     const bool last = k + 1 >= nch;
     const uint32_t lo = min(rg.p0 + min(k, nch) * static_cast<uint32_t>(kChunkRows), rg.p1);
@@ -2524,7 +2575,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
   constexpr bool kNT = (V & kVarTemporalStores) == 0;  // as interval_kernel
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) {
-    st.item_ctr[0] = 0u;
+    if (!st.keep_items) st.item_ctr[0] = 0u;  // the list stays for the next interval of one layout
     st.item_ctr[1] = 0u;
   }
   const uint32_t count = min(st.defer_ctr[0], st.defer_cap);
@@ -2891,6 +2942,8 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.defer = ctx->d_defer;
   s.defer_ctr = ctx->d_ctr + 2;
   s.defer_cap = ctx->defer_cap;
+  s.items_given = 0;
+  s.keep_items = 0;
   return s;
 }
 
@@ -3378,8 +3431,29 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
     ctx->live_nodes = dev_batches[count - 1].n_nodes;
     return KACC_OK;
   }
-  for (uint32_t k = 0; k < count; ++k)
-    if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
+  // intervals over ONE layout (every descriptor the same offset arrays and sizes)
+  // that may hold big nodes: their chunk items are generated once and reused
+  bool one_layout = count > 1;
+  for (uint32_t k = 1; k < count && one_layout; ++k) {
+    const kacc_interval &a = dev_batches[0], &b = dev_batches[k];
+    one_layout = a.n_nodes == b.n_nodes && a.n_procs == b.n_procs && a.n_ctrs == b.n_ctrs && a.n_vms == b.n_vms &&
+                 a.n_pods == b.n_pods && a.proc_off == b.proc_off && a.ctr_off == b.ctr_off && a.vm_off == b.vm_off &&
+                 a.pod_off == b.pod_off && a.ctr_proc_end == b.ctr_proc_end && a.vm_proc_end == b.vm_proc_end &&
+                 a.pod_ctr_end == b.pod_ctr_end && !(b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES));
+  }
+  if (one_layout && dev_batches[0].n_nodes && !(dev_batches[0].flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES))) {
+    hipLaunchKernelGGL((kacc::items_kernel<0>), dim3(dev_batches[0].n_nodes), dim3(kacc::kTpb<0>), 0, st,
+                       dev_batches[0], ds);
+    kacc::DevState dk = ds;
+    dk.items_given = 1;
+    for (uint32_t k = 0; k < count; ++k) {
+      dk.keep_items = k + 1 < count ? 1u : 0u;  // the last interval's pod_kernel clears the list
+      launch(ctx->cfg.zones, dev_batches[k], dk, st);
+    }
+  } else {
+    for (uint32_t k = 0; k < count; ++k)
+      if (dev_batches[k].n_nodes) launch(ctx->cfg.zones, dev_batches[k], ds, st);
+  }
   KACC_HIP(ctx, hipGetLastError());
   if (count) ctx->live_nodes = dev_batches[count - 1].n_nodes;
   return KACC_OK;

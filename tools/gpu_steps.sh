@@ -8,6 +8,7 @@ set -u
 mkdir -p gpurun_out
 while [ $# -ge 3 ]; do
   name=$1; secs=$2; cmd=$3; shift 3
+  mkdir -p "gpurun_out/$(dirname "$name")"
   echo "== $name (limit ${secs}s): $cmd"
   timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
   rc=$?
