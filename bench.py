@@ -79,7 +79,7 @@ def parse():
                          "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
     ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
                     help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
-    ap.add_argument("--totals", choices=["exports", "tables"], default="exports",
+    ap.add_argument("--totals", choices=["exports", "tables", "tables+writes"], default="exports",
                     help="cluster totals from the interval's exports, reduced on the comm stream while the next "
                          "interval runs (kacc_allreduce_exports), or from the state tables with the partial sums on "
                          "the compute stream (kacc_allreduce_namespaces)")
@@ -452,7 +452,8 @@ class Workload:
         self.exports = args.totals == "exports"
         self.pex = [torch.zeros(max(sizes["n_pods"], 1) * 2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
         self.nex = [torch.zeros(max(sizes["n_nodes"], 1) * 5 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
-        if self.exports:
+        if args.totals != "tables":  # "tables+writes": the exports are written, the totals come from the tables
+            # (an ablation: the cost of the export stores alone)
             for st in range(n_steps):
                 t = self.iv_tensors[st * K + K - 1]
                 t["pod_export"], t["node_export"] = self.pex[st % 2], self.nex[st % 2]

@@ -421,12 +421,16 @@ def test_config1_exact_layout_bit_exact(nodes, flags_mask):
     assert wrapped > 0  # the fake meter's counters wrapped at least once
 
 
+@pytest.mark.parametrize("shared", [False, True], ids=["own-arrays", "one-layout"])
 @pytest.mark.timeout(300)
-def test_config5_shape_60_intervals_one_call_bit_exact():
+def test_config5_shape_60_intervals_one_call_bit_exact(shared):
     """BASELINE config 5's shape: heavy-tailed nodes of 10k-50k processes, Z = 4, VMs +
     containers + pods, 60 intervals in ONE kacc_run_intervals call with counter wraparound
     (fake-meter MaxEnergy 1e6), churn, read errors and adversarial inputs: every table
-    bit-exact against the oracle after the call (and after the first-read call before it)."""
+    bit-exact against the oracle after the call (and after the first-read call before it).
+    one-layout: every descriptor points at the SAME offset arrays, so the call generates the
+    big nodes' chunk items once and reuses them (items_kernel), and the chunk kernel must skip
+    the items of nodes skipped (read error) in their interval."""
     from oracle.oracle import Oracle
 
     procs = [10000, 50000, 23000, 12000, 31000, 10000, 17500]
@@ -443,7 +447,16 @@ def test_config5_shape_60_intervals_one_call_bit_exact():
     acc.run_intervals([interval_from_tensors(t0, sizes)], s)
     ora.interval(first, sizes)
     ivs = [sim.next_interval() for _ in range(60)]
-    dev = [to_device(a) for a in ivs]
+    if shared:
+        statics = to_device(layout.static_arrays())
+        dev = []
+        for a in ivs:
+            t = to_device({k: v for k, v in a.items() if k not in statics})
+            t.update(statics)
+            dev.append(t)
+        assert sum(int((a["node_status"] & accel.KACC_NODE_READ_ERROR).any()) for a in ivs) > 3
+    else:
+        dev = [to_device(a) for a in ivs]
     acc.run_intervals([interval_from_tensors(t, sizes) for t in dev], s)
     acc.sync(s)
     for a in ivs:
