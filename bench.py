@@ -79,10 +79,13 @@ def parse():
                          "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
     ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
                     help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
-    ap.add_argument("--totals", choices=["exports", "tables", "tables+writes"], default="exports",
-                    help="cluster totals from the interval's exports, reduced on the comm stream while the next "
-                         "interval runs (kacc_allreduce_exports), or from the state tables with the partial sums on "
-                         "the compute stream (kacc_allreduce_namespaces)")
+    ap.add_argument("--totals", choices=["tables", "exports", "tables+writes"], default="tables",
+                    help="cluster totals from the state tables, partial sums on the compute stream and the RCCL "
+                         "all-reduce on the comm stream (kacc_allreduce_namespaces, the default: measured fastest), "
+                         "or from the interval's exports with everything on the comm stream (kacc_allreduce_exports: "
+                         "the export stores cost 26 us and the concurrent partial sums slow the next interval more "
+                         "than they save at config 3, profiles/r03/exports_ablation); tables+writes = the export "
+                         "stores alone (ablation)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
