@@ -530,6 +530,8 @@ def measure(args, w, rank, world, stream, comm_stream):
         rc = reduce_fn(cl.handle, w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
+        if ev is not None:
+            ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
         done[b].record(comm_stream)
         used[b] = True
 
@@ -537,8 +539,7 @@ def measure(args, w, rank, world, stream, comm_stream):
         step(k)
     acc.sync(stream)
     torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -550,11 +551,12 @@ def measure(args, w, rank, world, stream, comm_stream):
         dist.barrier()
     wall = time.perf_counter() - t0
     acc.sync(stream)  # surfaces any device-detected range error
-    kernel_ms = [a.elapsed_time(b) / K for a, b in events]  # per interval
+    kernel_ms = [a.elapsed_time(b) / K for a, b, _ in events]  # per interval
+    totals_ms = [b.elapsed_time(c) for _, b, c in events]  # per step
     wall_t = torch.tensor([wall], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    return float(wall_t.item()), kernel_ms
+    return float(wall_t.item()), kernel_ms, totals_ms
 
 
 def main():
@@ -593,7 +595,7 @@ def main():
     w.acc.sync(stream)
     del prime_t
     log(rank, f"[bench] setup {time.time() - t_setup:.1f}s")
-    wall_max, kernel_ms = measure(args, w, rank, world, stream, comm_stream)
+    wall_max, kernel_ms, totals_ms = measure(args, w, rank, world, stream, comm_stream)
 
     # same-box reference for the roofline: a 1.28 GB device-to-device copy
     src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
@@ -668,6 +670,7 @@ def main():
         "kernel_ms": k_avg_ms,
         "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
         "step_minus_kernel_ms": wall_max * 1e3 / args.steps - k_avg_ms * K,
+        "totals_compute_ms": float(np.mean(totals_ms)),  # interval end -> partial sums end, compute stream
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -727,7 +730,7 @@ def main():
         wk.acc.run_interval(interval_from_tensors(prime_t, wk.sizes), stream)
         wk.acc.sync(stream)
         del prime_t
-        wwall, wkms = measure(args, wk, rank, world, stream, comm_stream)
+        wwall, wkms, _ = measure(args, wk, rank, world, stream, comm_stream)
         wp = torch.tensor([wk.sizes["n_procs"]], dtype=torch.float64)
         dist.all_reduce(wp)
         result["weak_scaling"] = {"value": float(wp.item()) * K * args.steps / wwall, "unit": "proc-attr/s",

@@ -212,12 +212,15 @@ typedef struct kacc_interval {
  * new snapshot: node zones = monitor.NodeUsage (types.go:27-40), workload
  * zones = monitor.Usage (types.go:44-47).
  *
- * KACC_T_PROC_POWER is DERIVED, not stored (ABI 3): a process's power is
+ * KACC_T_PROC_POWER, KACC_T_CTR_POWER and KACC_T_VM_POWER are DERIVED, not
+ * stored (ABI 3): a process's (container's, VM's) power is
  * cpuTimeRatio · NodeUsage.ActivePower for a zone that passed the guard
- * (process.go:124, 142), and 0 otherwise, so the engine keeps per slot the
- * ratio (KACC_T_PROC_RATIO) and the node (KACC_T_PROC_NODE) of the slot's
- * last attribution and multiplies on read, bit-identical to a stored value
- * (8Z - 12 bytes less per process row and interval).  kacc_table_download,
+ * (process.go:124, 142; container.go:114, 134; vm.go:84, 103), and 0 otherwise,
+ * so the engine keeps per slot the ratio (KACC_T_*_RATIO) and the node
+ * (KACC_T_*_NODE) of the slot's last attribution and multiplies on read,
+ * bit-identical to a stored value (8Z - 12 bytes less per row and interval).
+ * Pod power stays stored (its guard is the node's Power, pod.go:96, and the
+ * namespace totals gather it).  kacc_table_download,
  * kacc_unpack, kacc_format_*, and the trackers' frozen copies derive it; it
  * has no device pointer (kacc_table_device_ptr: KACC_EINVAL) and cannot be
  * uploaded.  The derived value is Usage.Power for every slot its node
@@ -241,11 +244,11 @@ typedef enum kacc_table {
   KACC_T_PROC_ENERGY,           /* u64 [Sp*Z] Process Usage.EnergyTotal      */
   KACC_T_PROC_POWER,            /* f64 [Sp*Z] Process Usage.Power (DERIVED)  */
   KACC_T_CTR_ENERGY,            /* u64 [Sc*Z]                                */
-  KACC_T_CTR_POWER,             /* f64 [Sc*Z]                                */
+  KACC_T_CTR_POWER,             /* f64 [Sc*Z] (DERIVED)                      */
   KACC_T_CTR_CPU_DELTA,         /* f64 [Sc]  resource.Container.CPUTimeDelta */
   KACC_T_CTR_CPU_TOTAL,         /* f64 [Sc]  resource.Container.CPUTotalTime */
   KACC_T_VM_ENERGY,             /* u64 [Sv*Z]                                */
-  KACC_T_VM_POWER,              /* f64 [Sv*Z]                                */
+  KACC_T_VM_POWER,              /* f64 [Sv*Z] (DERIVED)                      */
   KACC_T_VM_CPU_DELTA,          /* f64 [Sv]  resource.VirtualMachine.CPUTimeDelta */
   KACC_T_POD_ENERGY,            /* u64 [Sq*Z]                                */
   KACC_T_POD_POWER,             /* f64 [Sq*Z]                                */
@@ -254,6 +257,10 @@ typedef enum kacc_table {
   KACC_T_PROC_RATIO,            /* f64 [Sp]  cpuTimeRatio of the slot's last attribution
                                               (process.go:128; Δ / ProcessTotalCPUTimeDelta) */
   KACC_T_PROC_NODE,             /* u32 [Sp]  the node of that attribution     */
+  KACC_T_CTR_RATIO,             /* f64 [Sc]  container cpuTimeRatio (container.go:118) */
+  KACC_T_CTR_NODE,              /* u32 [Sc]                                   */
+  KACC_T_VM_RATIO,              /* f64 [Sv]  VM cpuTimeRatio (vm.go:89)       */
+  KACC_T_VM_NODE,               /* u32 [Sv]                                   */
   KACC_T_COUNT
 } kacc_table;
 

@@ -82,13 +82,19 @@ TABLES = [
     ("pod_cpu_total", np.float64),
     ("proc_ratio", np.float64),
     ("proc_node", np.uint32),
+    ("ctr_ratio", np.float64),
+    ("ctr_node", np.uint32),
+    ("vm_ratio", np.float64),
+    ("vm_node", np.uint32),
 ]
-# derived on read (no device storage, no upload / device pointer): a process's power is
-# cpuTimeRatio x its node's ActivePower (process.go:124-142; kacc_derive.hpp)
-DERIVED_TABLES = {"proc_power"}
+# derived on read (no device storage, no upload / device pointer): a process's (container's,
+# VM's) power is cpuTimeRatio x its node's ActivePower (process.go:124-142; kacc_derive.hpp)
+DERIVED_TABLES = {"proc_power", "ctr_power", "vm_power"}
 # engine storage behind a derived table (not a Go quantity): the CPU restatements keep them
 # only to check the engine's layout
-ENGINE_TABLES = {"proc_ratio", "proc_node"}
+ENGINE_TABLES = {"proc_ratio", "proc_node", "ctr_ratio", "ctr_node", "vm_ratio", "vm_node"}
+# tables holding node indices (a subset / shard of a fleet renumbers its nodes)
+NODE_INDEX_TABLES = {"proc_node", "ctr_node", "vm_node"}
 TABLE_INDEX = {name: i for i, (name, _) in enumerate(TABLES)}
 
 # exported symbols, in header order (checked by tests/test_abi.py)

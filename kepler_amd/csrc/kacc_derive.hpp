@@ -1,4 +1,4 @@
-// Derived process power (device + host helpers; not part of the public ABI).
+// Derived process / container / VM power (device + host helpers; not part of the public ABI).
 //
 // The engine's process state is the energy totals plus, per slot, the row's
 // cpuTimeRatio and its node (kacc_engine.hip attribute_proc / store_proc):
@@ -45,11 +45,14 @@ __device__ __forceinline__ double proc_power(const ProcDerive &d, uint64_t s, ui
 
 }  // namespace kacc
 
-// The context's derivation inputs (host).
-inline kacc::ProcDerive kacc_proc_derive(const kacc_ctx *ctx) {
+// The context's derivation inputs for a workload kind (host): processes,
+// containers or VMs (their power has the same form and guard:
+// container.go:114, 134; vm.go:84, 103).
+inline kacc::ProcDerive kacc_derive(const kacc_ctx *ctx, kacc_kind kind) {
   kacc::ProcDerive d;
-  d.ratio = static_cast<const double *>(ctx->tables[KACC_T_PROC_RATIO]);
-  d.node = static_cast<const uint32_t *>(ctx->tables[KACC_T_PROC_NODE]);
+  const int tr = kind == KACC_KIND_CTR ? KACC_T_CTR_RATIO : kind == KACC_KIND_VM ? KACC_T_VM_RATIO : KACC_T_PROC_RATIO;
+  d.ratio = static_cast<const double *>(ctx->tables[tr]);
+  d.node = static_cast<const uint32_t *>(ctx->tables[tr + 1]);
   d.active_energy = static_cast<const uint64_t *>(ctx->tables[KACC_T_NODE_ACTIVE_ENERGY]);
   d.active_power = static_cast<const double *>(ctx->tables[KACC_T_NODE_ACTIVE_POWER]);
   d.cpu_delta = static_cast<const double *>(ctx->tables[KACC_T_NODE_CPU_DELTA]);
@@ -57,7 +60,15 @@ inline kacc::ProcDerive kacc_proc_derive(const kacc_ctx *ctx) {
   d.zones = ctx->cfg.zones;
   return d;
 }
+inline kacc::ProcDerive kacc_proc_derive(const kacc_ctx *ctx) { return kacc_derive(ctx, KACC_KIND_PROC); }
 
-// Elements [first, first + count) of the derived KACC_T_PROC_POWER table
-// ([slot*Z + z]) into out (device), async on `stream` (kacc_engine.hip).
-extern "C" int kacc_internal_proc_power(kacc_ctx *ctx, uint64_t first, uint64_t count, double *out, void *stream);
+// The kind whose power table t is derived (KACC_T_PROC_POWER / CTR / VM), or -1.
+inline int kacc_derived_kind(int t) {
+  return t == KACC_T_PROC_POWER ? KACC_KIND_PROC : t == KACC_T_CTR_POWER ? KACC_KIND_CTR
+                                                 : t == KACC_T_VM_POWER ? KACC_KIND_VM : -1;
+}
+
+// Elements [first, first + count) of the derived power table t ([slot*Z + z])
+// into out (device), async on `stream` (kacc_engine.hip).
+extern "C" int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, double *out,
+                                           void *stream);

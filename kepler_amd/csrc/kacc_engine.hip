@@ -44,8 +44,22 @@ constexpr int kRowsLds = 2048;               // Δcpu rows staged in LDS per nod
 constexpr int kBlock = 256;                  // namespace kernel workgroup
 template <int Z>
 constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 64-row groups
-constexpr int kNsLanes = 16;                 // lanes per namespace (namespace_kernel)
-constexpr int kNsUnroll = 4;                 // pods in flight per namespace lane
+// KACC_NS_LANES / KACC_NS_UNROLL: namespace-sum geometry (the lane count fixes
+// the f64 summation order, mirrored by oracle/kor_namespace_totals)
+#ifndef KACC_NS_LANES
+#define KACC_NS_LANES 16
+#endif
+#ifndef KACC_NS_UNROLL
+#define KACC_NS_UNROLL 4
+#endif
+constexpr int kNsLanes = KACC_NS_LANES;      // lanes per namespace (namespace_kernel)
+constexpr int kNsUnroll = KACC_NS_UNROLL;    // pods in flight per namespace lane
+// KACC_NS_PROBE_PAIRED=1: timing probe only (wrong sums) — the namespace gather
+// reads one 64-B record per pod (energy and power rows side by side) instead of
+// two 32-B rows of two tables
+#ifndef KACC_NS_PROBE_PAIRED
+#define KACC_NS_PROBE_PAIRED 0
+#endif
 
 // Debug variants (kacc_debug_run_variant, timing ablations only; results of a
 // variant != 0 are NOT the reference semantics).
@@ -133,9 +147,11 @@ struct DevState {
   double *proc_ratio;   // [Sp] cpuTimeRatio of the slot's last attribution (power is derived)
   uint32_t *proc_node;  // [Sp] the node that attribution belonged to
   uint64_t *ctr_energy;
-  double *ctr_power, *ctr_cpu_delta, *ctr_cpu_total;
+  double *ctr_ratio, *ctr_cpu_delta, *ctr_cpu_total;  // container / VM power is derived (as processes')
+  uint32_t *ctr_node;
   uint64_t *vm_energy;
-  double *vm_power, *vm_cpu_delta;
+  double *vm_ratio, *vm_cpu_delta;
+  uint32_t *vm_node;
   uint64_t *pod_energy;
   double *pod_power, *pod_cpu_delta, *pod_cpu_total;
   uint64_t proc_slots, ctr_slots, vm_slots, pod_slots;
@@ -268,9 +284,9 @@ __device__ __forceinline__ Attr<Z> make_attr(const NodeShared &sh) {
 
 // process.go:118-148 (and its container/VM/pod twins) for one row.
 template <int Z>
-__device__ __forceinline__ void attribute_row(const Attr<Z> &a, uint32_t live, double delta,
-                                              bool is_new, const uint64_t (&prev)[Z],
-                                              uint64_t (&E)[Z], double (&P)[Z]) {
+__device__ __forceinline__ double attribute_row(const Attr<Z> &a, uint32_t live, double delta,
+                                                bool is_new, const uint64_t (&prev)[Z],
+                                                uint64_t (&E)[Z], double (&P)[Z]) {
   const double ratio = delta / a.nd;  // one IEEE division per row, never a reciprocal
 #pragma unroll
   for (int z = 0; z < Z; ++z) {
@@ -283,6 +299,7 @@ __device__ __forceinline__ void attribute_row(const Attr<Z> &a, uint32_t live, d
       P[z] = 0.0;
     }
   }
+  return ratio;
 }
 
 // process.go:118-148 for one process row: the energy totals, and the row's
@@ -361,18 +378,27 @@ __device__ __forceinline__ void export_node_zone(const kacc_interval &b, uint32_
   o[4 * Z] = static_cast<uint64_t>(__double_as_longlong(ip));
 }
 
-// One aggregate row (container / VM / pod): read-modify-write of its slot.
+// An aggregate row's outputs at slot s: energy totals; for a pod its powers,
+// for a container / VM its ratio and node (their power is derived on read as
+// a process's: the same guard, container.go:106-140, vm.go:78-109).
 template <int Z, bool NT>
-__device__ __forceinline__ void attribute_slot(const Attr<Z> &a, uint32_t live, double delta,
-                                               uint32_t w, uint64_t *__restrict__ energy,
-                                               double *__restrict__ power) {
-  const uint64_t s = w & KACC_SLOT_MASK;
-  uint64_t prev[Z], E[Z];
-  double P[Z];
-  load_row<Z>(energy, s, prev);
-  attribute_row<Z>(a, live, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
-  store_row<Z, NT, uint64_t>(energy, s, E);
-  store_row<Z, NT, double>(power, s, P);
+__device__ __forceinline__ void store_agg(const DevState &st, uint32_t role, uint64_t s, const uint64_t (&E)[Z],
+                                          const double (&P)[Z], double ratio, uint32_t node) {
+  if (role == 3) {
+    store_row<Z, NT, uint64_t>(st.pod_energy, s, E);
+    store_row<Z, NT, double>(st.pod_power, s, P);
+    return;
+  }
+  store_row<Z, NT, uint64_t>(role == 1 ? st.ctr_energy : st.vm_energy, s, E);
+  double *r = role == 1 ? st.ctr_ratio : st.vm_ratio;
+  uint32_t *nd = role == 1 ? st.ctr_node : st.vm_node;
+  if constexpr (NT) {
+    __builtin_nontemporal_store(ratio, r + s);
+    __builtin_nontemporal_store(node, nd + s);
+  } else {
+    r[s] = ratio;
+    nd[s] = node;
+  }
 }
 
 // A container's CPU time (informer.go:229-233, 481-486): delta and total summed
@@ -745,7 +771,6 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   const uint32_t j = index_of();
   // per-role tables, re-derived at each use (keeps 8 VGPRs of pointers dead)
   auto a_energy = [&]() { return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy; };
-  auto a_power = [&]() { return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power; };
   auto a_cpu_total = [&]() { return role == 1 ? st.ctr_cpu_total : st.pod_cpu_total; };
   auto a_cpu_delta = [&]() {
     return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
@@ -932,10 +957,9 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), a_s, a_prev);
     uint64_t E[Z];
     double P[Z];
-    attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0,
-                     a_prev, E, P);
-    store_row<Z, kNtAgg, uint64_t>(a_energy(), a_s, E);
-    store_row<Z, kNtAgg, double>(a_power(), a_s, P);
+    const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta,
+                                          (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
+    store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
     if (role == 3) export_pod<Z>(b, q0 + j, E, P);
   };
   if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
@@ -1530,11 +1554,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         }
         uint64_t E[Z];
         double P[Z];
-        attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, c_aE, E, P);
-        uint64_t *ae = role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy;
-        double *ap = role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
-        store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, uint64_t>(ae, a_s, E);
-        store_row<Z, kNtAggStores || (V & kCarryNtAgg) != 0, double>(ap, a_s, P);
+        const double ratio =
+            attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, c_aE, E, P);
+        store_agg<Z, kNtAggStores || (V & kCarryNtAgg) != 0>(st, role, a_s, E, P, ratio, n);
         if (role == 3) export_pod<Z>(b, rg.q0 + (tid - nc - nv), E, P);
 #pragma unroll
         for (int z = 0; z < Z; ++z) c_aE[z] = E[z];
@@ -1773,7 +1795,6 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     return role == 1 ? st.ctr_slots : role == 2 ? st.vm_slots : role == 3 ? st.pod_slots : 0;
   };
   auto energy_of = [&](uint32_t role) { return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy; };
-  auto power_of = [&](uint32_t role) { return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power; };
   auto cpu_total_of = [&](uint32_t role) { return role == 1 ? st.ctr_cpu_total : st.pod_cpu_total; };
   auto cpu_delta_of = [&](uint32_t role) {
     return role == 1 ? st.ctr_cpu_delta : role == 2 ? st.vm_cpu_delta : st.pod_cpu_delta;
@@ -1947,10 +1968,9 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     }
     uint64_t E[Z];
     double P[Z];
-    attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h], (a_w[h] & KACC_SLOT_NEW) != 0,
-                     a_prev[h], E, P);
-    store_row<Z, kNT && kNtAggStores, uint64_t>(energy_of(role), a_s, E);
-    store_row<Z, kNT && kNtAggStores, double>(power_of(role), a_s, P);
+    const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h],
+                                          (a_w[h] & KACC_SLOT_NEW) != 0, a_prev[h], E, P);
+    store_agg<Z, kNT && kNtAggStores>(st, role, a_s, E, P, ratio, n);
     if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P);
   }
   auto attr_batch = [&](int kb) {  // process.go:118-148
@@ -2389,9 +2409,6 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     auto energy_of = [&](uint32_t role) {
       return role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy;
     };
-    auto power_of = [&](uint32_t role) {
-      return role == 1 ? st.ctr_power : role == 2 ? st.vm_power : st.pod_power;
-    };
     uint32_t a_role = 0, a_beg = 0, a_end = 0, a_w = 0xffffffffu;
     if (utid < nagg) a_role = agg(utid, a_beg, a_end, a_w);
     const uint32_t a_s = a_w & KACC_SLOT_MASK;
@@ -2423,9 +2440,9 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       const uint64_t s = wd & KACC_SLOT_MASK;
       uint64_t E[Z];
       double P[Z];
-      attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, delta, (wd & KACC_SLOT_NEW) != 0, pv, E, P);
-      store_row<Z, kNT, uint64_t>(energy_of(role), s, E);
-      store_row<Z, kNT, double>(power_of(role), s, P);
+      const double ratio =
+          attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, delta, (wd & KACC_SLOT_NEW) != 0, pv, E, P);
+      store_agg<Z, kNT>(st, role, s, E, P, ratio, n);
     };
     // ---- C: owned containers / VMs (informer.go:223-273) ------------------------
     auto segment = [&](uint32_t role, uint32_t beg, uint32_t end, uint32_t wd, bool ok,
@@ -2495,9 +2512,9 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       const uint64_t s = a_w & KACC_SLOT_MASK;
       uint64_t E[Z];
       double P[Z];
-      attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
-      store_row<Z, kNT, uint64_t>(energy_of(a_role), s, E);
-      store_row<Z, kNT, double>(power_of(a_role), s, P);
+      const double ratio =
+          attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
+      store_agg<Z, kNT>(st, a_role, s, E, P, ratio, n);
       if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P);
     } else if (a_role == 3 && !a_ok) {
       export_pod_zero<Z>(b, qb + (utid - ncv));
@@ -2664,7 +2681,15 @@ __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, con
     double pr[kNsUnroll][Z];
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
-      const uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
+      uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
+#if KACC_NS_PROBE_PAIRED
+      if (kW == Z) {  // probe: record at / 2 of a [pod_slots / 2][2Z] view of the energy table
+        at = min(at >> 1, (pod_slots >> 1) - 1);
+        load_row<Z>(pe + at * 2 * Z, 0, er[u]);
+        load_row_f64<Z>(reinterpret_cast<const double *>(pe) + at * 2 * Z + Z, 0, pr[u]);
+        continue;
+      }
+#endif
       load_row<Z>(pe + at * kW, 0, er[u]);
       load_row_f64<Z>(pp + at * kW, 0, pr[u]);
     }
@@ -2860,12 +2885,14 @@ const TableDesc kTables[KACC_T_COUNT] = {
     {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},
     {8, 0, true, false},  {8, 0, true, false},  {8, 0, true, false},  {8, 0, false, false},
     {4, 0, false, false}, {8, 0, false, false}, {8, 0, false, false}, {4, 0, false, false},
-    {8, 1, true, false},  {8, 1, true, true},   {8, 2, true, false},  {8, 2, true, false},
-    {8, 2, false, false}, {8, 2, false, false}, {8, 3, true, false},  {8, 3, true, false},
+    {8, 1, true, false},  {8, 1, true, true},   {8, 2, true, false},  {8, 2, true, true},
+    {8, 2, false, false}, {8, 2, false, false}, {8, 3, true, false},  {8, 3, true, true},
     {8, 3, false, false}, {8, 4, true, false},  {8, 4, true, false},  {8, 4, false, false},
-    {8, 4, false, false}, {8, 1, false, false}, {4, 1, false, false},
+    {8, 4, false, false}, {8, 1, false, false}, {4, 1, false, false}, {8, 2, false, false},
+    {4, 2, false, false}, {8, 3, false, false}, {4, 3, false, false},
 };
-static_assert(KACC_T_PROC_POWER == 13 && KACC_T_PROC_RATIO == 25 && KACC_T_PROC_NODE == 26 && KACC_T_COUNT == 27,
+static_assert(KACC_T_PROC_POWER == 13 && KACC_T_PROC_RATIO == 25 && KACC_T_PROC_NODE == 26 &&
+                  KACC_T_CTR_RATIO == 27 && KACC_T_VM_NODE == 30 && KACC_T_COUNT == 31,
               "kTables rows follow the kacc_table enum");
 
 }  // namespace
@@ -2921,11 +2948,13 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.proc_ratio = (double *)T(KACC_T_PROC_RATIO);
   s.proc_node = (uint32_t *)T(KACC_T_PROC_NODE);
   s.ctr_energy = (uint64_t *)T(KACC_T_CTR_ENERGY);
-  s.ctr_power = (double *)T(KACC_T_CTR_POWER);
+  s.ctr_ratio = (double *)T(KACC_T_CTR_RATIO);
+  s.ctr_node = (uint32_t *)T(KACC_T_CTR_NODE);
   s.ctr_cpu_delta = (double *)T(KACC_T_CTR_CPU_DELTA);
   s.ctr_cpu_total = (double *)T(KACC_T_CTR_CPU_TOTAL);
   s.vm_energy = (uint64_t *)T(KACC_T_VM_ENERGY);
-  s.vm_power = (double *)T(KACC_T_VM_POWER);
+  s.vm_ratio = (double *)T(KACC_T_VM_RATIO);
+  s.vm_node = (uint32_t *)T(KACC_T_VM_NODE);
   s.vm_cpu_delta = (double *)T(KACC_T_VM_CPU_DELTA);
   s.pod_energy = (uint64_t *)T(KACC_T_POD_ENERGY);
   s.pod_power = (double *)T(KACC_T_POD_POWER);
@@ -3774,10 +3803,10 @@ static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   if (!count) return KACC_OK;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (kTables[t].derived) {  // KACC_T_PROC_POWER: derived into a scratch buffer, then copied
+  if (kTables[t].derived) {  // a derived power table: derived into a scratch buffer, then copied
     double *tmp = nullptr;
     KACC_HIP(ctx, hipMalloc(&tmp, count * sizeof(double)));
-    int rc = kacc_internal_proc_power(ctx, first, count, tmp, ctx->stream);
+    int rc = kacc_internal_derived_power(ctx, t, first, count, tmp, ctx->stream);
     hipError_t e = rc == KACC_OK ? hipStreamSynchronize(ctx->stream) : hipSuccess;
     if (rc == KACC_OK && e == hipSuccess) e = hipMemcpy(host, tmp, count * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipFree(tmp);
@@ -3894,8 +3923,10 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   return KACC_OK;
 }
 
-int kacc_internal_proc_power(kacc_ctx *ctx, uint64_t first, uint64_t count, double *out, void *stream) {
+int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, double *out, void *stream) {
   if (!ctx) return KACC_EINVAL;
+  const int kind = kacc_derived_kind(t);
+  if (kind < 0) return fail(ctx, KACC_EINVAL, "table %d is not derived", t);
   if (!count) return KACC_OK;
   if (!out) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
@@ -3903,7 +3934,7 @@ int kacc_internal_proc_power(kacc_ctx *ctx, uint64_t first, uint64_t count, doub
   const uint64_t blocks = (count + kacc::kBlock - 1) / kacc::kBlock;
   (void)hipGetLastError();
   hipLaunchKernelGGL(kacc::proc_power_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
-                     dim3(kacc::kBlock), 0, st, kacc_proc_derive(ctx), first, count, out);
+                     dim3(kacc::kBlock), 0, st, kacc_derive(ctx, static_cast<kacc_kind>(kind)), first, count, out);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
@@ -3928,8 +3959,10 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
   const uint64_t node = 76 + 96ull * Z;
   // Δ 8 + slot 4 in, previous totals 8Z in; totals 8Z + ratio 8 + node 4 out
   const uint64_t proc = 24 + 16ull * Z;
-  const uint64_t ctr = 32 + 24ull * Z;
-  const uint64_t vm = 16 + 24ull * Z;
+  // container: end 4 + slot 4 + previous CPU total 8 in, Δ 8 + total 8 out; previous
+  // energies 8Z in, energies 8Z + ratio 8 + node 4 out (power derived since ABI 3)
+  const uint64_t ctr = 44 + 16ull * Z;
+  const uint64_t vm = 28 + 16ull * Z;  // end 4 + slot 4 in, Δ 8 out; 16Z + 12 as a container
   const uint64_t pod = 32 + 24ull * Z;
   return N * node + P * proc + C * ctr + V * vm + Q * pod;
 }

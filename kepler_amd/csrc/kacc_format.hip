@@ -781,10 +781,10 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   kacc::fmt::Args a{};
   a.src = static_cast<const char *>(ctx->tables[t]) + first * 8;
-  double *derived = nullptr;  // KACC_T_PROC_POWER: the range derived first (kacc_derive.hpp)
-  if (t == KACC_T_PROC_POWER) {
+  double *derived = nullptr;  // a derived power table: the range derived first (kacc_derive.hpp)
+  if (kacc_derived_kind(t) >= 0) {
     KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&derived), count * 8, st));
-    const int rc = kacc_internal_proc_power(ctx, first, count, derived, st);
+    const int rc = kacc_internal_derived_power(ctx, t, first, count, derived, st);
     if (rc != KACC_OK) {
       (void)hipFreeAsync(derived, st);
       return rc;
@@ -863,7 +863,7 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   a.out_cap = out_cap;
   a.err = ctx->d_err;
   // temporaries, stream ordered: consts, lengths, tile sums (+ the derived rows of
-  // KACC_T_PROC_POWER, rows [first, first + count), kacc_derive.hpp)
+  // a derived power table, rows [first, first + count), kacc_derive.hpp)
   const uint64_t tiles = (lines + 1 + kacc::fmt::kTile - 1) / kacc::fmt::kTile;
   if (tiles > 0x7fffffffull) return kacc_fail(ctx, KACC_EINVAL, "format_lines: too many lines");
   const size_t scan_bytes = 8 * tiles;
@@ -871,7 +871,7 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   // every sub-buffer 256-B aligned (the scan's look-back state needs aligned storage)
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
   const uint64_t off_len = 1024, off_scan = al(off_len + 8 * (lines + 1));
-  const bool derived = t == KACC_T_PROC_POWER;
+  const bool derived = kacc_derived_kind(t) >= 0;
   const uint64_t off_derived = al(off_scan + scan_bytes);
   KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), derived ? off_derived + 8 * count * Z : off_scan + scan_bytes,
                                st));
@@ -885,7 +885,7 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   if (derived) {
     a.src = tmp + off_derived;
     a.src_first = first * Z;
-    if ((rc = kacc_internal_proc_power(ctx, first * Z, count * Z, reinterpret_cast<double *>(tmp + off_derived), st)) !=
+    if ((rc = kacc_internal_derived_power(ctx, t, first * Z, count * Z, reinterpret_cast<double *>(tmp + off_derived), st)) !=
         KACC_OK)
       return done(rc);
   }

@@ -233,8 +233,8 @@ namespace unpack {
 constexpr int kThreads = 256;
 
 // out[dest ? dest[i] : i] = the tables' row of slot word w[i] (energy, power per zone).
-// Processes (tp NULL): power derived from the slot's ratio and its node's tables
-// (kacc_derive.hpp).
+// Processes / containers / VMs (tp NULL): power derived from the slot's ratio and
+// its node's tables (kacc_derive.hpp).
 template <int Z>
 __global__ __launch_bounds__(kThreads) void unpack_kernel(uint32_t n, const uint32_t *w, const uint32_t *dest,
                                                           uint64_t cap, const uint64_t *te, const double *tp,
@@ -347,8 +347,9 @@ int kacc_unpack(kacc_ctx *ctx, kacc_kind kind, uint32_t n, const uint32_t *slot_
                        : kind == KACC_KIND_VM ? ctx->cfg.vm_slots
                                               : ctx->cfg.pod_slots;
   const uint64_t *e = static_cast<const uint64_t *>(ctx->tables[te]);
-  const double *p = kind == KACC_KIND_PROC ? nullptr : static_cast<const double *>(ctx->tables[te + 1]);
-  const kacc::ProcDerive pd = kacc_proc_derive(ctx);
+  // processes, containers, VMs: power derived (kacc_derive.hpp); pods: the table
+  const double *p = kind == KACC_KIND_POD ? static_cast<const double *>(ctx->tables[te + 1]) : nullptr;
+  const kacc::ProcDerive pd = kacc_derive(ctx, kind);
   const uint32_t grid = (n + kacc::unpack::kThreads - 1) / kacc::unpack::kThreads;
   (void)hipGetLastError();
 #define KACC_UNPACK(Z)                                                                                          \

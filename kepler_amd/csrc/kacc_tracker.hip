@@ -44,7 +44,7 @@ constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node c
 
 struct Args {
   const uint64_t *tab_e;
-  const double *tab_p;  // NULL for processes: power derived (kacc_derive.hpp) from pd
+  const double *tab_p;  // NULL for processes / containers / VMs: power derived (kacc_derive.hpp) from pd
   ProcDerive pd;
   uint64_t min_e;
   int64_t max_size;
@@ -292,15 +292,16 @@ void kind_tables(const kacc_ctx *ctx, kacc_kind k, const uint64_t **e, const dou
                    : k == KACC_KIND_VM ? KACC_T_VM_ENERGY
                                        : KACC_T_POD_ENERGY;
   *e = static_cast<const uint64_t *>(ctx->tables[base]);
-  // a process's power is derived (kacc_derive.hpp) from its ratio and its node's
-  // tables of the same interval: the tracker must run before that node's next one
-  *p = k == KACC_KIND_PROC ? nullptr : static_cast<const double *>(ctx->tables[base + 1]);
+  // a process's (container's, VM's) power is derived (kacc_derive.hpp) from its
+  // ratio and its node's tables of the same interval: the tracker must run before
+  // that node's next one
+  *p = k == KACC_KIND_POD ? static_cast<const double *>(ctx->tables[base + 1]) : nullptr;
 }
 
 kacc::trk::Args tracker_args(const kacc_tracker *t) {
   kacc::trk::Args a{};
   kind_tables(t->ctx, t->kind, &a.tab_e, &a.tab_p);
-  a.pd = kacc_proc_derive(t->ctx);
+  a.pd = kacc_derive(t->ctx, t->kind);
   a.min_e = t->min_e;
   a.max_size = t->max_size;
   a.Z = t->Z;

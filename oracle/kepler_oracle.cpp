@@ -235,12 +235,16 @@ static void node_interval(kor_state *st, const kacc_interval *b, uint32_t n, int
     const uint64_t s = w & KACC_SLOT_MASK;
     attribute(Z, st->ctr_cpu_delta[s], node_delta, nz, false, first_read,
               (w & KACC_SLOT_NEW) != 0, st->ctr_energy + s * Z, st->ctr_power + s * Z);
+    if (st->ctr_ratio) st->ctr_ratio[s] = st->ctr_cpu_delta[s] / node_delta;  // container.go:118
+    if (st->ctr_node) st->ctr_node[s] = n;
   }
   for (uint32_t v = r.v0; v < r.v1; ++v) {
     const uint32_t w = b->vm_slot[v];
     const uint64_t s = w & KACC_SLOT_MASK;
     attribute(Z, st->vm_cpu_delta[s], node_delta, nz, false, first_read,
               (w & KACC_SLOT_NEW) != 0, st->vm_energy + s * Z, st->vm_power + s * Z);
+    if (st->vm_ratio) st->vm_ratio[s] = st->vm_cpu_delta[s] / node_delta;  // vm.go:89
+    if (st->vm_node) st->vm_node[s] = n;
   }
   // pod.go:70-73 returns early when no pod is running: nothing to write.
   for (uint32_t q = r.q0; q < r.q1; ++q) {

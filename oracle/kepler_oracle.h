@@ -55,6 +55,10 @@ typedef struct kor_state {
    * the row's cpuTimeRatio (process.go:128) and its node, per slot */
   double *proc_ratio;
   uint32_t *proc_node;
+  double *ctr_ratio; /* the same for containers and VMs (container.go:118, vm.go:89) */
+  uint32_t *ctr_node;
+  double *vm_ratio;
+  uint32_t *vm_node;
 } kor_state;
 
 /* Scalar Go-semantics helpers (exported so the KATs can pin them directly). */

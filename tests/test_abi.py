@@ -77,13 +77,14 @@ int main(void) {{
 
 def test_interval_bytes_formula(lib):
     # node 76+96Z, proc 24+16Z (Δ 8 + slot 4 + prev 8Z in; totals 8Z + ratio 8 +
-    # node 4 out: the power is derived, ABI 3), ctr 32+24Z, vm 16+24Z, pod 32+24Z
+    # node 4 out: the power is derived, ABI 3), ctr 44+16Z, vm 28+16Z (ratio + node stored
+    # for those too), pod 32+24Z (pod power stored)
     z = 4
     assert accel.interval_bytes(z, 1, 0, 0, 0, 0) == 76 + 96 * z
     assert accel.interval_bytes(z, 0, 1, 0, 0, 0) == 24 + 16 * z
-    assert accel.interval_bytes(z, 0, 0, 1, 1, 1) == (32 + 16 + 32) + 3 * 24 * z
+    assert accel.interval_bytes(z, 0, 0, 1, 1, 1) == (44 + 28 + 32) + (16 + 16 + 24) * z
     n, p, c, v, q = 10_000, 20_000_000, 1_975_000, 200_000, 711_000
-    assert accel.interval_bytes(z, n, p, c, v, q) == n * 460 + p * 88 + c * 128 + v * 112 + q * 128
+    assert accel.interval_bytes(z, n, p, c, v, q) == n * 460 + p * 88 + c * 108 + v * 92 + q * 128
 
 
 def test_create_error_visible_from_another_thread(lib):

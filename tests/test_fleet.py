@@ -3,7 +3,7 @@
 import numpy as np
 import pytest
 
-from kepler_amd import fleet, shard
+from kepler_amd import accel, fleet, shard
 
 
 def check_layout(L):
@@ -68,7 +68,7 @@ def test_subset_matches_full_fleet(oracle_lib):
         per = len(f) // (L.n_nodes if kind == "node" else L.capacities()[f"{kind}_slots"])
         got = f.reshape(-1, per)[maps[kind]].reshape(-1)
         want = sub.state[name][: len(got)]
-        if name == "proc_node":  # node indices of the subset -> the fleet's
+        if name in accel.NODE_INDEX_TABLES:  # node indices of the subset -> the fleet's
             want = maps["node"][want]
         np.testing.assert_array_equal(got, want, err_msg=name)
 

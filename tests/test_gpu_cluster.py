@@ -56,7 +56,7 @@ def _check_shard_tables(shard_acc, sl, lo, hi, maps, want_state, zones, nodes_to
             continue
         want = full.reshape(-1, per)[idx]
         g = got.reshape(-1, per)[: len(idx)]
-        if name == "proc_node":  # shard-local node indices -> the fleet's
+        if name in accel.NODE_INDEX_TABLES:  # shard-local node indices -> the fleet's
             g = g + lo
         np.testing.assert_array_equal(g, want, err_msg=f"shard [{lo},{hi}) {name}")
 
@@ -238,7 +238,7 @@ def test_config4_full_size_sharded_8_ways():
             n_rows = (hi - lo) if kind == "node" else sl.capacities()[f"{kind}_slots"]
             per = len(got) // n_rows
             want = full.download(name, base[kind] * per, len(got))
-            if name == "proc_node":  # shard-local node indices -> the fleet's
+            if name in accel.NODE_INDEX_TABLES:  # shard-local node indices -> the fleet's
                 got = got + lo
             np.testing.assert_array_equal(got, want, err_msg=f"shard [{lo},{hi}) {name}")
     # sampled oracle parity of the unsharded context
@@ -248,7 +248,7 @@ def test_config4_full_size_sharded_8_ways():
         per = full.table_info(name)[1] // cap
         got = _gather_rows(full, name, omaps[kind], per)
         want = ora.state[name]
-        if name == "proc_node":  # the sample's node indices -> the fleet's
+        if name in accel.NODE_INDEX_TABLES:  # the sample's node indices -> the fleet's
             want = omaps["node"][want]
         np.testing.assert_array_equal(got, want, err_msg=name)
     # cluster namespace totals (RCCL path) == one context's namespace kernel

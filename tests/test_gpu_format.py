@@ -61,11 +61,11 @@ def edge_powers():
 def test_format_edges():
     e, p = edge_energies(), edge_powers()
     n = max(e.size, p.size)
-    # power values through a stored power table (KACC_T_PROC_POWER is derived: not uploadable)
-    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=n, vm_slots=1, pod_slots=1)
+    # power values through the stored power table (process / container / VM power is derived)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=n)
     acc.upload("proc_energy", np.resize(e, n))
-    acc.upload("ctr_power", np.resize(p, n))
-    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "ctr_power", n)
+    acc.upload("pod_power", np.resize(p, n))
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "pod_power", n)
     for i in range(n):
         ev, pv = int(np.resize(e, n)[i]), float(np.resize(p, n)[i])
         assert got_e[i] == write_float(joules(ev)), (ev, got_e[i])
@@ -83,10 +83,10 @@ def test_format_random(kind):
     else:  # attribution-like: µJ totals and µW powers
         e = (rng.lognormal(18, 4, size=n)).astype(np.uint64)
         p = rng.lognormal(12, 3, size=n) * rng.choice([1.0, 1.0, 1.0, 0.0], size=n)
-    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=n, vm_slots=1, pod_slots=1)
+    acc = accel.Accel(1, nodes=1, proc_slots=n, ctr_slots=1, vm_slots=1, pod_slots=n)
     acc.upload("proc_energy", e)
-    acc.upload("ctr_power", p)
-    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "ctr_power", n)
+    acc.upload("pod_power", p)
+    got_e, got_p = device_text(acc, "proc_energy", n), device_text(acc, "pod_power", n)
     bad = []
     for i in range(n):
         we = write_float(joules(int(e[i])))
@@ -238,6 +238,12 @@ def test_format_derived_process_power():
         acc.device_ptr("proc_power")
     with pytest.raises(accel.AccelError):  # not uploadable
         acc.upload("proc_power", np.zeros(4), 0)
+    for tname in ("ctr_power", "vm_power"):  # containers and VMs are derived the same way
+        cp = acc.download(tname)
+        gc = device_text(acc, tname, cp.size)
+        for i in range(0, cp.size, 3):
+            want = write_float(watts(float(cp[i])))
+            assert gc[i] == want or (math.isnan(cp[i]) and gc[i] == "NaN"), (tname, i, cp[i], gc[i], want)
     pp = acc.download("proc_power")
     n = pp.size
     got = device_text(acc, "proc_power", n)

@@ -286,7 +286,7 @@ def test_config3_full_size_properties_and_sampled_parity():
         idx = maps[kind]
         got = full.reshape(-1, per)[idx].reshape(-1)
         want = ora.state[name]
-        if name == "proc_node":  # the sample's node indices -> the fleet's
+        if name in accel.NODE_INDEX_TABLES:  # the sample's node indices -> the fleet's
             want = maps["node"][want]
         np.testing.assert_array_equal(got, want, err_msg=name)
     # conservation on every node: sum of process power == ActivePower (rel 1e-9),
