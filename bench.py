@@ -86,6 +86,13 @@ def parse():
                          "the export stores cost 26 us and the concurrent partial sums slow the next interval more "
                          "than they save at config 3, profiles/r03/exports_ablation); tables+writes = the export "
                          "stores alone (ablation)")
+    ap.add_argument("--comm-wait", choices=["auto", "always"], default="auto",
+                    help="auto: the compute stream waits for the comm stream's all-reduce of step k-2 only when "
+                         "there is one (N > 1); at one rank the totals are the partial sums and the comm stream "
+                         "is idle, so no cross-stream packet is issued; always: issue it anyway (ablation)")
+    ap.add_argument("--step-events", choices=["all", "interval", "none"], default="all",
+                    help="HIP events recorded per timed step: all = around the interval and the totals; interval = "
+                         "around the interval only; none = only the wall clock (ablation: the cost of event markers)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -515,10 +522,12 @@ def measure(args, w, rank, world, stream, comm_stream):
     done = [torch.cuda.Event(), torch.cuda.Event()]
     used = [False, False]
     compute = torch.cuda.current_stream()
+    # one rank, one shard: kacc_allreduce_namespaces enqueues nothing on the comm stream
+    comm = world > 1 or w.exports or args.comm_wait == "always"
 
     def step(k, ev=None):
         b = k % 2
-        if used[b]:  # stream-level wait for step k-2's totals (its buffers are reused; no host sync)
+        if used[b] and comm:  # stream-level wait for step k-2's totals (its buffers are reused; no host sync)
             compute.wait_event(done[b])
         if ev is not None:
             ev[0].record()
@@ -530,9 +539,10 @@ def measure(args, w, rank, world, stream, comm_stream):
         rc = reduce_fn(cl.handle, w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
-        if ev is not None:
+        if ev is not None and args.step_events == "all":
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
-        done[b].record(comm_stream)
+        if comm:
+            done[b].record(comm_stream)
         used[b] = True
 
     for k in range(args.warmup):
@@ -545,14 +555,14 @@ def measure(args, w, rank, world, stream, comm_stream):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i, events[i])
+        step(args.warmup + i, events[i] if args.step_events != "none" else None)
     torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     acc.sync(stream)  # surfaces any device-detected range error
-    kernel_ms = [a.elapsed_time(b) / K for a, b, _ in events]  # per interval
-    totals_ms = [b.elapsed_time(c) for _, b, c in events]  # per step
+    kernel_ms = [a.elapsed_time(b) / K for a, b, _ in events] if args.step_events != "none" else [float("nan")]
+    totals_ms = [b.elapsed_time(c) for _, b, c in events] if args.step_events == "all" else [float("nan")]
     wall_t = torch.tensor([wall], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
