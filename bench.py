@@ -90,9 +90,14 @@ def parse():
                     help="auto: the compute stream waits for the comm stream's all-reduce of step k-2 only when "
                          "there is one (N > 1); at one rank the totals are the partial sums and the comm stream "
                          "is idle, so no cross-stream packet is issued; always: issue it anyway (ablation)")
-    ap.add_argument("--step-events", choices=["all", "interval", "none"], default="all",
-                    help="HIP events recorded per timed step: all = around the interval and the totals; interval = "
-                         "around the interval only; none = only the wall clock (ablation: the cost of event markers)")
+    ap.add_argument("--step-events", choices=["separate", "inline", "markers"], default="separate",
+                    help="how the kernels are timed with HIP events: separate = the timed region has NO event "
+                         "packet between its kernels (value, ms_per_step) and a second timed pass over the same "
+                         "number of steps right after it carries a start/stop pair on the dispatch packets of each "
+                         "step's interval and totals launches (kacc_time_next_launch) -> kernel_ms, "
+                         "totals_compute_ms; inline = those launch events inside the timed region; markers = "
+                         "hipEventRecord markers around them inside the timed region (round 2).  Every event "
+                         "packet costs a stream gap: ~9 us per step, profiles/r03/events")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -428,7 +433,7 @@ class Workload:
         self.Z = Z = layout.zones
         self.K = K
         sim = fleet.FleetSim(layout, seed=fleet.SEED + self.lo)
-        n_steps = args.warmup + args.steps
+        n_steps = total_steps(args)
         n_ivs = n_steps * K  # every interval has its own node counters / clocks
         n_distinct = max(1, min(args.distinct, n_ivs))
         self.prime = sim.next_interval()  # first read (monitor.go:326-330), untimed
@@ -488,6 +493,12 @@ class Workload:
         self.acc.close()
 
 
+def total_steps(args):
+    """Warm-up steps, the timed steps and (--step-events separate) the kernel-timing pass: every
+    step has its own node counters / clocks (monotonic, as a node's RAPL readings)."""
+    return args.warmup + args.steps * (2 if args.step_events == "separate" else 1)
+
+
 def measure(args, w, rank, world, stream, comm_stream):
     """W untimed warm-up steps, then exactly `steps` steps bracketed by barrier + synchronize;
     returns (max wall seconds over ranks, per-interval kernel ms of the launch stream).  A step =
@@ -525,48 +536,76 @@ def measure(args, w, rank, world, stream, comm_stream):
     # one rank, one shard: kacc_allreduce_namespaces enqueues nothing on the comm stream
     comm = world > 1 or w.exports or args.comm_wait == "always"
 
-    def step(k, ev=None):
+    time_next = lib.kacc_time_next_launch
+
+    def step(k, ev=None, markers=False):
         b = k % 2
         if used[b] and comm:  # stream-level wait for step k-2's totals (its buffers are reused; no host sync)
             compute.wait_event(done[b])
         if ev is not None:
-            ev[0].record()
+            if markers:
+                ev[0].record()
+            else:  # start / stop on the interval's kernels' dispatch packets
+                time_next(acc.ctx, ev[0], ev[1])
         rc = lib.kacc_run_intervals(acc.ctx, w.iv_arrays[k], K, cstream)
         if rc != accel.KACC_OK:
             acc._check(rc)
         if ev is not None:
-            ev[1].record()
+            if markers:
+                ev[1].record()
+            else:  # the totals' partial-sum kernel (compute stream)
+                time_next(acc.ctx, ev[2], ev[3])
         rc = reduce_fn(cl.handle, w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
-        if ev is not None and args.step_events == "all":
+        if ev is not None and markers:
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
         if comm:
             done[b].record(comm_stream)
         used[b] = True
 
+    def timed(first, evs=None, markers=False):
+        """`steps` steps from step index `first`, bracketed by barrier + synchronize: wall seconds."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(first + i, evs[i] if evs else None, markers)
+        torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        acc.sync(stream)  # surfaces any device-detected range error
+        return wall
+
     for k in range(args.warmup):
         step(k)
     acc.sync(stream)
     torch.cuda.synchronize()
-    events = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, events[i] if args.step_events != "none" else None)
-    torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    acc.sync(stream)  # surfaces any device-detected range error
-    kernel_ms = [a.elapsed_time(b) / K for a, b, _ in events] if args.step_events != "none" else [float("nan")]
-    totals_ms = [b.elapsed_time(c) for _, b, c in events] if args.step_events == "all" else [float("nan")]
-    wall_t = torch.tensor([wall], dtype=torch.float64)
+    tevs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
+    markers = args.step_events == "markers"
+    if not markers:  # torch creates an event on its first record; the library re-records it
+        for ev in tevs:
+            for e in ev:
+                e.record()
+        torch.cuda.synchronize()
+    hev = tevs if markers else [tuple(ctypes.c_void_p(e.cuda_event) for e in ev) for ev in tevs]
+    if args.step_events == "separate":
+        wall = timed(args.warmup)  # the timed region: kernels and totals only
+        wall_ev = timed(args.warmup + args.steps, hev)  # kernel timing: the same steps with launch events
+    else:
+        wall = wall_ev = timed(args.warmup, hev, markers)
+    if markers:  # interval, then interval end -> partial sums end
+        kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
+        totals_ms = [b.elapsed_time(c) for _, b, c, _ in tevs]
+    else:  # kernels only: interval start -> end, partial sums start -> end
+        kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
+        totals_ms = [c.elapsed_time(d) for _, _, c, d in tevs]
+    wall_t = torch.tensor([wall, wall_ev], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-    return float(wall_t.item()), kernel_ms, totals_ms
+    return float(wall_t[0].item()), kernel_ms, totals_ms, float(wall_t[1].item())
 
 
 def main():
@@ -605,7 +644,7 @@ def main():
     w.acc.sync(stream)
     del prime_t
     log(rank, f"[bench] setup {time.time() - t_setup:.1f}s")
-    wall_max, kernel_ms, totals_ms = measure(args, w, rank, world, stream, comm_stream)
+    wall_max, kernel_ms, totals_ms, wall_ev = measure(args, w, rank, world, stream, comm_stream)
 
     # same-box reference for the roofline: a 1.28 GB device-to-device copy
     src = torch.empty(160 * 1024 * 1024, dtype=torch.float64, device="cuda")
@@ -680,7 +719,16 @@ def main():
         "kernel_ms": k_avg_ms,
         "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
         "step_minus_kernel_ms": wall_max * 1e3 / args.steps - k_avg_ms * K,
-        "totals_compute_ms": float(np.mean(totals_ms)),  # interval end -> partial sums end, compute stream
+        "totals_compute_ms": float(np.mean(totals_ms)),  # the partial-sum kernel (launch) / interval end -> its end
+        "kernel_timing": {
+            "step_events": args.step_events,
+            "ms_per_step_timing_pass": wall_ev * 1e3 / args.steps,
+            "note": ("timed region without event packets; kernel_ms / totals_compute_ms from HIP events on the "
+                     "dispatch packets of the interval and totals launches (kacc_time_next_launch, the launch "
+                     "stream) over a second timed pass of the same number of steps right after it"
+                     if args.step_events == "separate" else
+                     "HIP events inside the timed region (" + args.step_events + ")"),
+        },
         "roofline": {
             "bound": "hbm",
             "achieved": achieved,
@@ -740,7 +788,7 @@ def main():
         wk.acc.run_interval(interval_from_tensors(prime_t, wk.sizes), stream)
         wk.acc.sync(stream)
         del prime_t
-        wwall, wkms, _ = measure(args, wk, rank, world, stream, comm_stream)
+        wwall, wkms, _, _ = measure(args, wk, rank, world, stream, comm_stream)
         wp = torch.tensor([wk.sizes["n_procs"]], dtype=torch.float64)
         dist.all_reduce(wp)
         result["weak_scaling"] = {"value": float(wp.item()) * K * args.steps / wwall, "unit": "proc-attr/s",

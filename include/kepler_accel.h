@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define KACC_ABI_VERSION 3u
+#define KACC_ABI_VERSION 4u
 #define KACC_MAX_ZONES 8u
 
 /* Status codes. */
@@ -250,8 +250,8 @@ typedef enum kacc_table {
   KACC_T_VM_ENERGY,             /* u64 [Sv*Z]                                */
   KACC_T_VM_POWER,              /* f64 [Sv*Z] (DERIVED)                      */
   KACC_T_VM_CPU_DELTA,          /* f64 [Sv]  resource.VirtualMachine.CPUTimeDelta */
-  KACC_T_POD_ENERGY,            /* u64 [Sq*Z]                                */
-  KACC_T_POD_POWER,             /* f64 [Sq*Z]                                */
+  KACC_T_POD_ENERGY,            /* u64 [Sq*Z] (stored in pod records, below) */
+  KACC_T_POD_POWER,             /* f64 [Sq*Z] (stored in pod records, below) */
   KACC_T_POD_CPU_DELTA,         /* f64 [Sq]  resource.Pod.CPUTimeDelta       */
   KACC_T_POD_CPU_TOTAL,         /* f64 [Sq]  resource.Pod.CPUTotalTime       */
   KACC_T_PROC_RATIO,            /* f64 [Sp]  cpuTimeRatio of the slot's last attribution
@@ -297,6 +297,15 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *dev_batch, void *strea
  * are one kernel launch (bit-identical to K launches).                      */
 int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t count, void *stream);
 int kacc_sync(kacc_ctx *ctx, void *stream);
+/* Measurement hook (no reference counterpart; bench.py and profiling): the
+ * NEXT call on ctx that launches kernels (kacc_run_interval, kacc_run_intervals,
+ * or this context's cluster partial sums in kacc_allreduce_namespaces /
+ * kacc_allreduce_exports) records `start_event` (a hipEvent_t) when its first
+ * kernel starts and `stop_event` when its last kernel ends.  The events ride on
+ * the kernels' own dispatch packets (hipExtLaunchKernelGGL): no marker packet
+ * is queued between two kernels, so timing every step costs no stream gap.
+ * Either event may be NULL; the hook is consumed by that one call.           */
+int kacc_time_next_launch(kacc_ctx *ctx, void *start_event, void *stop_event);
 
 /* Host-side layout check of a batch held in host memory (O(N+C+V+Q+P)). */
 int kacc_validate_host(const kacc_ctx *ctx, const kacc_interval *host_batch);
@@ -332,8 +341,15 @@ void kacc_batch_free(kacc_ctx *ctx, kacc_batch *batch);
 /* ---- state access -------------------------------------------------------- */
 /* Element size in bytes and element count of a table. */
 int kacc_table_info(const kacc_ctx *ctx, kacc_table t, uint64_t *elem_bytes, uint64_t *count);
-/* Device pointer of a table (for zero-copy readers on the same device). */
+/* Device pointer of a table's first element (for zero-copy readers on the same
+ * device).  Slot s's row starts row_stride elements after slot s-1's: Z for a
+ * zoned table, 1 for a scalar one, and 2Z for the two pod tables, which are
+ * stored as one record per pod slot — its Z energy words, then its Z power
+ * words (KACC_T_POD_POWER's pointer is KACC_T_POD_ENERGY's + Z elements) — so
+ * that the namespace totals gather ONE 64-B record per pod at Z = 4.
+ * kacc_table_download / upload / format take logical [slot*Z + z] ranges.     */
 int kacc_table_device_ptr(kacc_ctx *ctx, kacc_table t, void **dev_ptr);
+int kacc_table_row_stride(const kacc_ctx *ctx, kacc_table t, uint64_t *stride);
 /* Synchronous copies of `count` elements starting at element `first`. */
 int kacc_table_download(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host_dst);
 int kacc_table_upload(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const void *host_src);

@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KACC_LIB", os.path.join(_HERE, "lib", "libkepler_accel.so"))  # KACC_LIB: A/B builds
 
-KACC_ABI_VERSION = 3
+KACC_ABI_VERSION = 4
 KACC_MAX_ZONES = 8
 KACC_OK = 0
 KACC_EINVAL = -1
@@ -125,6 +125,7 @@ EXPORTS = [
     "kacc_run_interval",
     "kacc_run_intervals",
     "kacc_sync",
+    "kacc_time_next_launch",
     "kacc_validate_host",
     "kacc_batch_alloc",
     "kacc_batch_submit",
@@ -132,6 +133,7 @@ EXPORTS = [
     "kacc_batch_free",
     "kacc_table_info",
     "kacc_table_device_ptr",
+    "kacc_table_row_stride",
     "kacc_table_download",
     "kacc_table_upload",
     "kacc_namespace_totals",
@@ -281,6 +283,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                       POINTER(ctypes.c_uint64), c_void_p]
     lib.kacc_run_intervals.argtypes = [c_void_p, POINTER(KaccInterval), ctypes.c_uint32, c_void_p]
     lib.kacc_sync.argtypes = [c_void_p, c_void_p]
+    lib.kacc_time_next_launch.argtypes = [c_void_p, c_void_p, c_void_p]
     lib.kacc_validate_host.argtypes = [c_void_p, POINTER(KaccInterval)]
     lib.kacc_batch_alloc.argtypes = [c_void_p, POINTER(KaccShape), POINTER(c_void_p), POINTER(POINTER(KaccInterval))]
     lib.kacc_pack.argtypes = [POINTER(KaccRecords), POINTER(KaccPacked), c_uint32]
@@ -306,6 +309,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_batch_free.restype = None
     lib.kacc_table_info.argtypes = [c_void_p, c_int, POINTER(c_uint64), POINTER(c_uint64)]
     lib.kacc_table_device_ptr.argtypes = [c_void_p, c_int, POINTER(c_void_p)]
+    lib.kacc_table_row_stride.argtypes = [c_void_p, c_int, POINTER(c_uint64)]
     lib.kacc_table_download.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
     lib.kacc_table_upload.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
     lib.kacc_namespace_totals.argtypes = [
@@ -524,6 +528,12 @@ class Accel:
         self._check(self.lib.kacc_debug_carry_stamps(self.ctx, arr, len(dev_intervals), c_void_p(stream or None),
                                                      variant, c_void_p(d_out)))
 
+    def time_next_launch(self, start_event: int, stop_event: int) -> None:
+        """kacc_time_next_launch: the next launching call records these hipEvent_t handles on its
+        first kernel's start and its last kernel's end (dispatch packets, no marker packets)."""
+        self._check(self.lib.kacc_time_next_launch(self.ctx, c_void_p(start_event or None),
+                                                   c_void_p(stop_event or None)))
+
     def sync(self, stream: int = 0) -> None:
         self._check(self.lib.kacc_sync(self.ctx, c_void_p(stream or None)))
 
@@ -550,6 +560,12 @@ class Accel:
     def upload(self, name: str, values: np.ndarray, first: int = 0) -> None:
         v = np.ascontiguousarray(values, dtype=TABLES[TABLE_INDEX[name]][1])
         self._check(self.lib.kacc_table_upload(self.ctx, TABLE_INDEX[name], first, v.size, v.ctypes.data))
+
+    def row_stride(self, name: str) -> int:
+        """kacc_table_row_stride: elements between two slots' rows (2Z for the pod tables' records)."""
+        s = c_uint64()
+        self._check(self.lib.kacc_table_row_stride(self.ctx, TABLE_INDEX[name], ctypes.byref(s)))
+        return s.value
 
     def device_ptr(self, name: str) -> int:
         p = c_void_p()

@@ -146,9 +146,9 @@ __global__ __launch_bounds__(kThreads) void pod_pack_kernel(uint32_t q, const ui
     return;
   }
 #pragma unroll
-  for (int z = 0; z < Z; ++z) {
-    out_e[o + z] = pe[s * Z + z];
-    out_p[o + z] = pp[s * Z + z];
+  for (int z = 0; z < Z; ++z) {  // a pod slot's row: one [energy Z | power Z] record (kacc_table_row_stride)
+    out_e[o + z] = pe[s * 2 * Z + z];
+    out_p[o + z] = pp[s * 2 * Z + z];
   }
 }
 

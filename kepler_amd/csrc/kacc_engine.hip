@@ -54,12 +54,6 @@ constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 6
 #endif
 constexpr int kNsLanes = KACC_NS_LANES;      // lanes per namespace (namespace_kernel)
 constexpr int kNsUnroll = KACC_NS_UNROLL;    // pods in flight per namespace lane
-// KACC_NS_PROBE_PAIRED=1: timing probe only (wrong sums) — the namespace gather
-// reads one 64-B record per pod (energy and power rows side by side) instead of
-// two 32-B rows of two tables
-#ifndef KACC_NS_PROBE_PAIRED
-#define KACC_NS_PROBE_PAIRED 0
-#endif
 
 // Debug variants (kacc_debug_run_variant, timing ablations only; results of a
 // variant != 0 are NOT the reference semantics).
@@ -251,6 +245,17 @@ __device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, cons
   }
 }
 
+// Pod rows are stored as one record per slot: the Z energy words then the Z
+// power words (KACC_T_POD_POWER's base is KACC_T_POD_ENERGY's + Z words), so a
+// pod's row is ONE 64-B gather at Z = 4 for the namespace totals (two 32-B rows
+// of two tables before: cluster partials 31.5 -> 22.0 us at config 3,
+// profiles/r03/abns).  load_row / store_row address base + s*Z, so a pod slot s
+// is passed as row 2s.
+constexpr uint64_t kPodRowScale = 2;
+__device__ __forceinline__ uint64_t pod_row(uint64_t s) { return s * kPodRowScale; }
+// the row index of aggregate slot s in its role's tables (1 container, 2 VM, 3 pod)
+__device__ __forceinline__ uint64_t agg_row(uint32_t role, uint64_t s) { return role == 3 ? pod_row(s) : s; }
+
 // Node-uniform attribution parameters (SGPRs) for the row passes.
 template <int Z>
 struct Attr {
@@ -385,8 +390,8 @@ template <int Z, bool NT>
 __device__ __forceinline__ void store_agg(const DevState &st, uint32_t role, uint64_t s, const uint64_t (&E)[Z],
                                           const double (&P)[Z], double ratio, uint32_t node) {
   if (role == 3) {
-    store_row<Z, NT, uint64_t>(st.pod_energy, s, E);
-    store_row<Z, NT, double>(st.pod_power, s, P);
+    store_row<Z, NT, uint64_t>(st.pod_energy, pod_row(s), E);
+    store_row<Z, NT, double>(st.pod_power, pod_row(s), P);
     return;
   }
   store_row<Z, NT, uint64_t>(role == 1 ? st.ctr_energy : st.vm_energy, s, E);
@@ -590,8 +595,8 @@ __device__ __forceinline__ void export_skipped(const kacc_interval &b, const Dev
       }
       uint64_t E[Z];
       double P[Z];
-      load_row<Z>(st.pod_energy, sl, E);
-      load_row_f64<Z>(st.pod_power, sl, P);
+      load_row<Z>(st.pod_energy, pod_row(sl), E);
+      load_row_f64<Z>(st.pod_power, pod_row(sl), P);
       export_pod<Z>(b, q, E, P);
     }
   }
@@ -843,7 +848,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   uint64_t a_prev[Z];
   double a_total = 0.0;
   if (a_ok) {
-    if constexpr ((V & kVarLateAgg) == 0) load_row<Z>(a_energy(), a_s, a_prev);
+    if constexpr ((V & kVarLateAgg) == 0) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
     if (role != 2 && !(a_w & KACC_SLOT_NEW)) a_total = a_cpu_total()[a_s];
   } else {
 #pragma unroll
@@ -954,7 +959,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       if (role == 3) export_pod_zero<Z>(b, q0 + j);
       return;
     }
-    if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), a_s, a_prev);
+    if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
     uint64_t E[Z];
     double P[Z];
     const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta,
@@ -1420,7 +1425,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           }
         }
         if (a_moved) {
-          load_row<Z>(role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy, a_s, c_aE);
+          load_row<Z>(role == 1 ? st.ctr_energy : role == 2 ? st.vm_energy : st.pod_energy, agg_row(role, a_s), c_aE);
           c_atotal = role == 1 ? st.ctr_cpu_total[a_s] : role == 3 ? st.pod_cpu_total[a_s] : 0.0;
         }
         lds_barrier();
@@ -1825,7 +1830,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     a_total[h] = 0.0;
     a_delta[h] = 0.0;
     if (a_ok) {
-      load_row<Z>(energy_of(role), a_s, a_prev[h]);
+      load_row<Z>(energy_of(role), agg_row(role, a_s), a_prev[h]);
       if (role != 2 && !(a_w[h] & KACC_SLOT_NEW)) a_total[h] = cpu_total_of(role)[a_s];
     } else {
 #pragma unroll
@@ -2416,7 +2421,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     uint64_t a_prev[Z];
     double a_total = 0.0;
     if (a_ok) {
-      load_row<Z>(energy_of(a_role), a_s, a_prev);
+      load_row<Z>(energy_of(a_role), agg_row(a_role, a_s), a_prev);
       if (a_role != 2 && !(a_w & KACC_SLOT_NEW))
         a_total = (a_role == 1 ? st.ctr_cpu_total : st.pod_cpu_total)[a_s];
     } else {
@@ -2572,7 +2577,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         continue;
       }
       uint64_t pv[Z];
-      load_row<Z>(energy_of(role), s, pv);
+      load_row<Z>(energy_of(role), agg_row(role, s), pv);
       double total = (role == 1 && !(wd & KACC_SLOT_NEW)) ? st.ctr_cpu_total[s] : 0.0;
       const double delta = segment(role, beg, end, wd, true, total);
       agg_out(role, wd, delta, pv);
@@ -2611,7 +2616,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     const uint32_t w = b.pod_slot[q];
     const uint64_t sl = w & KACC_SLOT_MASK;  // < pod_slots (checked before deferral)
     uint64_t prev[Z];
-    load_row<Z>(st.pod_energy, sl, prev);
+    load_row<Z>(st.pod_energy, pod_row(sl), prev);
     double total = (w & KACC_SLOT_NEW) ? 0.0 : st.pod_cpu_total[sl];
     double delta = 0.0;
     for (uint32_t c = beg; c < end; ++c) {
@@ -2641,8 +2646,8 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     uint64_t E[Z];
     double P[Z];
     attribute_row<Z>(a, a.live_pod, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
-    store_row<Z, kNT, uint64_t>(st.pod_energy, sl, E);
-    store_row<Z, kNT, double>(st.pod_power, sl, P);
+    store_row<Z, kNT, uint64_t>(st.pod_energy, pod_row(sl), E);
+    store_row<Z, kNT, double>(st.pod_power, pod_row(sl), P);
     export_pod<Z>(b, q, E, P);
   }
 }
@@ -2652,10 +2657,10 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
 // kNsUnroll at a time, adds in order), then the 16 lane sums are halved
 // pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
 // f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
-// kW: 8-byte words between consecutive rows — Z for the state tables (rows =
-// pod slots, energy and power tables apart), 2Z for an interval's pod export
-// (rows = batch pod rows, energy then power bits in one record).
-template <int Z, int kW = Z>
+// kW: 8-byte words between consecutive rows — 2Z both for the state tables
+// (rows = pod slots: one [energy Z | power Z] record per slot, pod_row) and for
+// an interval's pod export (rows = batch pod rows, the same record).
+template <int Z, int kW = 2 * Z>
 __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
                                                 const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
                                                 const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
@@ -2682,14 +2687,6 @@ __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, con
 #pragma unroll
     for (int u = 0; u < kNsUnroll; ++u) {
       uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
-#if KACC_NS_PROBE_PAIRED
-      if (kW == Z) {  // probe: record at / 2 of a [pod_slots / 2][2Z] view of the energy table
-        at = min(at >> 1, (pod_slots >> 1) - 1);
-        load_row<Z>(pe + at * 2 * Z, 0, er[u]);
-        load_row_f64<Z>(reinterpret_cast<const double *>(pe) + at * 2 * Z + Z, 0, pr[u]);
-        continue;
-      }
-#endif
       load_row<Z>(pe + at * kW, 0, er[u]);
       load_row_f64<Z>(pp + at * kW, 0, pr[u]);
     }
@@ -2749,7 +2746,7 @@ struct NodeTotalsArgs {
   double *out_p;
 };
 
-template <int Z, int kW = Z>
+template <int Z, int kW = 2 * Z>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
                                                                   const uint32_t *__restrict__ slots,
@@ -2860,6 +2857,21 @@ __global__ __launch_bounds__(kBlock) void proc_power_kernel(const ProcDerive d, 
   }
 }
 
+// Elements [first, first + count) of a pod table (logical [slot*Z + z]) to / from
+// a dense array: base is the table's first element inside the [Sq][2Z] records.
+__global__ __launch_bounds__(kBlock) void pod_pair_copy_kernel(uint64_t *base, uint32_t Z, uint64_t first,
+                                                               uint64_t count, uint64_t *dense, int to_table) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < count;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint64_t e = first + i;
+    uint64_t *p = base + (e / Z) * (2ull * Z) + e % Z;
+    if (to_table)
+      *p = dense[i];
+    else
+      dense[i] = *p;
+  }
+}
+
 }  // namespace kacc
 
 // =============================================================================
@@ -2915,6 +2927,16 @@ int kacc_fail(kacc_ctx *ctx, int code, const char *fmt, ...) {
 namespace {
 
 #define fail kacc_fail
+
+// KACC_T_POD_ENERGY's allocation holds the pod records [Sq][2Z] (energy Z words,
+// then power Z words: kacc_table_row_stride 2Z); KACC_T_POD_POWER points Z words in.
+bool pod_paired(int t) { return t == KACC_T_POD_ENERGY || t == KACC_T_POD_POWER; }
+
+uint64_t table_count(const kacc_config &c, int t);
+size_t table_alloc_bytes(const kacc_ctx *ctx, int t) {
+  const size_t n = std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem;
+  return t == KACC_T_POD_ENERGY ? 2 * n : n;
+}
 
 uint64_t table_count(const kacc_config &c, int t) {
   const TableDesc &d = kTables[t];
@@ -2984,21 +3006,21 @@ template <int Z>
 void launch_small(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   const uint32_t grid = (b.n_nodes + kacc::kSmallWaves - 1) / kacc::kSmallWaves;
   if (!kacc::kTransposed<Z> && b.node_proc_span)  // Z without the transposed paths: row-wise slot sweep
-    hipLaunchKernelGGL((kacc::small_kernel<Z, true>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
+    KACC_LAUNCH((kacc::small_kernel<Z, true>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
   else
-    hipLaunchKernelGGL((kacc::small_kernel<Z, false>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
+    KACC_LAUNCH((kacc::small_kernel<Z, false>), dim3(grid), dim3(64 * kacc::kSmallWaves), 0, st, b, s);
 }
 
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   if (V == 0 && (b.flags & KACC_F_SMALL_NODES)) return launch_small<Z>(b, s, st);
-  hipLaunchKernelGGL((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
+  KACC_LAUNCH((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
                      s);
   if (b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES)) return;
   const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
-  hipLaunchKernelGGL((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
+  KACC_LAUNCH((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
                      b, s);
-  hipLaunchKernelGGL((kacc::pod_kernel<Z, V>), dim3(kacc::kPodGrid), dim3(kacc::kBlock), 0, st, b, s);
+  KACC_LAUNCH((kacc::pod_kernel<Z, V>), dim3(kacc::kPodGrid), dim3(kacc::kBlock), 0, st, b, s);
 }
 
 void launch(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
@@ -3061,11 +3083,11 @@ void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t 
   const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
   const uint32_t ns_blocks = (n_ns + per_block - 1) / per_block;
   if (pod_export)
-    hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z, 2 * Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0,
+    KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0,
                        st, ns_blocks, n_ns, off, slots, pod_export, reinterpret_cast<const double *>(pod_export + Z),
                        n_pods, out_e, out_p, ctx->d_err, na);
-  else
-    hipLaunchKernelGGL((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
+  else  // the pod tables: one [energy | power] record per slot, like an export row
+    KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
                        ns_blocks, n_ns, off, slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
                        (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p, ctx->d_err,
                        na);
@@ -3265,14 +3287,14 @@ void launch_carry(uint32_t Z, bool medium, const kacc_interval *d_b, uint32_t K,
                   const kacc::DevState &s, hipStream_t st) {
   if (medium) {
     if (Z == 1)
-      hipLaunchKernelGGL((kacc::intervals_carry_kernel<1, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
+      KACC_LAUNCH((kacc::intervals_carry_kernel<1, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
     else
-      hipLaunchKernelGGL((kacc::intervals_carry_kernel<2, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
+      KACC_LAUNCH((kacc::intervals_carry_kernel<2, V, 256>), dim3(n_nodes), dim3(256), 0, st, d_b, K, s);
   } else {
     if (Z == 1)
-      hipLaunchKernelGGL((kacc::intervals_carry_kernel<1, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
+      KACC_LAUNCH((kacc::intervals_carry_kernel<1, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
     else
-      hipLaunchKernelGGL((kacc::intervals_carry_kernel<2, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
+      KACC_LAUNCH((kacc::intervals_carry_kernel<2, V, 512>), dim3(n_nodes), dim3(512), 0, st, d_b, K, s);
   }
 }
 
@@ -3345,13 +3367,14 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
   }
   for (int t = 0; t < KACC_T_COUNT; ++t) {
     ctx->counts[t] = table_count(ctx->cfg, t);
-    if (kTables[t].derived) continue;  // computed on read
-    const size_t bytes = std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem;
+    if (kTables[t].derived || t == KACC_T_POD_POWER) continue;  // computed on read / inside the pod records
+    const size_t bytes = table_alloc_bytes(ctx, t);
     if ((e = hipMalloc(&ctx->tables[t], bytes)) != hipSuccess) {
       fail(ctx, KACC_ENOMEM, "hipMalloc table %d (%zu B): %s", t, bytes, hipGetErrorString(e));
       return bail(KACC_ENOMEM);
     }
   }
+  ctx->tables[KACC_T_POD_POWER] = static_cast<char *>(ctx->tables[KACC_T_POD_ENERGY]) + 8ull * ctx->cfg.zones;
   if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
       (e = hipMalloc(&ctx->d_ctr, 16)) != hipSuccess) {
     fail(ctx, KACC_ENOMEM, "hipMalloc work words: %s", hipGetErrorString(e));
@@ -3368,7 +3391,7 @@ void kacc_destroy(kacc_ctx *ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (int t = 0; t < KACC_T_COUNT; ++t)
-    if (ctx->tables[t]) (void)hipFree(ctx->tables[t]);
+    if (ctx->tables[t] && t != KACC_T_POD_POWER) (void)hipFree(ctx->tables[t]);  // pod power: inside the records
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
   if (ctx->d_items) (void)hipFree(ctx->d_items);
@@ -3398,9 +3421,8 @@ int kacc_reset(kacc_ctx *ctx) {
   if (!ctx) return KACC_EINVAL;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   for (int t = 0; t < KACC_T_COUNT; ++t)
-    if (!kTables[t].derived)
-      KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0, std::max<uint64_t>(ctx->counts[t], 1) * kTables[t].elem,
-                                   ctx->stream));
+    if (!kTables[t].derived && t != KACC_T_POD_POWER)
+      KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0, table_alloc_bytes(ctx, t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -3408,8 +3430,16 @@ int kacc_reset(kacc_ctx *ctx) {
   return KACC_OK;
 }
 
+int kacc_time_next_launch(kacc_ctx *ctx, void *start_event, void *stop_event) {
+  if (!ctx) return KACC_EINVAL;
+  ctx->time_start = static_cast<hipEvent_t>(start_event);
+  ctx->time_stop = static_cast<hipEvent_t>(stop_event);
+  return KACC_OK;
+}
+
 int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   if (!ctx) return KACC_EINVAL;
+  const kacc::TimingScope timing(ctx);
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK || b->n_nodes == 0) return rc;
@@ -3428,6 +3458,7 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
 // round trip between intervals).  Every shape is checked before any launch.
 int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t count, void *stream) {
   if (!ctx) return KACC_EINVAL;
+  const kacc::TimingScope timing(ctx);
   if (count && !dev_batches) return fail(ctx, KACC_EINVAL, "dev_batches is NULL");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   uint64_t max_nodes = 0, max_procs = 0, max_pods = 0;
@@ -3471,7 +3502,7 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
                  a.pod_ctr_end == b.pod_ctr_end && !(b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES));
   }
   if (one_layout && dev_batches[0].n_nodes && !(dev_batches[0].flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES))) {
-    hipLaunchKernelGGL((kacc::items_kernel<0>), dim3(dev_batches[0].n_nodes), dim3(kacc::kTpb<0>), 0, st,
+    KACC_LAUNCH((kacc::items_kernel<0>), dim3(dev_batches[0].n_nodes), dim3(kacc::kTpb<0>), 0, st,
                        dev_batches[0], ds);
     kacc::DevState dk = ds;
     dk.items_given = 1;
@@ -3791,6 +3822,13 @@ int kacc_table_device_ptr(kacc_ctx *ctx, kacc_table t, void **dev_ptr) {
   return KACC_OK;
 }
 
+int kacc_table_row_stride(const kacc_ctx *ctx, kacc_table t, uint64_t *stride) {
+  if (!ctx || t < 0 || t >= KACC_T_COUNT || !stride) return KACC_EINVAL;
+  const uint64_t w = kTables[t].zoned ? ctx->cfg.zones : 1;
+  *stride = pod_paired(t) ? 2 * w : w;
+  return KACC_OK;
+}
+
 static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host,
                       bool down) {
   if (!ctx || t < 0 || t >= KACC_T_COUNT || (!host && count)) return KACC_EINVAL;
@@ -3803,15 +3841,23 @@ static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   if (!count) return KACC_OK;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (kTables[t].derived) {  // a derived power table: derived into a scratch buffer, then copied
-    double *tmp = nullptr;
-    KACC_HIP(ctx, hipMalloc(&tmp, count * sizeof(double)));
-    int rc = kacc_internal_derived_power(ctx, t, first, count, tmp, ctx->stream);
-    hipError_t e = rc == KACC_OK ? hipStreamSynchronize(ctx->stream) : hipSuccess;
-    if (rc == KACC_OK && e == hipSuccess) e = hipMemcpy(host, tmp, count * sizeof(double), hipMemcpyDeviceToHost);
+  if (kTables[t].derived || pod_paired(t)) {  // derived / inside the pod records: through a dense scratch range
+    void *tmp = nullptr;
+    KACC_HIP(ctx, hipMalloc(&tmp, count * 8));
+    hipError_t e = hipSuccess;
+    int rc = KACC_OK;
+    if (down) {
+      rc = kacc_internal_dense_range(ctx, t, first, count, tmp, ctx->stream);
+      e = rc == KACC_OK ? hipStreamSynchronize(ctx->stream) : hipSuccess;
+      if (rc == KACC_OK && e == hipSuccess) e = hipMemcpy(host, tmp, count * 8, hipMemcpyDeviceToHost);
+    } else {
+      e = hipMemcpy(tmp, host, count * 8, hipMemcpyHostToDevice);
+      if (e == hipSuccess) rc = kacc_internal_pod_scatter(ctx, t, first, count, tmp, ctx->stream);
+      if (rc == KACC_OK && e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    }
     (void)hipFree(tmp);
     if (rc != KACC_OK) return rc;
-    if (e != hipSuccess) return fail(ctx, KACC_EHIP, "derived table %d: %s", (int)t, hipGetErrorString(e));
+    if (e != hipSuccess) return fail(ctx, KACC_EHIP, "table %d: %s", (int)t, hipGetErrorString(e));
     return KACC_OK;
   }
   char *dev = static_cast<char *>(ctx->tables[t]) + first * kTables[t].elem;
@@ -3866,6 +3912,7 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
                                   uint64_t n_nodes, uint64_t *out_energy, double *out_power, uint64_t *node_energy,
                                   double *node_power, void *stream) {
   if (!ctx) return KACC_EINVAL;
+  const kacc::TimingScope timing(ctx);
   if (n_ns && (!off || !rows || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -3935,6 +3982,40 @@ int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t c
   (void)hipGetLastError();
   hipLaunchKernelGGL(kacc::proc_power_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
                      dim3(kacc::kBlock), 0, st, kacc_derive(ctx, static_cast<kacc_kind>(kind)), first, count, out);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_internal_dense_range(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, void *out, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (kacc_derived_kind(t) >= 0) return kacc_internal_derived_power(ctx, t, first, count, static_cast<double *>(out), stream);
+  if (!count) return KACC_OK;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (!pod_paired(t)) {
+    KACC_HIP(ctx, hipMemcpyAsync(out, static_cast<const char *>(ctx->tables[t]) + first * 8, count * 8,
+                                 hipMemcpyDeviceToDevice, st));
+    return KACC_OK;
+  }
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  const uint64_t blocks = (count + kacc::kBlock - 1) / kacc::kBlock;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(kacc::pod_pair_copy_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
+                     dim3(kacc::kBlock), 0, st, static_cast<uint64_t *>(ctx->tables[t]), ctx->cfg.zones, first, count,
+                     static_cast<uint64_t *>(out), 0);
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_internal_pod_scatter(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, const void *in, void *stream) {
+  if (!ctx || !pod_paired(t)) return KACC_EINVAL;
+  if (!count) return KACC_OK;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const uint64_t blocks = (count + kacc::kBlock - 1) / kacc::kBlock;
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(kacc::pod_pair_copy_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
+                     dim3(kacc::kBlock), 0, st, static_cast<uint64_t *>(ctx->tables[t]), ctx->cfg.zones, first, count,
+                     const_cast<uint64_t *>(static_cast<const uint64_t *>(in)), 1);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }

@@ -781,10 +781,12 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   kacc::fmt::Args a{};
   a.src = static_cast<const char *>(ctx->tables[t]) + first * 8;
-  double *derived = nullptr;  // a derived power table: the range derived first (kacc_derive.hpp)
-  if (kacc_derived_kind(t) >= 0) {
+  // a derived power table (kacc_derive.hpp) or a pod table (inside the pod records):
+  // the range made dense first
+  double *derived = nullptr;
+  if (kacc_derived_kind(t) >= 0 || t == KACC_T_POD_ENERGY || t == KACC_T_POD_POWER) {
     KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&derived), count * 8, st));
-    const int rc = kacc_internal_derived_power(ctx, t, first, count, derived, st);
+    const int rc = kacc_internal_dense_range(ctx, t, first, count, derived, st);
     if (rc != KACC_OK) {
       (void)hipFreeAsync(derived, st);
       return rc;
@@ -871,7 +873,7 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   // every sub-buffer 256-B aligned (the scan's look-back state needs aligned storage)
   auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
   const uint64_t off_len = 1024, off_scan = al(off_len + 8 * (lines + 1));
-  const bool derived = kacc_derived_kind(t) >= 0;
+  const bool derived = kacc_derived_kind(t) >= 0 || t == KACC_T_POD_ENERGY || t == KACC_T_POD_POWER;
   const uint64_t off_derived = al(off_scan + scan_bytes);
   KACC_HIP(ctx, hipMallocAsync(reinterpret_cast<void **>(&tmp), derived ? off_derived + 8 * count * Z : off_scan + scan_bytes,
                                st));
@@ -885,8 +887,7 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   if (derived) {
     a.src = tmp + off_derived;
     a.src_first = first * Z;
-    if ((rc = kacc_internal_derived_power(ctx, t, first * Z, count * Z, reinterpret_cast<double *>(tmp + off_derived), st)) !=
-        KACC_OK)
+    if ((rc = kacc_internal_dense_range(ctx, t, first * Z, count * Z, tmp + off_derived, st)) != KACC_OK)
       return done(rc);
   }
   if (hipMemcpyAsync(tmp, consts.data(), consts.size(), hipMemcpyHostToDevice, st) != hipSuccess)

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <string>
 #include <utility>
@@ -35,6 +36,7 @@ struct kacc_ctx {
   uint32_t batch_cap = 0;
   hipEvent_t batch_copied = nullptr;
   uint32_t live_nodes = 0;  // n_nodes of the last interval run: the nodes the cluster totals sum
+  hipEvent_t time_start = nullptr, time_stop = nullptr;  // kacc_time_next_launch (one call)
   std::string err;
 };
 
@@ -50,6 +52,63 @@ struct kacc_batch {
   uint32_t *h_err = nullptr;    // pinned: device error word after the last submit
   bool submitted = false;
 };
+
+// Elements [first, first + count) of table t as a dense array (device, async on
+// `stream`): derived power tables are derived, the pod tables (stored as [Sq][2Z]
+// energy | power records) gathered, the others copied; and the inverse scatter
+// into a pod table (kacc_engine.hip).
+extern "C" int kacc_internal_dense_range(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, void *out,
+                                         void *stream);
+extern "C" int kacc_internal_pod_scatter(kacc_ctx *ctx, int t, uint64_t first, uint64_t count, const void *in,
+                                         void *stream);
+
+// kacc_time_next_launch: while a LaunchTiming scope is alive on this thread,
+// KACC_LAUNCH attaches the scope's start event to the first kernel it launches
+// and its stop event to every one (the last recording wins), through the
+// dispatch packets (hipExtLaunchKernelGGL); otherwise a plain launch.
+namespace kacc {
+struct LaunchTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+inline LaunchTiming *&launch_timing() {
+  static thread_local LaunchTiming *t = nullptr;
+  return t;
+}
+// Takes the context's pending events for the duration of one entry point.
+class TimingScope {
+ public:
+  explicit TimingScope(kacc_ctx *ctx) {
+    if (ctx && (ctx->time_start || ctx->time_stop)) {
+      t_.start = ctx->time_start;
+      t_.stop = ctx->time_stop;
+      ctx->time_start = ctx->time_stop = nullptr;
+      launch_timing() = &t_;
+      on_ = true;
+    }
+  }
+  ~TimingScope() {
+    if (on_) launch_timing() = nullptr;
+  }
+  TimingScope(const TimingScope &) = delete;
+  TimingScope &operator=(const TimingScope &) = delete;
+
+ private:
+  LaunchTiming t_;
+  bool on_ = false;
+};
+}  // namespace kacc
+
+#define KACC_LAUNCH(kernel, grid, block, shmem, stream, ...)                                             \
+  do {                                                                                                    \
+    kacc::LaunchTiming *kacc_lt_ = kacc::launch_timing();                                                 \
+    if (kacc_lt_) {                                                                                       \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, kacc_lt_->start, kacc_lt_->stop, 0,       \
+                            __VA_ARGS__);                                                                 \
+      kacc_lt_->start = nullptr;                                                                          \
+    } else {                                                                                              \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                                \
+    }                                                                                                     \
+  } while (0)
 
 // Slot map of one workload kind (kacc_join.hip).
 struct kacc_slotmap {

@@ -234,12 +234,13 @@ constexpr int kThreads = 256;
 
 // out[dest ? dest[i] : i] = the tables' row of slot word w[i] (energy, power per zone).
 // Processes / containers / VMs (tp NULL): power derived from the slot's ratio and
-// its node's tables (kacc_derive.hpp).
+// its node's tables (kacc_derive.hpp).  Pods (tp given): te / tp point into the
+// pod records, a slot's row `stride` = 2Z words after the previous one's.
 template <int Z>
 __global__ __launch_bounds__(kThreads) void unpack_kernel(uint32_t n, const uint32_t *w, const uint32_t *dest,
                                                           uint64_t cap, const uint64_t *te, const double *tp,
-                                                          const ProcDerive pd, uint64_t *oe, double *op,
-                                                          uint32_t *err) {
+                                                          uint32_t stride, const ProcDerive pd, uint64_t *oe,
+                                                          double *op, uint32_t *err) {
   const uint32_t i = blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint64_t s = w[i] & KACC_SLOT_MASK;
@@ -250,8 +251,8 @@ __global__ __launch_bounds__(kThreads) void unpack_kernel(uint32_t n, const uint
   }
 #pragma unroll
   for (int z = 0; z < Z; ++z) {
-    oe[o + z] = te[s * Z + z];
-    op[o + z] = tp ? tp[s * Z + z] : proc_power(pd, s, z);
+    oe[o + z] = te[s * stride + z];
+    op[o + z] = tp ? tp[s * stride + z] : proc_power(pd, s, z);
   }
 }
 
@@ -354,7 +355,8 @@ int kacc_unpack(kacc_ctx *ctx, kacc_kind kind, uint32_t n, const uint32_t *slot_
   (void)hipGetLastError();
 #define KACC_UNPACK(Z)                                                                                          \
   hipLaunchKernelGGL((kacc::unpack::unpack_kernel<Z>), dim3(grid), dim3(kacc::unpack::kThreads), 0, st, n,   \
-                     slot_words, dest, cap, e, p, pd, out_energy, out_power, ctx->d_err)
+                     slot_words, dest, cap, e, p, kind == KACC_KIND_POD ? 2 * Z : Z, pd, out_energy, out_power,   \
+                     ctx->d_err)
   switch (ctx->cfg.zones) {
     case 1: KACC_UNPACK(1); break;
     case 2: KACC_UNPACK(2); break;

@@ -49,6 +49,7 @@ struct Args {
   uint64_t min_e;
   int64_t max_size;
   uint32_t Z, z0, cap, n_nodes;
+  uint32_t tab_stride;  // words between two slots' rows: Z (2Z for pods: energy | power records)
   const uint32_t *slot_off;
   const uint64_t *term_key;
   const uint32_t *term_slot;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       if (i < m0) {
         slot[u] = a.term_slot[b0 + c0 + i];
         key[u] = a.term_key[b0 + c0 + i];
-        e[u] = a.tab_e[static_cast<uint64_t>(slot[u]) * Z + z0];
+        e[u] = a.tab_e[static_cast<uint64_t>(slot[u]) * a.tab_stride + z0];
         pass[u] = e[u] >= a.min_e && !(full && e[u] <= min_full);  // :102, :124
       }
     }
@@ -234,8 +235,8 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       const uint64_t sl = s_slot[src];
       a.set_key[base + r] = s_key[src];
       for (uint32_t z = 0; z < Z; ++z) {
-        a.set_e[(base + r) * Z + z] = a.tab_e[sl * Z + z];
-        a.set_p[(base + r) * Z + z] = a.tab_p ? a.tab_p[sl * Z + z] : proc_power(a.pd, sl, z);
+        a.set_e[(base + r) * Z + z] = a.tab_e[sl * a.tab_stride + z];
+        a.set_p[(base + r) * Z + z] = a.tab_p ? a.tab_p[sl * a.tab_stride + z] : proc_power(a.pd, sl, z);
       }
     }
     size = new_size;
@@ -305,6 +306,7 @@ kacc::trk::Args tracker_args(const kacc_tracker *t) {
   a.min_e = t->min_e;
   a.max_size = t->max_size;
   a.Z = t->Z;
+  a.tab_stride = t->kind == KACC_KIND_POD ? 2 * t->Z : t->Z;
   a.z0 = t->zone;
   a.cap = t->cap;
   a.n_nodes = t->nodes;
