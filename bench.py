@@ -98,6 +98,9 @@ def parse():
                          "totals_compute_ms; inline = those launch events inside the timed region; markers = "
                          "hipEventRecord markers around them inside the timed region (round 2).  Every event "
                          "packet costs a stream gap: ~9 us per step, profiles/r03/events")
+    ap.add_argument("--slot-nodes", choices=["stable", "write"], default="stable",
+                    help="stable: KACC_F_STABLE_SLOT_NODES (a process slot keeps its node; only NEW rows store "
+                         "it); write: every row stores its node (ablation)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -265,7 +268,7 @@ def slot_layout_lines(args, frag, K, steps, bytes_per_interval, steady_intervals
 
     sim = fleet.FleetSim(layout, seed=fleet.SEED)
     statics = to_device(layout.static_arrays())
-    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES | accel.KACC_F_STABLE_SLOT_NODES
     prime = sim.next_interval()
     prime["proc_slot"] = pristine
     tp = dict(statics)
@@ -371,7 +374,8 @@ def pipeline_line(args, steps=10, warm=8):
                             if n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max")}))
         t["proc_slot"] = d_slot  # the join writes the batch's slot words in place
         t["node_proc_span"] = span
-        ivs.append((interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES), t))
+        ivs.append((interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+                                          | accel.KACC_F_STABLE_SLOT_NODES), t))
     tj, tt, ti, tall = [], [], [], []
     for k in range(warm + steps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -474,7 +478,9 @@ class Workload:
                 t["pod_export"], t["node_export"] = self.pex[st % 2], self.nex[st % 2]
         # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
         # runs K > 1 fast-node intervals as one launch
-        self.flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+        # (KACC_F_STABLE_SLOT_NODES: a slot stays with its node; only NEW rows write their node)
+        self.flags = (layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+                      | (accel.KACC_F_STABLE_SLOT_NODES if args.slot_nodes == "stable" else 0))
         self.ivs = [interval_from_tensors(t, sizes, self.flags) for t in self.iv_tensors]
         self.iv_arrays = [(accel.KaccInterval * K)(*self.ivs[k * K:(k + 1) * K]) for k in range(n_steps)]
         ns_off, ns_slot = layout.namespace_csr()
@@ -669,7 +675,7 @@ def main():
     # once and carries it on chip, so its algorithmic bytes are fewer (kacc_intervals_bytes)
     fused = accel.fused_intervals(w.flags, K, args.node_order, Z)
     bytes_per_launch = accel.intervals_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"], sizes["n_vms"],
-                                             sizes["n_pods"], K, fused) / K
+                                             sizes["n_pods"], K, fused, w.flags) / K
     k_avg_ms = float(np.mean(kernel_ms))
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
 
@@ -739,7 +745,7 @@ def main():
             "traffic_source": traffic_source,
             "bytes_per_interval": bytes_per_launch,
             "bytes_per_interval_unfused": accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
-                                                               sizes["n_vms"], sizes["n_pods"]),
+                                                               sizes["n_vms"], sizes["n_pods"], w.flags),
             "kernel": kernel_name(w.flags, K, fused, Z),
             "same_box_copy_GBps": copy_gbps,
             "frac_of_copy": achieved / copy_gbps,

@@ -115,6 +115,18 @@ extern "C" {
                                      not fit is not computed and raises
                                      KACC_ERANGE (bit 32).  kacc_batch_submit
                                      sets it by itself.                      */
+#define KACC_F_STABLE_SLOT_NODES 0x40u /* caller guarantees that a process
+                                          slot's node never changes while this
+                                          context lives, except through a row
+                                          whose slot word carries KACC_SLOT_NEW
+                                          (a slot stays in one node's range:
+                                          kacc_slot_join's fixed per-node
+                                          ranges).  KACC_T_PROC_NODE then already
+                                          holds the node of every other row, so
+                                          the interval writes it only for NEW
+                                          rows and on a node's first read: 4 B
+                                          per process row less HBM traffic.
+                                          Results are bit-identical.           */
 #define KACC_FAST_MAX_PROCS 2048u
 #define KACC_FAST_MAX_AGGREGATES 512u
 #define KACC_SMALL_MAX_PROCS 512u
@@ -698,11 +710,13 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
  * which reads the engine state a node / row / aggregate needs once and carries
  * it on chip while the slots stay put) that minus K-1 state reads.          */
 uint64_t kacc_intervals_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,
-                              uint64_t n_vms, uint64_t n_pods, uint32_t intervals, int carried);
+                              uint64_t n_vms, uint64_t n_pods, uint32_t intervals, int carried, uint32_t flags);
 /* Algorithmic HBM bytes one kacc_run_interval moves for a batch of these
- * sizes (the roofline numerator).                  */
+ * sizes and flags (the roofline numerator): with
+ * KACC_F_STABLE_SLOT_NODES a process row does not write its node (4 B; the
+ * few NEW rows of an interval that do are not counted).                      */
 uint64_t kacc_interval_bytes(uint32_t zones, uint64_t n_nodes, uint64_t n_procs, uint64_t n_ctrs,
-                             uint64_t n_vms, uint64_t n_pods);
+                             uint64_t n_vms, uint64_t n_pods, uint32_t flags);
 
 #ifdef __cplusplus
 }

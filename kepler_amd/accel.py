@@ -47,6 +47,7 @@ KACC_F_NODE_SLOT_RANGES = 0x10
 KACC_SMALL_MAX_PROCS = 512
 KACC_SMALL_MAX_AGGREGATES = 128
 KACC_F_MEDIUM_NODES = 0x20
+KACC_F_STABLE_SLOT_NODES = 0x40  # a slot never changes node except through a NEW row (slot join ranges)
 KACC_MEDIUM_MAX_PROCS = 1024
 KACC_MEDIUM_MAX_AGGREGATES = 256
 KACC_UNIQUE_ID_BYTES = 128
@@ -315,9 +316,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_namespace_totals.argtypes = [
         c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     ]
-    lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64]
+    lib.kacc_interval_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32]
     lib.kacc_interval_bytes.restype = c_uint64
-    lib.kacc_intervals_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_int]
+    lib.kacc_intervals_bytes.argtypes = [c_uint32, c_uint64, c_uint64, c_uint64, c_uint64, c_uint64, c_uint32, c_int,
+                                         c_uint32]
     lib.kacc_intervals_bytes.restype = c_uint64
     lib.kacc_debug_run_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_void_p, c_int]
     lib.kacc_debug_run_intervals_variant.argtypes = [c_void_p, POINTER(KaccInterval), c_uint32, c_void_p, c_int]
@@ -399,13 +401,14 @@ def pack(rec_off, pid, cpu_delta, ptype, ctr_key, vm_key, pod_key=None, pod_ns=N
     return res
 
 
-def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int) -> int:
-    return int(load().kacc_interval_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods))
+def interval_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int, flags: int = 0) -> int:
+    return int(load().kacc_interval_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods, flags))
 
 
 def intervals_bytes(zones: int, n_nodes: int, n_procs: int, n_ctrs: int, n_vms: int, n_pods: int, intervals: int,
-                    carried: bool) -> int:
-    return int(load().kacc_intervals_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods, intervals, int(carried)))
+                    carried: bool, flags: int = 0) -> int:
+    return int(load().kacc_intervals_bytes(zones, n_nodes, n_procs, n_ctrs, n_vms, n_pods, intervals, int(carried),
+                                           flags))
 
 
 KACC_CARRY_MAX_ZONES = 2

@@ -265,14 +265,19 @@ struct Attr {
   uint32_t live_pod;  // pod.go:96 guards on Power instead of ActivePower
   double nd;       // ProcessTotalCPUTimeDelta
   uint32_t first;  // first*Read variant: EnergyTotal = interval energy, Power 0
+  // KACC_F_STABLE_SLOT_NODES on a node past its first read: a row's slot already
+  // holds this node in KACC_T_PROC_NODE unless the row is NEW, so only NEW rows
+  // store it (4 B per process row less HBM traffic)
+  uint32_t keep_node;
 };
 
 // Attr from the node phase's LDS results (block-uniform -> SGPRs).
 template <int Z>
-__device__ __forceinline__ Attr<Z> make_attr(const NodeShared &sh) {
+__device__ __forceinline__ Attr<Z> make_attr(const NodeShared &sh, uint32_t flags) {
   Attr<Z> a;
   a.nd = uniform_f64(sh.node_delta);
   a.first = uniform_u32(sh.first);
+  a.keep_node = (flags & KACC_F_STABLE_SLOT_NODES) && !a.first ? 1u : 0u;
   a.live = 0;
   a.live_pod = 0;
 #pragma unroll
@@ -332,14 +337,14 @@ __device__ __forceinline__ double attribute_proc(const Attr<Z> &a, double delta,
 // A process row's outputs at slot s: energy totals, ratio and node.
 template <int Z, bool NT>
 __device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const uint64_t (&E)[Z], double ratio,
-                                           uint32_t node) {
+                                           uint32_t node, bool wnode) {
   store_row<Z, NT, uint64_t>(st.proc_energy, s, E);
   if constexpr (NT) {
     __builtin_nontemporal_store(ratio, st.proc_ratio + s);
-    __builtin_nontemporal_store(node, st.proc_node + s);
+    if (wnode) __builtin_nontemporal_store(node, st.proc_node + s);
   } else {
     st.proc_ratio[s] = ratio;
-    st.proc_node[s] = node;
+    if (wnode) st.proc_node[s] = node;
   }
 }
 
@@ -520,12 +525,13 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
     else
       pe[piece] = ev;
     if (zp == 0) {  // the slot's ratio and node: contiguous across the group's lanes
+      const bool wnode = !a.keep_node || is_new;
       if constexpr (NT) {
         __builtin_nontemporal_store(ratio, ratio_tab + s0 + idx);
-        __builtin_nontemporal_store(node, node_tab + s0 + idx);
+        if (wnode) __builtin_nontemporal_store(node, node_tab + s0 + idx);
       } else {
         ratio_tab[s0 + idx] = ratio;
-        node_tab[s0 + idx] = node;
+        if (wnode) node_tab[s0 + idx] = node;
       }
     }
   }
@@ -946,7 +952,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   }
 
   // ---- E: attribution ------------------------------------------------------------
-  const Attr<Z> a = make_attr<Z>(sh);
+  const Attr<Z> a = make_attr<Z>(sh, b.flags);
   if (tid == 0) {  // node scalars of the new snapshot
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
@@ -979,7 +985,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
         const uint32_t wk = s_w[r];
         uint64_t E[Z];
         const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E);
-        store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n);
+        store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
       }
     }
     if constexpr (kSweepable) {
@@ -1014,7 +1020,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       }
       uint64_t E[Z];
       const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[k], E);
-      store_proc<Z, kNtScat>(st, sl, E, ratio, n);
+      store_proc<Z, kNtScat>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   }
   if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
@@ -1539,7 +1545,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         st.node_idle_power[zi] = z_ip;
         export_node_zone<Z>(b, n, tid, c_atot, c_itot, z_p, z_ap, z_ip);
       }
-      const Attr<Z> a = make_attr<Z>(sh);
+      const Attr<Z> a = make_attr<Z>(sh, b.flags);
       if (tid == 0) {
         st.node_ts[n] = ts;
         st.node_has_prev[n] = 1u;
@@ -1585,7 +1591,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           for (int z = 0; z < Z; ++z) pv[z] = s_cE[pos * Z + z];
           const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E);
           if constexpr ((V & kCarryNoRowStores) == 0) {
-            store_proc<Z, true>(st, static_cast<uint64_t>(s_lo) + pos, E, ratio, n);
+            store_proc<Z, true>(st, static_cast<uint64_t>(s_lo) + pos, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
           }
 #pragma unroll
           for (int z = 0; z < Z; ++z) s_cE[pos * Z + z] = E[z];
@@ -1610,7 +1616,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         for (int z = 0; z < Z; ++z) pv[z] = s_cE[r * Z + z];
         const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, pv, E);
         if constexpr ((V & kCarryNoRowStores) == 0) {
-          store_proc<Z, kNtScatterStores>(st, sl, E, ratio, n);
+          store_proc<Z, kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
         }
 #pragma unroll
         for (int z = 0; z < Z; ++z) s_cE[r * Z + z] = E[z];
@@ -1954,7 +1960,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   }
 
   // ---- E: attribution ------------------------------------------------------------------
-  const Attr<Z> a = make_attr<Z>(sh);
+  const Attr<Z> a = make_attr<Z>(sh, b.flags);
   if (lane == 0) {
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
@@ -1990,7 +1996,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
           if (e == 0xffffu) continue;
           uint64_t E[Z];
           const double ratio = attribute_proc<Z>(a, s_d[e & 0x7fffu], (e & 0x8000u) != 0, prev[g], E);
-          store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n);
+          store_proc<Z, kNT>(st, static_cast<uint64_t>(smin) + pos, E, ratio, n, !a.keep_node || (e & 0x8000u));
           continue;
         }
       }
@@ -2022,7 +2028,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
       }
       uint64_t E[Z];
       const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[g], E);
-      store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n);
+      store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   };
   attr_batch(0);
@@ -2439,7 +2445,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       }
     }
     __syncthreads();
-    const Attr<Z> a = make_attr<Z>(sh);
+    const Attr<Z> a = make_attr<Z>(sh, b.flags);
 
     auto agg_out = [&](uint32_t role, uint32_t wd, double delta, const uint64_t (&pv)[Z]) {
       const uint64_t s = wd & KACC_SLOT_MASK;
@@ -2553,7 +2559,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         }
         uint64_t E[Z];
         const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E);
-        store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n);
+        store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
       }
     }
     // aggregates beyond one per lane (chunks of mostly empty containers):
@@ -2631,6 +2637,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     Attr<Z> a;
     a.nd = st.node_cpu_delta[n];
     a.first = st.node_status[n] == KACC_NODE_FIRST_READ ? 1u : 0u;
+    a.keep_node = 0;  // pods only
     a.live = 0;
     a.live_pod = 0;
 #pragma unroll
@@ -3137,7 +3144,8 @@ int check_shape(kacc_ctx *ctx, const kacc_interval *b) {
   if ((b->flags & KACC_F_NODE_CPU_DELTA_GIVEN) && !b->node_cpu_delta)
     return fail(ctx, KACC_EINVAL, "KACC_F_NODE_CPU_DELTA_GIVEN without node_cpu_delta");
   if (b->flags & ~(KACC_F_NODE_CPU_DELTA_GIVEN | KACC_F_FAST_NODES | KACC_F_TRUSTED_LAYOUT |
-                   KACC_F_SMALL_NODES | KACC_F_NODE_SLOT_RANGES | KACC_F_MEDIUM_NODES))
+                   KACC_F_SMALL_NODES | KACC_F_NODE_SLOT_RANGES | KACC_F_MEDIUM_NODES |
+                   KACC_F_STABLE_SLOT_NODES))
     return fail(ctx, KACC_EINVAL, "unknown flags 0x%x", b->flags);
   return KACC_OK;
 }
@@ -4021,25 +4029,26 @@ int kacc_internal_pod_scatter(kacc_ctx *ctx, int t, uint64_t first, uint64_t cou
 }
 
 uint64_t kacc_intervals_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V, uint64_t Q, uint32_t K,
-                              int carried) {
+                              int carried, uint32_t flags) {
   // K intervals of these sizes.  Carried (intervals_carry_kernel,
   // steady state): the engine state a node / row / aggregate reads back — zone
   // counters and totals, has_prev / ts, previous workload totals and CPU totals —
   // is read once, then carried on chip.
-  if (!carried) return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q);
+  if (!carried) return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q, flags);
   if (K == 0) return 0;
   const uint64_t state_once = N * (12 + 24ull * Z) + P * 8ull * Z + C * (8 + 8ull * Z) + V * 8ull * Z +
                               Q * (8 + 8ull * Z);
-  return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q) -
+  return static_cast<uint64_t>(K) * kacc_interval_bytes(Z, N, P, C, V, Q, flags) -
          static_cast<uint64_t>(K - 1) * state_once;
 }
 
 uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uint64_t V,
-                             uint64_t Q) {
+                             uint64_t Q, uint32_t flags) {
   // minimal HBM bytes of one interval_kernel launch.
   const uint64_t node = 76 + 96ull * Z;
-  // Δ 8 + slot 4 in, previous totals 8Z in; totals 8Z + ratio 8 + node 4 out
-  const uint64_t proc = 24 + 16ull * Z;
+  // Δ 8 + slot 4 in, previous totals 8Z in; totals 8Z + ratio 8 + node 4 out (the node
+  // only for NEW rows under KACC_F_STABLE_SLOT_NODES: not counted)
+  const uint64_t proc = ((flags & KACC_F_STABLE_SLOT_NODES) ? 20 : 24) + 16ull * Z;
   // container: end 4 + slot 4 + previous CPU total 8 in, Δ 8 + total 8 out; previous
   // energies 8Z in, energies 8Z + ratio 8 + node 4 out (power derived since ABI 3)
   const uint64_t ctr = 44 + 16ull * Z;

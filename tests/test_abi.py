@@ -85,6 +85,11 @@ def test_interval_bytes_formula(lib):
     assert accel.interval_bytes(z, 0, 0, 1, 1, 1) == (44 + 28 + 32) + (16 + 16 + 24) * z
     n, p, c, v, q = 10_000, 20_000_000, 1_975_000, 200_000, 711_000
     assert accel.interval_bytes(z, n, p, c, v, q) == n * 460 + p * 88 + c * 108 + v * 92 + q * 128
+    # KACC_F_STABLE_SLOT_NODES: a process row's node is not rewritten (4 B)
+    stable = accel.KACC_F_STABLE_SLOT_NODES
+    assert accel.interval_bytes(z, 0, 1, 0, 0, 0, stable) == 20 + 16 * z
+    assert accel.interval_bytes(z, n, p, c, v, q, stable) == accel.interval_bytes(z, n, p, c, v, q) - 4 * p
+    assert accel.intervals_bytes(z, n, p, c, v, q, 3, False, stable) == 3 * accel.interval_bytes(z, n, p, c, v, q, stable)
 
 
 def test_create_error_visible_from_another_thread(lib):

@@ -94,3 +94,77 @@ def test_time_next_launch_rides_on_the_dispatch():
     ms = ev[0].elapsed_time(ev[1])
     assert 0.0 < ms < 100.0, ms
     acc.close()
+
+
+@pytest.mark.parametrize("name,kw,shape", [
+    # interval_kernel fast path: transposed 64-row groups and the per-row fallback
+    ("z4-fast", dict(n_nodes=24, procs_per_node=[2000, 1500, 1, 0, 700, 64] * 4, zones=4), "fast"),
+    ("z4-fast-shuffled", dict(n_nodes=12, procs_per_node=[2000, 900, 3, 64] * 3, zones=4, shuffle_slots=True), "fast"),
+    # slot sweep (node_proc_span) over fragmented node ranges
+    ("z4-sweep", dict(n_nodes=12, procs_per_node=[1900, 800, 1, 64] * 3, zones=4, fragment_slots=0.04), "fast"),
+    ("z3-rowsweep", dict(n_nodes=12, procs_per_node=[1900, 800, 1, 64] * 3, zones=3, fragment_slots=0.04), "fast"),
+    # small_kernel (one wavefront per node)
+    ("z2-small", dict(n_nodes=36, procs_per_node=[500, 120, 1, 0, 512, 77] * 6, zones=2), "small"),
+    ("z4-small-sweep", dict(n_nodes=36, procs_per_node=[480, 120, 1, 0, 500, 77] * 6, zones=4, fragment_slots=0.02),
+     "small"),
+    # big nodes: chunk_kernel
+    ("z4-big", dict(n_nodes=6, procs_per_node=[9000, 300, 2049, 0, 5000, 12], zones=4), "generic"),
+    # K intervals in one launch (intervals_carry_kernel)
+    ("z2-carry", dict(n_nodes=24, procs_per_node=[1000, 700, 1, 0, 2048, 513] * 4, zones=2), "carry"),
+    ("z2-carry-sweep", dict(n_nodes=12, procs_per_node=[1000, 700, 64, 3] * 3, zones=2, fragment_slots=0.05), "carry"),
+])
+@pytest.mark.parametrize("stable", [True, False])
+def test_stable_slot_nodes_bit_exact(name, kw, shape, stable):
+    """KACC_F_STABLE_SLOT_NODES: KACC_T_PROC_NODE is written only for NEW rows and on a node's
+    first read; every table (the node ids and the powers derived through them included) stays
+    bit-exact with the oracle, with churn (NEW rows), read errors (incl. skipped first reads)
+    and adversarial inputs, in every kernel shape that stores process rows."""
+    layout = fleet.make_layout(seed=31, **kw)
+    sizes = layout.sizes()
+    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES | (accel.KACC_F_STABLE_SLOT_NODES if stable else 0)
+    if shape == "fast" or shape == "carry":
+        flags &= ~accel.KACC_F_SMALL_NODES
+    if shape == "small":
+        assert flags & accel.KACC_F_SMALL_NODES
+    if shape == "generic":
+        assert not flags & accel.KACC_F_FAST_NODES
+    sim = fleet.FleetSim(layout, seed=31, churn=0.04, read_error_frac=0.1, max_energy=fleet.MAX_ENERGY_FAKE,
+                         adversarial=0.1)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ora = Oracle(layout.zones, **layout.capacities())
+    s = current_stream_handle()
+    K = 9
+    ivs = [sim.next_interval() for _ in range(K)]
+    if kw.get("fragment_slots"):
+        for a in ivs:
+            a["node_proc_span"] = layout.proc_span()
+    dev = [to_device(a) for a in ivs]
+    descs = [interval_from_tensors(t, sizes, flags) for t in dev]
+    if shape == "carry":
+        acc.run_intervals(descs[:2], s)
+        acc.run_intervals(descs[2:], s)
+    else:
+        for d in descs:
+            acc.run_interval(d, s)
+    acc.sync(s)
+    for a in ivs:
+        ora.interval(a, sizes)
+    bad = []
+    # a derived power is defined for the slots rows use (table_check.LiveSlots): a free slot of a
+    # fragmented range derives 0 x its node's ActivePower (NaN when that is +-Inf)
+    used = np.zeros(layout.capacities()["proc_slots"], dtype=bool)
+    used[layout.proc_slot] = True
+    for tname, _ in accel.TABLES:
+        got, want = acc.download(tname), ora.state[tname]
+        if tname == "proc_power":
+            m = np.repeat(used, layout.zones)
+            got, want = got[m], want[m]
+        if not np.array_equal(got, want, equal_nan=want.dtype.kind == "f"):
+            neq = got != want
+            if want.dtype.kind == "f":
+                neq &= ~(np.isnan(got) & np.isnan(want))
+            i = np.flatnonzero(neq)
+            bad.append(f"{tname}: {i.size} differ, first {i[:4].tolist()} got {got[i[:4]].tolist()} "
+                       f"want {want[i[:4]].tolist()}")
+    assert not bad, f"{name} stable={stable}: " + "; ".join(bad)
+    acc.close()

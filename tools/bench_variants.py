@@ -52,12 +52,14 @@ def main():
         span = to_device({"s": layout.proc_span()})["s"]
         for d in dev:
             d["node_proc_span"] = span
-    flag = 0 if os.environ.get("KACC_LIB") else layout.fast_flag()  # older builds reject the flag
+    # the bench's production flags (NO_STABLE=1: without KACC_F_STABLE_SLOT_NODES)
+    flag = 0 if os.environ.get("KACC_LIB") else (layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+                                                 | (0 if os.environ.get("NO_STABLE") else accel.KACC_F_STABLE_SLOT_NODES))
     ivs = [interval_from_tensors(a, layout.sizes(), flag) for a in dev]
     it = ivs[0]
     Z = layout.zones
     sizes = layout.sizes()
-    nbytes = accel.interval_bytes(Z, *[sizes[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")])
+    nbytes = accel.interval_bytes(Z, *[sizes[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")], flag)
     times = {v: [] for v in variants}
     step_t = {v: [] for v in variants}
     off, slots = layout.namespace_csr()

@@ -41,7 +41,10 @@ def main():
     layout = fleet.config_layout(cfg, nodes=40000 if cfg == 1 else None)  # bench.py --config 1 fleet
     s = layout.sizes()
     dims = [s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")]
-    alg = accel.interval_bytes(layout.zones, *dims) if K == 1 else accel.intervals_bytes(layout.zones, *dims, K, True)
+    # the flags bench.py / tools/bench_variants.py run with
+    flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES | accel.KACC_F_STABLE_SLOT_NODES
+    alg = (accel.interval_bytes(layout.zones, *dims, flags) if K == 1 else
+           accel.intervals_bytes(layout.zones, *dims, K, True, flags))
     fv, wv = values(fdir, "FETCH_SIZE", kernel), values(wdir, "WRITE_SIZE", kernel)
     if not fv or not wv:
         raise SystemExit(f"no {kernel} counter rows found")
