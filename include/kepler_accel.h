@@ -125,7 +125,10 @@ extern "C" {
                                           holds the node of every other row, so
                                           the interval writes it only for NEW
                                           rows and on a node's first read: 4 B
-                                          per process row less HBM traffic.
+                                          per process row less HBM traffic (the
+                                          one-wavefront-per-node kernel of
+                                          KACC_F_SMALL_NODES ignores it: faster
+                                          without the per-lane predicate).
                                           Results are bit-identical.           */
 #define KACC_FAST_MAX_PROCS 2048u
 #define KACC_FAST_MAX_AGGREGATES 512u

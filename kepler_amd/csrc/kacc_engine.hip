@@ -50,7 +50,7 @@ constexpr bool kTransposed = (Z % 2 == 0) && Z >= 4;  // 32-B+ rows: transpose 6
 #define KACC_NS_LANES 16
 #endif
 #ifndef KACC_NS_UNROLL
-#define KACC_NS_UNROLL 4
+#define KACC_NS_UNROLL 2  // 2: 17.9 us at config 3, 4: 19.4, 8: 18.8 (profiles/r03/sq ns_*)
 #endif
 constexpr int kNsLanes = KACC_NS_LANES;      // lanes per namespace (namespace_kernel)
 constexpr int kNsUnroll = KACC_NS_UNROLL;    // pods in flight per namespace lane
@@ -62,11 +62,32 @@ constexpr int kVarSkipProcs = 2;       // skip the process attribution pass
 constexpr int kVarUnstaged = 4;        // never stage Δ in LDS
 constexpr int kVarTemporalStores = 8;  // plain (temporal) stores for the row outputs
 constexpr int kVarNoTranspose = 32;    // per-row scatter only (no 64-row group transpose)
-constexpr int kVarLateAgg = 128;       // aggregates' previous totals loaded after the process pass
+constexpr int kVarLateAgg = 128;       // flips kLateAgg below (timing ablation)
 constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row order only)
 constexpr int kVarNtAgg = 4096;        // non-temporal stores for the aggregate rows too (round 2)
 constexpr int kVarNtScatter = 8192;    // non-temporal per-row scattered process stores (round 2)
 constexpr int kVarTemporalLoads = 16384;  // plain loads of the streamed inputs and prev totals
+// KACC_LATE_AGG: interval_kernel loads the aggregates' previous totals and stores
+// their rows AFTER the process pass (1, round 3) or before it (0, rounds 1-2).
+// Early aggregate rows sit dirty in L2 through the whole process stream and
+// leave it as ~80 MB of extra write traffic per config-3 launch (WRITE_SIZE
+// 1.083 GB early vs 1.002 GB late = the algorithmic writes; profiles/r03/pmcvar2);
+// same-box bench A/B 363 -> 347 us (profiles/r03/late)
+#ifndef KACC_LATE_AGG
+#define KACC_LATE_AGG 1  // 347 vs 363 us at config 3, same box (profiles/r03/late)
+#endif
+// small_kernel (one wavefront per node): the same late aggregate stores, and it
+// ignores KACC_F_STABLE_SLOT_NODES — the per-lane node-store predicate cost it
+// more than the 4 B (config-1 fleet, same box: 312.6 / 289.2 us with the flag
+// honoured and early aggregates, 289.2 / 265.7 us like this; profiles/r03/small2)
+#ifndef KACC_SMALL_LATE_AGG
+#define KACC_SMALL_LATE_AGG 1
+#endif
+#ifndef KACC_SMALL_STABLE
+#define KACC_SMALL_STABLE 0
+#endif
+template <int V>
+constexpr bool kLateAgg = (KACC_LATE_AGG != 0) != ((V & kVarLateAgg) != 0);
 constexpr int kVarBigNoTotal = 256;    // big nodes: no node CPU-total pass
 constexpr int kVarBigNoScan = 512;     // big nodes: no segment-owner scan
 constexpr int kVarBigNoAtomic = 1024;  // big nodes: no item-list atomic (chunk kernel idles)
@@ -97,16 +118,23 @@ constexpr bool kNtAggStores = KACC_NT_AGG != 0;
 #endif
 constexpr bool kNtScatterStores = KACC_NT_SCATTER != 0;
 constexpr uint32_t kPodGrid = 256;     // deferred-pod kernel workgroups (kBlock threads)
-constexpr int kChunkRows = kRowsLds;   // big-node rows per chunk item
-constexpr int kChunkThreads = 512;     // chunk kernel workgroup
-constexpr int kChunkRpt = kChunkRows / kChunkThreads;
 constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node CPU total)
-// KACC_CHUNK_WAVES: waves per SIMD the chunk kernel is compiled for at Z <= 4
-// (4 = two workgroups per CU, 121 VGPRs; 6 = three, 80 VGPRs with spills)
+// KACC_CHUNK_THREADS: chunk kernel workgroup (4 rows per lane: 512 -> 2048-row
+// chunks); KACC_CHUNK_WAVES: waves per SIMD it is compiled for at Z <= 4
+// (512 threads: 4 = two workgroups per CU, 119 VGPRs; 6 = three, 80 VGPRs with
+// spills; 256 threads: a workgroup is one wave per SIMD)
+#ifndef KACC_CHUNK_THREADS
+#define KACC_CHUNK_THREADS 512
+#endif
 #ifndef KACC_CHUNK_WAVES
 #define KACC_CHUNK_WAVES 4
 #endif
-constexpr uint32_t kChunkGrid = 128 * KACC_CHUNK_WAVES;  // persistent chunk-kernel workgroups (all resident)
+constexpr int kChunkThreads = KACC_CHUNK_THREADS;
+constexpr int kChunkRpt = 4;
+constexpr int kChunkRows = kChunkRpt * kChunkThreads;  // big-node rows per chunk item
+static_assert(kChunkRows <= kRowsLds, "a chunk's rows are staged like a fast node's");
+// persistent chunk-kernel workgroups: all resident (256 CUs)
+constexpr uint32_t kChunkGrid = 256u * 4u * KACC_CHUNK_WAVES / (kChunkThreads / 64);
 
 template <int V>
 constexpr int kTpb = 512;  // threads per workgroup (fast path)
@@ -854,7 +882,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   uint64_t a_prev[Z];
   double a_total = 0.0;
   if (a_ok) {
-    if constexpr ((V & kVarLateAgg) == 0) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
+    if constexpr (!kLateAgg<V>) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
     if (role != 2 && !(a_w & KACC_SLOT_NEW)) a_total = a_cpu_total()[a_s];
   } else {
 #pragma unroll
@@ -965,7 +993,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       if (role == 3) export_pod_zero<Z>(b, q0 + j);
       return;
     }
-    if constexpr ((V & kVarLateAgg) != 0) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
+    if constexpr (kLateAgg<V>) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
     uint64_t E[Z];
     double P[Z];
     const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta,
@@ -973,7 +1001,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
     if (role == 3) export_pod<Z>(b, q0 + j, E, P);
   };
-  if constexpr ((V & kVarLateAgg) == 0) aggregate_out();
+  if constexpr (!kLateAgg<V>) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
     if constexpr (kRowSweep) {
 #pragma unroll
@@ -1023,7 +1051,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       store_proc<Z, kNtScat>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   }
-  if constexpr ((V & kVarLateAgg) != 0) aggregate_out();
+  if constexpr (kLateAgg<V>) aggregate_out();
 }
 
 template <int Z, int V>
@@ -1960,7 +1988,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
   }
 
   // ---- E: attribution ------------------------------------------------------------------
-  const Attr<Z> a = make_attr<Z>(sh, b.flags);
+  const Attr<Z> a = make_attr<Z>(sh, KACC_SMALL_STABLE ? b.flags : (b.flags & ~KACC_F_STABLE_SLOT_NODES));
   if (lane == 0) {
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
@@ -1968,22 +1996,27 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     st.node_cpu_delta[n] = a.nd;
     st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
+  // aggregate rows: stored after the process rows when KACC_SMALL_LATE_AGG (as
+  // interval_kernel's KACC_LATE_AGG: early rows sit dirty in L2 through the stream)
+  auto aggregate_out = [&]() {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
-    const uint32_t i = lane + 64u * h, role = role_of(i);
-    const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
-    if (role == 0) continue;
-    if (a_s >= cap_of(role)) {
-      if (role == 3) export_pod_zero<Z>(b, q0 + index_of(i));
-      continue;
+    for (int h = 0; h < 2; ++h) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
+      const uint32_t i = lane + 64u * h, role = role_of(i);
+      const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
+      if (role == 0) continue;
+      if (a_s >= cap_of(role)) {
+        if (role == 3) export_pod_zero<Z>(b, q0 + index_of(i));
+        continue;
+      }
+      uint64_t E[Z];
+      double P[Z];
+      const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h],
+                                            (a_w[h] & KACC_SLOT_NEW) != 0, a_prev[h], E, P);
+      store_agg<Z, kNT && kNtAggStores>(st, role, a_s, E, P, ratio, n);
+      if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P);
     }
-    uint64_t E[Z];
-    double P[Z];
-    const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h],
-                                          (a_w[h] & KACC_SLOT_NEW) != 0, a_prev[h], E, P);
-    store_agg<Z, kNT && kNtAggStores>(st, role, a_s, E, P, ratio, n);
-    if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P);
-  }
+  };
+  if constexpr (KACC_SMALL_LATE_AGG == 0) aggregate_out();
   auto attr_batch = [&](int kb) {  // process.go:118-148
 #pragma unroll
     for (int g = 0; g < kSmallBatch; ++g) {
@@ -2037,6 +2070,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
     load_batch(1, false);
     attr_batch(1);
   }
+  if constexpr (KACC_SMALL_LATE_AGG != 0) aggregate_out();
 }
 
 // ======================= big nodes: chunked row passes ==========================
@@ -4048,7 +4082,9 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
   const uint64_t node = 76 + 96ull * Z;
   // Δ 8 + slot 4 in, previous totals 8Z in; totals 8Z + ratio 8 + node 4 out (the node
   // only for NEW rows under KACC_F_STABLE_SLOT_NODES: not counted)
-  const uint64_t proc = ((flags & KACC_F_STABLE_SLOT_NODES) ? 20 : 24) + 16ull * Z;
+  // (small_kernel, KACC_F_SMALL_NODES, writes it anyway: KACC_SMALL_STABLE)
+  const bool stable = (flags & KACC_F_STABLE_SLOT_NODES) && (KACC_SMALL_STABLE || !(flags & KACC_F_SMALL_NODES));
+  const uint64_t proc = (stable ? 20 : 24) + 16ull * Z;
   // container: end 4 + slot 4 + previous CPU total 8 in, Δ 8 + total 8 out; previous
   // energies 8Z in, energies 8Z + ratio 8 + node 4 out (power derived since ABI 3)
   const uint64_t ctr = 44 + 16ull * Z;
