@@ -1,5 +1,5 @@
 #!/bin/bash
-# Chunk-kernel geometry A/B on config 5 x 60 (kepler_amd/lib/nsvar builds with
+# Chunk-kernel build A/B (geometry, aggregate store order / hints) on config 5 x 60 (kepler_amd/lib/nsvar builds with
 # -DKACC_CHUNK_THREADS / -DKACC_CHUNK_WAVES), parity of each variant's big-node
 # path first (random fleets, chunk edges, config-5 shape, adversarial, stable nodes).
 #   OUT=<dir> LIBS="main c256w5" tools/gpu_chunk_geo.sh
@@ -7,7 +7,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 O=${OUT:-geo}
 mkdir -p gpurun_out/$O
-L=${LIBS:-main c256w4 c256w5 c256w6}
+L=${LIBS:-main cL cP cLP}
 libpath() { [ "$1" = main ] && echo "" || echo "KACC_LIB=kepler_amd/lib/nsvar/libkepler_accel_$1.so"; }
 for l in $L; do
   env $(libpath $l) timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_layout.py -m gpu -q \
