@@ -101,6 +101,8 @@ def parse():
     ap.add_argument("--slot-nodes", choices=["stable", "write"], default="stable",
                     help="stable: KACC_F_STABLE_SLOT_NODES (a process slot keeps its node; only NEW rows store "
                          "it); write: every row stores its node (ablation)")
+    ap.add_argument("--totals-probe", choices=["both", "ns", "nodes"], default="both",
+                    help="ablation: only the namespace sums (ns) or only the cluster node totals (nodes) per step")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -532,8 +534,10 @@ def measure(args, w, rank, world, stream, comm_stream):
                     P([w.nd_p[b].data_ptr()]), P([stream]), P([comm_stream.cuda_stream])) for b in range(2)]
         reduce_fn = lib.kacc_allreduce_exports
     else:  # partial sums from the state tables on the compute stream, the all-reduce on the comm stream
+        no_nodes = args.totals_probe == "ns"
         ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
-                    P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]), P([w.nd_p[b].data_ptr()]), P([stream]),
+                    P([w.ns_p[b].data_ptr()]), None if no_nodes else P([w.nd_e[b].data_ptr()]),
+                    None if no_nodes else P([w.nd_p[b].data_ptr()]), P([stream]),
                     P([comm_stream.cuda_stream])) for b in range(2)]
         reduce_fn = lib.kacc_allreduce_namespaces
     done = [torch.cuda.Event(), torch.cuda.Event()]
@@ -561,7 +565,7 @@ def measure(args, w, rank, world, stream, comm_stream):
                 ev[1].record()
             else:  # the totals' partial-sum kernel (compute stream)
                 time_next(acc.ctx, ev[2], ev[3])
-        rc = reduce_fn(cl.handle, w.n_ns, *ns_args[b])
+        rc = reduce_fn(cl.handle, 0 if args.totals_probe == "nodes" else w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
         if ev is not None and markers:

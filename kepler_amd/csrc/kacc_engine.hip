@@ -2862,17 +2862,24 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
       for (int w = 1; w < kBlock / 64; ++w) t = t + __longlong_as_double(static_cast<long long>(s_w[w][tid]));
       r = static_cast<uint64_t>(__double_as_longlong(t));
     }
-    na.part[static_cast<uint64_t>(b) * kV + tid] = r;
+    // the block partials cross XCDs as device-scope atomic exchanges, performed
+    // beyond L2 (their returned value is waited for, so each is done before the
+    // block counts itself): no L2 write-back per block (a __threadfence pair,
+    // buffer_wbl2 + buffer_inv in every node block, made the node totals the
+    // longest chain of the step: 7.0 of 9.2 us at the 1/8 shard, profiles/r03/tprobe)
+    const unsigned long long old =
+        atomicExch(reinterpret_cast<unsigned long long *>(na.part) + static_cast<uint64_t>(b) * kV + tid,
+                   static_cast<unsigned long long>(r));
+    asm volatile("" ::"v"(old));
   }
   __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    s_last = atomicAdd(na.done, 1u) == nb - 1 ? 1u : 0u;
-  }
+  if (tid == 0) s_last = atomicAdd(na.done, 1u) == nb - 1 ? 1u : 0u;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
-  for (uint32_t x = tid; x < nb * kV; x += kBlock)  // every partial in flight at once
+  // the last block only: drop this XCD's L2 copies of the partials (an earlier
+  // launch's), then read every partial at once
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (uint32_t x = tid; x < nb * kV; x += kBlock)
     s_part[x] = __hip_atomic_load(na.part + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (tid < 2u * Z) {
@@ -2884,7 +2891,7 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
     for (uint32_t k = 0; k < nb; ++k) t = t + __longlong_as_double(static_cast<long long>(s_part[k * kV + tid]));
     na.out_p[tid - 2 * Z] = t;
   }
-  if (tid == 0) *na.done = 0u;  // re-armed for the next launch (stream order)
+  if (tid == 0) atomicExch(na.done, 0u);  // re-armed for the next launch (stream order)
 }
 
 // Elements [first, first + count) of the derived process power table
