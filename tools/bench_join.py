@@ -21,10 +21,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def node_buckets(s):
-    h = 64
-    while h * 2 < 3 * s:
-        h <<= 1
-    return h
+    """kacc_join.hip node_buckets: 1.5 x the node's slots rounded up to 64 buckets (round 3;
+    a power of two before, JOIN_POW2=1 for that build's bytes)."""
+    if os.environ.get("JOIN_POW2"):
+        h = 64
+        while h * 2 < 3 * s:
+            h <<= 1
+        return h
+    return max(64, (3 * s // 2 + 64) & ~63)
 
 
 def main():
