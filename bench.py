@@ -489,12 +489,15 @@ class Workload:
         _, ns_row = layout.namespace_csr_rows()
         self.ns_t = to_device({"off": ns_off, "slot": ns_slot, "row": ns_row})
         self.n_ns = len(ns_off) - 1
-        # cluster totals double-buffered: step k's all-reduce (comm stream) overlaps step k+1's
-        # interval; buffer k % 2 is rewritten only after the all-reduce of step k-2 is done
-        self.ns_e = [torch.zeros(self.n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
-        self.ns_p = [torch.zeros(self.n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
-        self.nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
-        self.nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+        # cluster totals: step k's all-reduce (comm stream) overlaps step k+1's interval.  One
+        # output buffer per step (640 KB at config 3), so the compute stream never waits for an
+        # earlier all-reduce inside the timed loop (a cross-stream wait is a packet on it);
+        # the exports ablation keeps two buffers and waits for step k-2's all-reduce
+        self.n_bufs = 2 if self.exports else n_steps
+        self.ns_e = [torch.zeros(self.n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(self.n_bufs)]
+        self.ns_p = [torch.zeros(self.n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(self.n_bufs)]
+        self.nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(self.n_bufs)]
+        self.nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(self.n_bufs)]
 
     def close(self):
         self.cluster.close()
@@ -538,10 +541,10 @@ def measure(args, w, rank, world, stream, comm_stream):
         ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
                     P([w.ns_p[b].data_ptr()]), None if no_nodes else P([w.nd_e[b].data_ptr()]),
                     None if no_nodes else P([w.nd_p[b].data_ptr()]), P([stream]),
-                    P([comm_stream.cuda_stream])) for b in range(2)]
+                    P([comm_stream.cuda_stream])) for b in range(w.n_bufs)]
         reduce_fn = lib.kacc_allreduce_namespaces
-    done = [torch.cuda.Event(), torch.cuda.Event()]
-    used = [False, False]
+    done = [torch.cuda.Event() for _ in range(w.n_bufs)]
+    used = [False] * w.n_bufs
     compute = torch.cuda.current_stream()
     # one rank, one shard: kacc_allreduce_namespaces enqueues nothing on the comm stream
     comm = world > 1 or w.exports or args.comm_wait == "always"
@@ -549,8 +552,8 @@ def measure(args, w, rank, world, stream, comm_stream):
     time_next = lib.kacc_time_next_launch
 
     def step(k, ev=None, markers=False):
-        b = k % 2
-        if used[b] and comm:  # stream-level wait for step k-2's totals (its buffers are reused; no host sync)
+        b = k % w.n_bufs
+        if used[b] and comm:  # exports ablation: wait for step k-2's all-reduce (its buffers are reused)
             compute.wait_event(done[b])
         if ev is not None:
             if markers:
@@ -570,7 +573,7 @@ def measure(args, w, rank, world, stream, comm_stream):
             cl._check(rc)
         if ev is not None and markers:
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
-        if comm:
+        if comm and w.n_bufs == 2:
             done[b].record(comm_stream)
         used[b] = True
 
