@@ -1055,7 +1055,10 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
 }
 
 template <int Z, int V>
-__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : 6)
+#ifndef KACC_FAST_WAVES
+#define KACC_FAST_WAVES 6  // interval_kernel: waves per SIMD it is compiled for at Z <= 4
+#endif
+__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
 void interval_kernel(const kacc_interval b, const DevState st) {
   interval_node<Z, V>(b, st, blockIdx.x);
 }
