@@ -19,8 +19,9 @@ per GPU) is added as `weak_scaling`; `--scaling weak` makes it the headline.
 `--shard-of W` runs rank 0's shard of a W-way split on one GPU (the per-GPU step
 of a W-GPU run).  Only the cluster totals cross GPUs: per-namespace and cluster
 node totals, all-reduced by the library's own RCCL communicator
-(kacc_cluster_join + kacc_allreduce_namespaces, the C ABI a cgo caller uses; at
-N = 1 the same call runs with a one-rank communicator).  torch.distributed
+(kacc_cluster_join; every step's partial sums by kacc_cluster_partials, then one
+kacc_allreduce_sums per --allreduce-every steps on the comm stream — the C ABI a
+cgo caller uses; at N = 1 the same calls run with a one-rank communicator).  torch.distributed
 (gloo) is only the control plane: rank-0 unique-id broadcast, barriers,
 max-over-ranks timing.
 
@@ -86,10 +87,16 @@ def parse():
                          "the export stores cost 26 us and the concurrent partial sums slow the next interval more "
                          "than they save at config 3, profiles/r03/exports_ablation); tables+writes = the export "
                          "stores alone (ablation)")
+    ap.add_argument("--allreduce-every", type=int, default=8,
+                    help="tables mode: the cluster totals of this many consecutive steps are all-reduced by ONE "
+                         "kacc_allreduce_sums (each step's partial sums have their own rows; SURVEY 5: one "
+                         "all-reduce per K intervals), so the compute stream carries one handoff event per group "
+                         "(each costs ~6.5 us of stream gap, profiles/r03/handoff); 1 = every step")
     ap.add_argument("--comm-wait", choices=["auto", "always"], default="auto",
-                    help="auto: the compute stream waits for the comm stream's all-reduce of step k-2 only when "
-                         "there is one (N > 1); at one rank the totals are the partial sums and the comm stream "
-                         "is idle, so no cross-stream packet is issued; always: issue it anyway (ablation)")
+                    help="auto: cross-stream packets only where the library issues them (N > 1: an event on the "
+                         "compute stream after the partial sums, waited for by the comm stream's all-reduce); "
+                         "always: at one rank, record the same timing-free event on the compute stream and make "
+                         "the comm stream wait for it every step (the N > 1 handoff without RCCL, ablation)")
     ap.add_argument("--step-events", choices=["separate", "inline", "markers"], default="separate",
                     help="how the kernels are timed with HIP events: separate = the timed region has NO event "
                          "packet between its kernels (value, ms_per_step) and a second timed pass over the same "
@@ -489,15 +496,28 @@ class Workload:
         _, ns_row = layout.namespace_csr_rows()
         self.ns_t = to_device({"off": ns_off, "slot": ns_slot, "row": ns_row})
         self.n_ns = len(ns_off) - 1
-        # cluster totals: step k's all-reduce (comm stream) overlaps step k+1's interval.  One
-        # output buffer per step (640 KB at config 3), so the compute stream never waits for an
-        # earlier all-reduce inside the timed loop (a cross-stream wait is a packet on it);
-        # the exports ablation keeps two buffers and waits for step k-2's all-reduce
+        # cluster totals.  Tables mode: step k's partial sums go to row k of tot_e / tot_p
+        # ([namespaces Z | node totals 2Z] u64, [namespaces Z | node totals 3Z] f64; 640 KB per
+        # step at config 3), and every --allreduce-every steps ONE kacc_allreduce_sums reduces
+        # those rows on the comm stream while the next intervals run: one compute-to-comm
+        # handoff (an event packet on the compute stream, ~6.5 us of stream gap,
+        # profiles/r03/handoff) per group instead of per step, and the compute stream never
+        # waits for an all-reduce.  The exports ablation keeps two buffers per step parity and
+        # waits for step k-2's all-reduce.
         self.n_bufs = 2 if self.exports else n_steps
-        self.ns_e = [torch.zeros(self.n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(self.n_bufs)]
-        self.ns_p = [torch.zeros(self.n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(self.n_bufs)]
-        self.nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(self.n_bufs)]
-        self.nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(self.n_bufs)]
+        nsz = self.n_ns * Z
+        self.tot_e = torch.zeros(n_steps, nsz + 2 * Z, dtype=torch.int64, device="cuda")
+        self.tot_p = torch.zeros(n_steps, nsz + 3 * Z, dtype=torch.float64, device="cuda")
+        if self.exports:
+            self.ns_e = [torch.zeros(nsz, dtype=torch.int64, device="cuda") for _ in range(2)]
+            self.ns_p = [torch.zeros(nsz, dtype=torch.float64, device="cuda") for _ in range(2)]
+            self.nd_e = [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+            self.nd_p = [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(2)]
+        else:
+            self.ns_e = [self.tot_e[k, :nsz] for k in range(n_steps)]
+            self.ns_p = [self.tot_p[k, :nsz] for k in range(n_steps)]
+            self.nd_e = [self.tot_e[k, nsz:] for k in range(n_steps)]
+            self.nd_p = [self.tot_p[k, nsz:] for k in range(n_steps)]
 
     def close(self):
         self.cluster.close()
@@ -536,24 +556,45 @@ def measure(args, w, rank, world, stream, comm_stream):
                     P([w.ns_e[b].data_ptr()]), P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]),
                     P([w.nd_p[b].data_ptr()]), P([stream]), P([comm_stream.cuda_stream])) for b in range(2)]
         reduce_fn = lib.kacc_allreduce_exports
-    else:  # partial sums from the state tables on the compute stream, the all-reduce on the comm stream
+    else:  # partial sums from the state tables on the compute stream (kacc_cluster_partials); the
+        # all-reduce of a group of steps' rows on the comm stream (kacc_allreduce_sums, flush())
         no_nodes = args.totals_probe == "ns"
         ns_args = [(P([w.ns_t["off"].data_ptr()]), P([w.ns_t["slot"].data_ptr()]), P([w.ns_e[b].data_ptr()]),
                     P([w.ns_p[b].data_ptr()]), None if no_nodes else P([w.nd_e[b].data_ptr()]),
-                    None if no_nodes else P([w.nd_p[b].data_ptr()]), P([stream]),
-                    P([comm_stream.cuda_stream])) for b in range(w.n_bufs)]
-        reduce_fn = lib.kacc_allreduce_namespaces
+                    None if no_nodes else P([w.nd_p[b].data_ptr()]), P([stream])) for b in range(w.n_bufs)]
+        reduce_fn = lib.kacc_cluster_partials
     done = [torch.cuda.Event() for _ in range(w.n_bufs)]
     used = [False] * w.n_bufs
     compute = torch.cuda.current_stream()
-    # one rank, one shard: kacc_allreduce_namespaces enqueues nothing on the comm stream
-    comm = world > 1 or w.exports or args.comm_wait == "always"
+    # one rank, one shard: the library enqueues nothing on the comm stream
+    comm = world > 1 or w.exports
+    handoff = world == 1 and args.comm_wait == "always"
+    handoff_ev = torch.cuda.Event()  # timing disabled, as the library's own handoff event
+    group = max(1, args.allreduce_every)
+    pending = [None]  # first step whose partial-sum rows are not all-reduced yet
+    ne_row, np_row = w.tot_e.shape[1], w.tot_p.shape[1]
+
+    def flush(last):
+        """Tables mode: ONE all-reduce of the rows of steps pending[0] .. last (contiguous)."""
+        k0 = pending[0]
+        if k0 is None:
+            return
+        pending[0] = None
+        m = last - k0 + 1
+        if handoff:  # one rank: the library reduces nothing; the handoff it would issue
+            handoff_ev.record(compute)
+            comm_stream.wait_event(handoff_ev)
+        rc = lib.kacc_allreduce_sums(cl.handle, P([w.tot_e[k0].data_ptr()]), m * ne_row,
+                                     P([w.tot_p[k0].data_ptr()]), m * np_row, P([stream]),
+                                     P([comm_stream.cuda_stream]))
+        if rc != accel.KACC_OK:
+            cl._check(rc)
 
     time_next = lib.kacc_time_next_launch
 
-    def step(k, ev=None, markers=False):
+    def step(k, ev=None, markers=False, last=None):
         b = k % w.n_bufs
-        if used[b] and comm:  # exports ablation: wait for step k-2's all-reduce (its buffers are reused)
+        if used[b] and comm and w.exports:  # exports ablation: wait for step k-2's all-reduce (its buffers are reused)
             compute.wait_event(done[b])
         if ev is not None:
             if markers:
@@ -573,7 +614,14 @@ def measure(args, w, rank, world, stream, comm_stream):
             cl._check(rc)
         if ev is not None and markers:
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
-        if comm and w.n_bufs == 2:
+        if not w.exports:
+            if pending[0] is None:
+                pending[0] = k
+            # a full group, or the one before a region's last step: that step is reduced
+            # alone, so the all-reduce left after the region's last interval is one step's
+            if k - pending[0] + 1 >= group or (last is not None and k == last - 1):
+                flush(k)
+        if comm and w.exports:
             done[b].record(comm_stream)
         used[b] = True
 
@@ -584,7 +632,8 @@ def measure(args, w, rank, world, stream, comm_stream):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(first + i, evs[i] if evs else None, markers)
+            step(first + i, evs[i] if evs else None, markers, first + args.steps - 1)
+        flush(first + args.steps - 1)  # the last group, however short
         torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
         if world > 1:
             dist.barrier()
@@ -594,6 +643,7 @@ def measure(args, w, rank, world, stream, comm_stream):
 
     for k in range(args.warmup):
         step(k)
+    flush(args.warmup - 1)
     acc.sync(stream)
     torch.cuda.synchronize()
     tevs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
@@ -724,9 +774,11 @@ def main():
             "shard_of": args.shard_of,
             "cluster_totals": ("kacc_allreduce_exports (interval exports; partial sums + RCCL on the comm stream)"
                                if args.totals == "exports" else
-                               "kacc_allreduce_namespaces (partial sums from the tables on the compute stream)"),
+                               f"kacc_cluster_partials every step (from the tables, compute stream) + one "
+                               f"kacc_allreduce_sums per {max(1, args.allreduce_every)} steps (comm stream)"),
+            "allreduce_every": None if args.totals == "exports" else max(1, args.allreduce_every),
             "parallelism": f"node-sharded x{world} (shard.plan_node_ranges); namespace + cluster node "
-                           f"totals all-reduced over RCCL by kacc_allreduce_namespaces",
+                           f"totals all-reduced over RCCL inside libkepler_accel",
         },
         "node_snapshots_per_s": total_nodes_done * K * args.steps / wall_max,
         "kernel_ms": k_avg_ms,

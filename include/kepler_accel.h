@@ -445,6 +445,26 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
                               double *const *out_power, uint64_t *const *out_node_energy,
                               double *const *out_node_power, void *const *streams,
                               void *const *comm_streams);
+/* The two halves of kacc_allreduce_namespaces, for a caller that reduces the
+ * totals of several intervals with ONE collective (one all-reduce
+ * per K intervals; the cluster sum is PromQL's in the reference,
+ * internal/resource/types.go:106-110, so no reference call is replaced).
+ * kacc_cluster_partials: step 1 only — each shard's partial sums into its own
+ * out_* on streams[s] (arguments as kacc_allreduce_namespaces).
+ * kacc_allreduce_sums: the rest, in place, over any vectors: energy[s] u64
+ * [n_e] and power[s] f64 [n_p] of every local shard are summed over the
+ * shards (shard order) and the ranks, and every shard receives the sum.  Lay
+ * K intervals' partials out back to back ([K][n_ns*Z + 2Z] u64, [K][n_ns*Z +
+ * 3Z] f64) and one call reduces all of them: one compute-to-comm stream
+ * handoff (an event packet on streams[s]) and one RCCL group per K
+ * intervals instead of per interval.  The collective runs on comm_streams[s]
+ * when given.  One rank with one shard: nothing to do.                     */
+int kacc_cluster_partials(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                          const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
+                          double *const *out_power, uint64_t *const *out_node_energy,
+                          double *const *out_node_power, void *const *streams);
+int kacc_allreduce_sums(kacc_cluster *c, uint64_t *const *energy, uint64_t n_e, double *const *power,
+                        uint64_t n_p, void *const *streams, void *const *comm_streams);
 /* The same cluster totals from the interval's exports (kacc_interval.pod_export
  * / node_export) instead of the state tables: nothing runs on streams[s]
  * except an event record — the partial sums run on comm_streams[s] after the

@@ -145,6 +145,8 @@ EXPORTS = [
     "kacc_cluster_rccl",
     "kacc_cluster_info",
     "kacc_allreduce_namespaces",
+    "kacc_cluster_partials",
+    "kacc_allreduce_sums",
     "kacc_allreduce_exports",
     "kacc_gather_pods",
     "kacc_last_error_copy",
@@ -300,6 +302,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_cluster_info.argtypes = [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]
     lib.kacc_cluster_rccl.argtypes = [POINTER(c_int), c_char_p, ctypes.c_size_t]
     lib.kacc_allreduce_namespaces.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 8
+    lib.kacc_cluster_partials.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 7
+    lib.kacc_allreduce_sums.argtypes = [c_void_p, POINTER(c_void_p), c_uint64, POINTER(c_void_p), c_uint64,
+                                        POINTER(c_void_p), POINTER(c_void_p)]
     lib.kacc_allreduce_exports.argtypes = [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_uint32),
                                            POINTER(c_void_p), POINTER(c_uint32)] + [POINTER(c_void_p)] * 7
     lib.kacc_gather_pods.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_void_p), c_uint64, POINTER(c_void_p),
@@ -904,6 +909,29 @@ class Cluster:
             self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_slot) if n_ns else None,
             _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
             _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
+            _ptrs(streams) if streams else None, _ptrs(comm_streams) if comm_streams else None))
+
+    def partials(self, n_ns: int, ns_pod_off, ns_pod_slot, out_energy, out_power, out_node_energy=None,
+                 out_node_power=None, streams=None) -> None:
+        """kacc_cluster_partials: each shard's partial sums only (no collective)."""
+        n = len(self.shards)
+        if n_ns and not (len(ns_pod_off) == len(ns_pod_slot) == len(out_energy) == len(out_power) == n):
+            raise ValueError("one namespace CSR and output pair per local shard")
+        node = out_node_energy is not None
+        self._check(self.lib.kacc_cluster_partials(
+            self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_slot) if n_ns else None,
+            _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
+            _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
+            _ptrs(streams) if streams else None))
+
+    def allreduce_sums(self, energy, n_e: int, power, n_p: int, streams=None, comm_streams=None) -> None:
+        """kacc_allreduce_sums: in-place sum over shards and ranks of per-shard u64 [n_e] / f64 [n_p]
+        device vectors (several intervals' partials back to back: one collective for all)."""
+        n = len(self.shards)
+        if (n_e and len(energy) != n) or (n_p and len(power) != n):
+            raise ValueError("one vector pair per local shard")
+        self._check(self.lib.kacc_allreduce_sums(
+            self.handle, _ptrs(energy) if n_e else None, n_e, _ptrs(power) if n_p else None, n_p,
             _ptrs(streams) if streams else None, _ptrs(comm_streams) if comm_streams else None))
 
     def allreduce_exports(self, n_ns: int, ns_pod_off, ns_pod_row, n_pods, pod_export, out_energy, out_power,

@@ -459,15 +459,17 @@ int kacc_cluster_info(const kacc_cluster *c, int *nranks, int *rank, int *n_shar
   return KACC_OK;
 }
 
-int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
-                              const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
-                              double *const *out_power, uint64_t *const *out_node_energy,
-                              double *const *out_node_power, void *const *streams,
-                              void *const *comm_streams) {
-  if (!c) return KACC_EINVAL;
+}  // extern "C"
+
+namespace {
+// Step 1 of kacc_allreduce_namespaces / kacc_cluster_partials: the checked
+// arguments, then every shard's partial vectors (namespace sums and node totals
+// in one launch per shard) on its stream.
+int shard_partials(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                   const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy, double *const *out_power,
+                   uint64_t *const *out_node_energy, double *const *out_node_power, void *const *streams) {
   kacc_ctx *c0 = c->shards[0];
   const size_t ns = c->shards.size();
-  const uint64_t Z = c->zones;
   const bool nodes = out_node_energy && out_node_power;
   if ((out_node_energy != nullptr) != (out_node_power != nullptr))
     return kacc_fail(c0, KACC_EINVAL, "node totals need both output arrays");
@@ -479,8 +481,6 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
     if (nodes && (!out_node_energy[s] || !out_node_power[s]))
       return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL node-total array", s);
   }
-  // 1. partial vectors of every shard, on its stream: namespace sums and node
-  //    totals in one launch per shard
   for (size_t s = 0; s < ns; ++s) {
     kacc_ctx *x = c->shards[s];
     hipStream_t st = shard_stream(c, streams, s);
@@ -489,24 +489,77 @@ int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *co
         n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr, st);
     if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
   }
+  return KACC_OK;
+}
+
+// The comm streams wait for the work queued on the compute streams so far (one
+// event packet on each compute stream).
+int handoff(kacc_cluster *c, void *const *streams, void *const *comm_streams) {
+  kacc_ctx *c0 = c->shards[0];
+  if (!comm_streams) return KACC_OK;
+  for (size_t s = 0; s < c->shards.size(); ++s) {
+    hipStream_t a = shard_stream(c, streams, s), b = shard_stream(c, comm_streams, s);
+    if (a == b) continue;
+    KACC_HIP(c0, hipSetDevice(c->shards[s]->device));
+    KACC_HIP(c0, hipEventRecord(c->events[s], a));
+    KACC_HIP(c0, hipStreamWaitEvent(b, c->events[s], 0));
+  }
+  return KACC_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int kacc_cluster_partials(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                          const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy, double *const *out_power,
+                          uint64_t *const *out_node_energy, double *const *out_node_power, void *const *streams) {
+  if (!c) return KACC_EINVAL;
+  return shard_partials(c, n_ns, ns_pod_off, ns_pod_slot, out_energy, out_power, out_node_energy, out_node_power,
+                        streams);
+}
+
+int kacc_allreduce_sums(kacc_cluster *c, uint64_t *const *energy, uint64_t n_e, double *const *power, uint64_t n_p,
+                        void *const *streams, void *const *comm_streams) {
+  if (!c) return KACC_EINVAL;
+  kacc_ctx *c0 = c->shards[0];
+  const size_t ns = c->shards.size();
+  if ((n_e && !energy) || (n_p && !power)) return kacc_fail(c0, KACC_EINVAL, "NULL argument");
+  for (size_t s = 0; s < ns; ++s)
+    if ((n_e && !energy[s]) || (n_p && !power[s])) return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL vector", s);
+  if ((c->nranks == 1 && ns == 1) || (!n_e && !n_p)) return KACC_OK;
+  int rc = local_combine(c, streams, energy, n_e, power, n_p);
+  if (rc != KACC_OK) return rc;
+  if ((rc = handoff(c, streams, comm_streams)) != KACC_OK) return rc;
+  void *const *cs = comm_streams ? comm_streams : streams;
+  const ReduceReq req{energy, n_e, power, n_p};
+  if ((rc = allreduce(c, cs, &req, 1)) != KACC_OK) return rc;
+  return local_broadcast(c, cs, energy, n_e, power, n_p);
+}
+
+int kacc_allreduce_namespaces(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
+                              const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
+                              double *const *out_power, uint64_t *const *out_node_energy,
+                              double *const *out_node_power, void *const *streams,
+                              void *const *comm_streams) {
+  if (!c) return KACC_EINVAL;
+  const size_t ns = c->shards.size();
+  const uint64_t Z = c->zones;
+  const bool nodes = out_node_energy && out_node_power;
+  // 1. partial vectors of every shard, on its stream: namespace sums and node
+  //    totals in one launch per shard
+  int rc = shard_partials(c, n_ns, ns_pod_off, ns_pod_slot, out_energy, out_power, out_node_energy, out_node_power,
+                          streams);
+  if (rc != KACC_OK) return rc;
   // one rank, one shard: the partial sums are the cluster totals (no combine, no
   // collective, and no cross-stream packets between the caller's intervals)
   if (c->nranks == 1 && ns == 1) return KACC_OK;
   // 2. shards of one GPU (on the compute streams)
-  int rc = KACC_OK;
   if (n_ns && (rc = local_combine(c, streams, out_energy, n_ns * Z, out_power, n_ns * Z)) != KACC_OK) return rc;
   if (nodes && (rc = local_combine(c, streams, out_node_energy, 2 * Z, out_node_power, 3 * Z)) != KACC_OK) return rc;
   // the collective may run on other streams: they wait for the partial sums,
   // and the caller's next interval on the compute stream overlaps it
   void *const *cs = comm_streams ? comm_streams : streams;
-  if (comm_streams)
-    for (size_t s = 0; s < ns; ++s) {
-      hipStream_t a = shard_stream(c, streams, s), b = shard_stream(c, comm_streams, s);
-      if (a == b) continue;
-      KACC_HIP(c0, hipSetDevice(c->shards[s]->device));
-      KACC_HIP(c0, hipEventRecord(c->events[s], a));
-      KACC_HIP(c0, hipStreamWaitEvent(b, c->events[s], 0));
-    }
+  if ((rc = handoff(c, streams, comm_streams)) != KACC_OK) return rc;
   // 3. across GPUs (RCCL: every vector in one group), 4. back to every shard
   ReduceReq reqs[2];
   int n_reqs = 0;

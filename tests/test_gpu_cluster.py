@@ -149,6 +149,64 @@ def test_sharded_fleet_matches_unsharded_oracle(world):
     cl.close()
 
 
+def test_batched_allreduce_matches_per_interval():
+    """kacc_cluster_partials per interval into back-to-back [K][n_ns*Z + 2Z] / [K][n_ns*Z + 3Z]
+    rows, then ONE kacc_allreduce_sums over all K intervals == kacc_allreduce_namespaces after
+    each interval (bit-exact: the same shard partials, shard-order combine, the same collective)."""
+    L = fleet.make_layout(40, [2000, 300, 0, 1, 700, 64, 1500, 9] * 5, 4, seed=43, n_namespaces=11,
+                          shuffle_slots=True)
+    world, K = 3, 4
+    shards = shard.shard(L, world)
+    cl = accel.Cluster.create_multi([0] * world, L.zones, [sl.capacities() for _, _, sl in shards])
+    sim = fleet.FleetSim(L, seed=43, churn=0.04, read_error_frac=0.05)
+    s = current_stream_handle()
+    comm = torch.cuda.Stream()
+    Z, n_ns = L.zones, L.n_namespaces
+    csr = _namespace_csr_device([sl for _, _, sl in shards])
+    ne, npw = n_ns * Z + 2 * Z, n_ns * Z + 3 * Z
+    te = [torch.zeros(K, ne, dtype=torch.int64, device="cuda") for _ in range(world)]
+    tp = [torch.zeros(K, npw, dtype=torch.float64, device="cuda") for _ in range(world)]
+    ref = []
+    keep = []
+    for k in range(K):
+        a = sim.next_interval()
+        for (lo, hi, sl), acc in zip(shards, cl.shards):
+            sub, sizes, _ = fleet.subset_interval(a, np.arange(lo, hi), L.zones)
+            t = to_device(sub)
+            keep.append(t)
+            acc.run_interval(interval_from_tensors(t, sizes, sl.fast_flag()), s)
+        r = ([torch.zeros(n_ns * Z, dtype=torch.int64, device="cuda") for _ in range(world)],
+             [torch.zeros(n_ns * Z, dtype=torch.float64, device="cuda") for _ in range(world)],
+             [torch.zeros(2 * Z, dtype=torch.int64, device="cuda") for _ in range(world)],
+             [torch.zeros(3 * Z, dtype=torch.float64, device="cuda") for _ in range(world)])
+        cl.allreduce_namespaces(n_ns, [c["o"].data_ptr() for c in csr], [c["s"].data_ptr() for c in csr],
+                                *[[x.data_ptr() for x in v] for v in r], streams=[s] * world,
+                                comm_streams=[comm.cuda_stream] * world)
+        ref.append(r)
+        cl.partials(n_ns, [c["o"].data_ptr() for c in csr], [c["s"].data_ptr() for c in csr],
+                    [x[k].data_ptr() for x in te], [x[k].data_ptr() for x in tp],
+                    [x[k, n_ns * Z:].data_ptr() for x in te], [x[k, n_ns * Z:].data_ptr() for x in tp],
+                    streams=[s] * world)
+    cl.allreduce_sums([x.data_ptr() for x in te], K * ne, [x.data_ptr() for x in tp], K * npw,
+                      streams=[s] * world, comm_streams=[comm.cuda_stream] * world)
+    torch.cuda.synchronize()
+    for acc in cl.shards:
+        acc.sync(s)
+    for k in range(K):
+        oe, op, nde, ndp = ref[k]
+        for r in range(world):
+            e, p = te[r][k].cpu().numpy(), tp[r][k].cpu().numpy()
+            np.testing.assert_array_equal(e[:n_ns * Z], oe[r].cpu().numpy(), err_msg=f"interval {k} shard {r}")
+            np.testing.assert_array_equal(e[n_ns * Z:], nde[r].cpu().numpy())
+            np.testing.assert_array_equal(p[:n_ns * Z].view(np.uint64), op[r].cpu().numpy().view(np.uint64))
+            np.testing.assert_array_equal(p[n_ns * Z:].view(np.uint64), ndp[r].cpu().numpy().view(np.uint64))
+    assert np.count_nonzero(ref[-1][0][0].cpu().numpy()) > 0  # (the first interval is a first read: zeros)
+    with pytest.raises(accel.AccelError) as ei:  # a missing shard vector is refused
+        cl.allreduce_sums([te[0].data_ptr(), 0, te[2].data_ptr()], ne, [x.data_ptr() for x in tp], npw)
+    assert ei.value.code == accel.KACC_EINVAL
+    cl.close()
+
+
 def test_cluster_join_one_rank():
     """The one-process-per-GPU entry (kacc_cluster_unique_id + kacc_cluster_join, what
     bench.py --gpus N uses) with a one-rank communicator == the context's own totals."""
