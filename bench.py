@@ -524,6 +524,19 @@ class Workload:
         self.acc.close()
 
 
+def allreduce_groups(first, n, group):
+    """The all-reduce groups of the n consecutive steps first .. first + n - 1 (tables mode): at
+    most `group` steps each, and the region's last step alone, so that what is left to reduce
+    after the region's last interval is one step's rows.  [(first_step, last_step), ...] in
+    order, covering every step exactly once."""
+    out, k0, last = [], first, first + n - 1
+    for k in range(first, first + n):
+        if k - k0 + 1 >= max(1, group) or k >= last - 1:
+            out.append((k0, k))
+            k0 = k + 1
+    return out
+
+
 def total_steps(args):
     """Warm-up steps, the timed steps and (--step-events separate) the kernel-timing pass: every
     step has its own node counters / clocks (monotonic, as a node's RAPL readings)."""
@@ -571,15 +584,15 @@ def measure(args, w, rank, world, stream, comm_stream):
     handoff = world == 1 and args.comm_wait == "always"
     handoff_ev = torch.cuda.Event()  # timing disabled, as the library's own handoff event
     group = max(1, args.allreduce_every)
-    pending = [None]  # first step whose partial-sum rows are not all-reduced yet
     ne_row, np_row = w.tot_e.shape[1], w.tot_p.shape[1]
+    group_of = {}  # last step of a group -> its first step (allreduce_groups of each region)
 
-    def flush(last):
-        """Tables mode: ONE all-reduce of the rows of steps pending[0] .. last (contiguous)."""
-        k0 = pending[0]
-        if k0 is None:
-            return
-        pending[0] = None
+    def plan(first, n):
+        group_of.clear()
+        group_of.update({k1: k0 for k0, k1 in allreduce_groups(first, n, group)})
+
+    def flush(k0, last):
+        """Tables mode: ONE all-reduce of the rows of steps k0 .. last (contiguous)."""
         m = last - k0 + 1
         if handoff:  # one rank: the library reduces nothing; the handoff it would issue
             handoff_ev.record(compute)
@@ -592,7 +605,7 @@ def measure(args, w, rank, world, stream, comm_stream):
 
     time_next = lib.kacc_time_next_launch
 
-    def step(k, ev=None, markers=False, last=None):
+    def step(k, ev=None, markers=False):
         b = k % w.n_bufs
         if used[b] and comm and w.exports:  # exports ablation: wait for step k-2's all-reduce (its buffers are reused)
             compute.wait_event(done[b])
@@ -614,13 +627,8 @@ def measure(args, w, rank, world, stream, comm_stream):
             cl._check(rc)
         if ev is not None and markers:
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
-        if not w.exports:
-            if pending[0] is None:
-                pending[0] = k
-            # a full group, or the one before a region's last step: that step is reduced
-            # alone, so the all-reduce left after the region's last interval is one step's
-            if k - pending[0] + 1 >= group or (last is not None and k == last - 1):
-                flush(k)
+        if not w.exports and k in group_of:
+            flush(group_of[k], k)
         if comm and w.exports:
             done[b].record(comm_stream)
         used[b] = True
@@ -630,10 +638,10 @@ def measure(args, w, rank, world, stream, comm_stream):
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        plan(first, args.steps)
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(first + i, evs[i] if evs else None, markers, first + args.steps - 1)
-        flush(first + args.steps - 1)  # the last group, however short
+            step(first + i, evs[i] if evs else None, markers)
         torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
         if world > 1:
             dist.barrier()
@@ -641,9 +649,9 @@ def measure(args, w, rank, world, stream, comm_stream):
         acc.sync(stream)  # surfaces any device-detected range error
         return wall
 
+    plan(0, args.warmup)
     for k in range(args.warmup):
         step(k)
-    flush(args.warmup - 1)
     acc.sync(stream)
     torch.cuda.synchronize()
     tevs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]

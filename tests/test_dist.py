@@ -107,3 +107,22 @@ def test_bench_control_plane_two_ranks(tmp_path):
     import bench
 
     assert bench.bench_nodes(3, 2, 60, "weak") == 120 and bench.bench_nodes(4, 2, 90, "weak") == 90
+
+
+def test_bench_allreduce_groups():
+    """bench.py's schedule of the grouped cluster all-reduce (kacc_allreduce_sums over K steps'
+    rows): every step of a region in exactly one group, in order, contiguous, at most `group`
+    steps each, and the region's last step alone (one step's rows left after its last interval).
+    Every rank derives the same schedule from its arguments, so the collectives match."""
+    import bench
+
+    assert bench.allreduce_groups(0, 20, 8) == [(0, 7), (8, 15), (16, 18), (19, 19)]
+    assert bench.allreduce_groups(23, 20, 8) == [(23, 30), (31, 38), (39, 41), (42, 42)]
+    assert bench.allreduce_groups(0, 3, 8) == [(0, 1), (2, 2)]
+    assert bench.allreduce_groups(5, 1, 8) == [(5, 5)]
+    assert bench.allreduce_groups(0, 0, 8) == []
+    assert bench.allreduce_groups(0, 4, 1) == [(0, 0), (1, 1), (2, 2), (3, 3)]
+    for first, n, g in [(0, 20, 8), (3, 50, 7), (0, 17, 16), (9, 2, 3), (0, 64, 0)]:
+        gs = bench.allreduce_groups(first, n, g)
+        assert [k for a, b in gs for k in range(a, b + 1)] == list(range(first, first + n))
+        assert all(b - a + 1 <= max(1, g) for a, b in gs) and gs[-1][0] == gs[-1][1]
