@@ -92,6 +92,9 @@ def parse():
                          "kacc_allreduce_sums (each step's partial sums have their own rows; SURVEY 5: one "
                          "all-reduce per K intervals), so the compute stream carries one handoff event per group "
                          "(each costs ~6.5 us of stream gap, profiles/r03/handoff); 1 = every step")
+    ap.add_argument("--handoff-event", choices=["device", "torch"], default="device",
+                    help="--comm-wait always: the emulated handoff event is the library's (timing disabled, "
+                         "device-scope release) or a default torch event (system-scope release; ablation)")
     ap.add_argument("--comm-wait", choices=["auto", "always"], default="auto",
                     help="auto: cross-stream packets only where the library issues them (N > 1: an event on the "
                          "compute stream after the partial sums, waited for by the comm stream's all-reduce); "
@@ -582,7 +585,14 @@ def measure(args, w, rank, world, stream, comm_stream):
     # one rank, one shard: the library enqueues nothing on the comm stream
     comm = world > 1 or w.exports
     handoff = world == 1 and args.comm_wait == "always"
-    handoff_ev = torch.cuda.Event()  # timing disabled, as the library's own handoff event
+    # the library's own handoff event: timing disabled, device-scope release (--handoff-event
+    # torch: a default torch event, system-scope release, ablation)
+    if args.handoff_event == "torch":
+        handoff_ev = torch.cuda.Event()
+    else:
+        handoff_ev = ctypes.c_void_p()
+        if lib.hipEventCreateWithFlags(ctypes.byref(handoff_ev), ctypes.c_uint(0x2 | 0x40000000)) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
     group = max(1, args.allreduce_every)
     ne_row, np_row = w.tot_e.shape[1], w.tot_p.shape[1]
     group_of = {}  # last step of a group -> its first step (allreduce_groups of each region)
@@ -595,8 +605,12 @@ def measure(args, w, rank, world, stream, comm_stream):
         """Tables mode: ONE all-reduce of the rows of steps k0 .. last (contiguous)."""
         m = last - k0 + 1
         if handoff:  # one rank: the library reduces nothing; the handoff it would issue
-            handoff_ev.record(compute)
-            comm_stream.wait_event(handoff_ev)
+            if args.handoff_event == "torch":
+                handoff_ev.record(compute)
+                comm_stream.wait_event(handoff_ev)
+            else:
+                lib.hipEventRecord(handoff_ev, ctypes.c_void_p(stream))
+                lib.hipStreamWaitEvent(ctypes.c_void_p(comm_stream.cuda_stream), handoff_ev, ctypes.c_uint(0))
         rc = lib.kacc_allreduce_sums(cl.handle, P([w.tot_e[k0].data_ptr()]), m * ne_row,
                                      P([w.tot_p[k0].data_ptr()]), m * np_row, P([stream]),
                                      P([comm_stream.cuda_stream]))
