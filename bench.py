@@ -585,9 +585,12 @@ def measure(args, w, rank, world, stream, comm_stream):
     # one rank, one shard: the library enqueues nothing on the comm stream
     comm = world > 1 or w.exports
     handoff = world == 1 and args.comm_wait == "always"
-    # the library's own handoff event: timing disabled, device-scope release (--handoff-event
-    # torch: a default torch event, system-scope release, ablation)
-    if args.handoff_event == "torch":
+    # --comm-wait always: the emulated handoff event, timing-free with a device-scope release
+    # (--handoff-event device) or a default torch event (torch: system-scope release)
+    handoff_ev = None
+    if not handoff:
+        pass
+    elif args.handoff_event == "torch":
         handoff_ev = torch.cuda.Event()
     else:
         handoff_ev = ctypes.c_void_p()
