@@ -72,6 +72,8 @@ def parse():
                          "without / with node_proc_span, F fragmented) and report them as `slot_layouts` (0 = off)")
     ap.add_argument("--no-pipeline-line", dest="pipeline_line", action="store_false",
                     help="N = 1, config 3: skip the join -> tracker -> interval line (`pipeline`)")
+    ap.add_argument("--no-host-line", dest="host_line", action="store_false",
+                    help="N = 1, config 3: skip the end-to-end pinned-batch line (`host_path`)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="N > 1: strong = the config's fixed fleet (config 3: 10k nodes) cut into N node ranges "
                          "(the north star's 8-GPU target); weak = N x the fleet, a full shard per GPU")
@@ -140,6 +142,32 @@ def host_cpu():
     return dict(model=model, nproc=os.cpu_count(), usable=usable)
 
 
+def cpu_share():
+    """Host threads this job may use and where that number comes from.  A GPU box grants each
+    one-GPU job a share of its host (OMP_NUM_THREADS, set by the box: 16 of the 256 hardware
+    threads; the rest belong to the other GPUs' jobs), else a cgroup CPU quota, else the
+    affinity mask (usable cores)."""
+    usable = host_cpu()["usable"] or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return min(usable, int(env)), "OMP_NUM_THREADS (the box's CPU share for this job)"
+    for path, parse_q in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                          ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+            if parse_q:
+                q, per = parse_q(txt)
+            else:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    q, per = txt, f.read().strip()
+            if q not in ("max", "-1"):
+                return max(1, min(usable, -(-int(q) // int(per)))), f"cgroup CPU quota ({path})"
+        except (OSError, ValueError):
+            pass
+    return usable, "affinity mask (usable cores)"
+
+
 def _median_rate(run, rows, budget_s, min_runs=5, max_runs=0):
     """Warm-up call, then timed calls until the budget (>= min_runs); rows / median seconds."""
     run(-1)  # warm-up (untimed)
@@ -189,10 +217,11 @@ def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds, max_runs=0):
         pre = [batch(k) for k in range(8)]
         out[name] = _median_rate(lambda k: o.interval(pre[max(k, 0) % 8], sizes), sizes["n_procs"], budget,
                                  max_runs=max_runs)
-    # the flat-array port on the host's cores (node ranges per thread), on a 10x larger node
-    # sample: the strongest CPU number this repo can produce
-    threads = max(1, min(16, host_cpu()["usable"] or 1, int(os.environ.get("OMP_NUM_THREADS", "16"))))
-    nodes_mt = np.arange(min(10 * n_nodes, layout.n_nodes))
+    # the flat-array port on every host thread this job may use (node ranges per thread), on a
+    # node sample of >= 10x the 1-thread one and >= 40 nodes per thread: the strongest CPU
+    # number this repo can produce
+    threads, share_source = cpu_share()
+    nodes_mt = np.arange(min(max(10 * n_nodes, 40 * threads), layout.n_nodes))
     subs_mt = [fleet.subset_interval(a, nodes_mt, layout.zones) for a in intervals[:3]]
     _, sizes_mt, _ = subs_mt[0]
     o = Oracle(layout.zones, nodes=sizes_mt["n_nodes"], proc_slots=sizes_mt["n_procs"],
@@ -200,7 +229,7 @@ def cpu_baseline(layout, intervals, node_steps, n_nodes, seconds, max_runs=0):
     o.interval_mt(subs_mt[0][0], sizes_mt, threads)
     out["soa_mt"] = _median_rate(lambda k: o.interval_mt(subs_mt[1 + max(k, 0) % 2][0], sizes_mt, threads),
                                  sizes_mt["n_procs"], 5.0, max_runs=max_runs)
-    out["soa_mt"].update(threads=threads, procs=sizes_mt["n_procs"])
+    out["soa_mt"].update(threads=threads, procs=sizes_mt["n_procs"], share_source=share_source)
     return out, sizes
 
 
@@ -418,6 +447,74 @@ def pipeline_line(args, steps=10, warm=8):
             "terminated_last_interval": n_term, "intervals": steps,
             "note": "kacc_slot_join (reuse policy) -> kacc_tracker_add -> kacc_run_interval on one stream, "
                     "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device"}
+
+
+def host_path_line(args, steps=10):
+    """End-to-end, PCIe-inclusive: what a Go caller of calculatePower (monitor.go:399-431) sees
+    per interval through the cgo boundary.  The packer's output sits in two pinned batches
+    (kacc_batch_alloc); each interval is kacc_batch_submit (host layout check, H2D of the
+    interval's inputs on the context's copy stream, the interval kernel after an event) and
+    kacc_batch_wait, two batches in flight (submit B, wait A, ...) so one interval's copies
+    overlap the previous one's kernel.  Trusted: KACC_F_TRUSTED_LAYOUT (slots from
+    kacc_slot_join, no host check; the device range checks stay).  Beside it the PCIe ceiling:
+    a pinned -> device copy of the same bytes.  Reported beside the headline, never as `value`."""
+    import torch
+
+    from kepler_amd import accel, fleet
+
+    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes))
+    sizes = layout.sizes()
+    sim = fleet.FleetSim(layout, seed=fleet.SEED)
+    acc = accel.Accel(layout.zones, **layout.capacities())
+    ivs = [sim.next_interval() for _ in range(5)]
+    batches = [accel.HostBatch.alloc(acc, **sizes) for _ in range(2)]
+    nbytes = int(sum(v.nbytes for k, v in ivs[0].items() if k in accel.INTERVAL_ARRAYS and v is not None))
+    try:
+        batches[0].fill(ivs[0])  # first read (monitor.go:326-330), untimed
+        batches[0].submit()
+        batches[0].wait()
+
+        def pipelined(k):
+            t0 = time.perf_counter()
+            batches[0].submit()
+            for i in range(1, k):
+                batches[i % 2].submit()
+                batches[(i - 1) % 2].wait()
+            batches[(k - 1) % 2].wait()
+            return (time.perf_counter() - t0) / k
+
+        res = {}
+        for name, flags, first in (("checked", 0, 1), ("trusted", accel.KACC_F_TRUSTED_LAYOUT, 3)):
+            for b, a in zip(batches, ivs[first:first + 2]):
+                b.fill(a, flags)
+            pipelined(4)
+            res[name] = float(np.median([pipelined(steps) for _ in range(3)]))
+        src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        cps = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            cps.append(time.perf_counter() - t0)
+        t_copy = float(np.median(cps[1:]))
+        del src, dst
+    finally:
+        for b in batches:
+            b.free()
+        acc.close()
+    P, N = sizes["n_procs"], sizes["n_nodes"]
+    tp = res["trusted"]
+    return {"label": "END-TO-END (PCIe-inclusive; pinned host batches -> H2D -> interval kernel), not `value`",
+            "proc_attr_per_s": P / tp, "node_snapshots_per_s": N / tp, "ms_per_interval": tp * 1e3,
+            "checked_ms_per_interval": res["checked"] * 1e3, "checked_proc_attr_per_s": P / res["checked"],
+            "h2d_bytes_per_interval": nbytes,
+            "pcie_copy_ms": t_copy * 1e3, "pcie_copy_GBps": nbytes / t_copy / 1e9,
+            "frac_of_pcie_copy": t_copy / tp, "batches_in_flight": 2, "intervals": steps,
+            "note": "kacc_batch_submit / kacc_batch_wait, two pinned batches in flight; value: "
+                    "KACC_F_TRUSTED_LAYOUT (slots from kacc_slot_join), checked: with the host layout check; "
+                    "pcie_copy: torch pinned -> device copy of the same bytes (the ceiling)"}
 
 
 def bench_nodes(config, world, nodes=None, scaling="strong"):
@@ -690,6 +787,9 @@ def measure(args, w, rank, world, stream, comm_stream):
     else:  # kernels only: interval start -> end, partial sums start -> end
         kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
         totals_ms = [c.elapsed_time(d) for _, _, c, d in tevs]
+    if isinstance(handoff_ev, ctypes.c_void_p):  # the raw device-scope handoff event (ablation)
+        torch.cuda.synchronize()
+        lib.hipEventDestroy(handoff_ev)
     wall_t = torch.tensor([wall, wall_ev], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
@@ -862,9 +962,14 @@ def main():
             "runs": gf["runs"],
             "soa_port_1thread": res["soa"]["value"],
             "soa_port_threads": {"value": res["soa_mt"]["value"], "threads": res["soa_mt"]["threads"],
+                                 "threads_source": res["soa_mt"]["share_source"],
+                                 "usable_cores": hc["usable"],
                                  "runs": res["soa_mt"]["runs"],
                                  "sample": f"{res['soa_mt']['procs']} procs per run, median of "
-                                           f"{res['soa_mt']['runs']} runs"},
+                                           f"{res['soa_mt']['runs']} runs",
+                                 "note": "the flat-array C++ port over node ranges, one host thread per CPU this "
+                                         "job may use (threads_source); usable_cores is the whole host's "
+                                         "affinity mask, shared with the other GPUs' jobs"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
     w.close()
@@ -894,12 +999,27 @@ def main():
                                                        bytes_per_launch)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["slot_layouts"] = {"error": repr(e)}
+        sl_ = result["slot_layouts"]
+        if "join_steady_state_span" in sl_:  # the headline kernel on the layout production runs on
+            result["production_layout"] = {
+                "kernel_ms": sl_["join_steady_state_span"]["kernel_ms"],
+                "frac": sl_["join_steady_state_span"]["frac"],
+                "over_pristine": sl_["join_steady_state_over_pristine"],
+                "note": "the same kernel and algorithmic bytes on the slot words and spans kacc_slot_join "
+                        "(KACC_JOIN_REUSE_TERMINATED) returns after 40 intervals of 2 % /proc-shaped churn, "
+                        "timed on one context beside pristine slots (slot_layouts)"}
 
     if world == 1 and args.pipeline_line and args.fragment == 0 and args.config == 3 and K == 1 and not emulated:
         try:
             result["pipeline"] = pipeline_line(args)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["pipeline"] = {"error": repr(e)}
+
+    if world == 1 and args.host_line and args.fragment == 0 and args.config == 3 and K == 1 and not emulated:
+        try:
+            result["host_path"] = host_path_line(args)
+        except Exception as e:  # a secondary line: report, never lose the headline
+            result["host_path"] = {"error": repr(e)}
 
     if rank == 0:
         line = json.dumps(result)

@@ -661,7 +661,16 @@ void kacc_tracker_destroy(kacc_tracker *t); /* safe before or after kacc_destroy
 /* node_mask: DEVICE [nodes], nonzero = clear that node's tracker; NULL = all. */
 int kacc_tracker_clear(kacc_tracker *t, const uint32_t *node_mask, void *stream);
 /* m: the slot map whose kacc_slot_join produced term_key / term_slot /
- * term_count (device pointers); asynchronous on `stream`.                    */
+ * term_count (device pointers); asynchronous on `stream`.
+ * ORDERING: call it after that join and BEFORE the next kacc_run_interval (or
+ * kacc_run_intervals / kacc_batch_submit) of the same context, on the same
+ * stream or with an event the interval's stream waits for.  The frozen power
+ * of a terminated process / container / VM is derived (its stored ratio x its
+ * node's ActivePower, see kacc_table), and the next interval rewrites the
+ * node's ActivePower (and, under KACC_JOIN_REUSE_TERMINATED, the slots): a
+ * tracker that runs beside or after that interval freezes a wrong power.
+ * This is Go's own order: calculateProcessPower adds procs.Terminated
+ * (process.go:87-99) before it attributes the interval (:118-148).           */
 int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *term_key,
                      const uint32_t *term_slot, const uint32_t *term_count, void *stream);
 /* Items(): synchronous.  *count = tracked items of all nodes; when the arrays

@@ -607,7 +607,8 @@ int kacc_allreduce_exports(kacc_cluster *c, uint32_t n_ns, const uint32_t *const
     // 1. partial vectors of every shard from its exports
     const int rc = kacc_internal_export_partials(
         x, n_ns, n_ns ? ns_pod_off[s] : nullptr, n_ns ? ns_pod_row[s] : nullptr, n_ns ? pod_export[s] : nullptr,
-        n_ns ? n_pods[s] : 0, nodes ? node_export[s] : nullptr, nodes ? n_nodes[s] : 0, n_ns ? out_energy[s] : nullptr,
+        n_ns ? n_pods[s] : 0, nodes ? node_export[s] : nullptr, nodes ? n_nodes[s] : 0, nodes ? 1 : 0,
+        n_ns ? out_energy[s] : nullptr,
         n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr, b);
     if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
   }

@@ -2777,6 +2777,24 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 // order whichever block is last: reproducible f64 sums) into
 //   node_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal   (u64, modular)
 //   node_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower       (f64)
+//
+// The last-block handoff is NOT a C++-memory-model release/acquire pair: the
+// partials are published by relaxed agent-scope atomic exchanges and the block
+// counter by a relaxed agent-scope add.  It is correct on gfx950 (as on gfx942)
+// because of how that hardware executes them: an agent-scope atomic RMW is
+// performed at the device's coherence point beyond the XCD's L2 (sc1), and its
+// RETURNED value only arrives once it has been performed — every lane waits for
+// its exchange's old value before the barrier that precedes thread 0's count,
+// so all partials are performed before the count is; the last block then drops
+// its XCD's L2 (acquire fence) and reads them with agent-scope atomic loads.  A
+// release fetch_add on the counter would make it portable, at the cost of an L2
+// write-back (buffer_wbl2) in every node block: the __threadfence pair that
+// cost 2.2 us of the partial sums (profiles/r03/tprobe).  The build refuses any
+// other target; tests/test_gpu_cluster.py::test_cluster_node_totals_back_to_back_launches
+// pins it over 24 back-to-back launches with changing node data.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "cluster_partials_kernel's last-block handoff is written for gfx950's agent-scope atomics"
+#endif
 constexpr uint32_t kNodeBlocksMax = 64;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
@@ -3494,7 +3512,11 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   const kacc::TimingScope timing(ctx);
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
-  if (rc != KACC_OK || b->n_nodes == 0) return rc;
+  if (rc != KACC_OK) return rc;
+  if (b->n_nodes == 0) {  // an emptied batch: no node of it counts in the cluster totals
+    ctx->live_nodes = 0;
+    return KACC_OK;
+  }
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
@@ -3955,13 +3977,14 @@ int kacc_namespace_totals(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, con
 int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
                                    uint64_t *out_energy, double *out_power, uint64_t *node_energy, double *node_power,
                                    void *stream) {
-  return kacc_internal_export_partials(ctx, n_ns, off, slots, nullptr, 0, nullptr, 0, out_energy, out_power,
+  return kacc_internal_export_partials(ctx, n_ns, off, slots, nullptr, 0, nullptr, 0, 0, out_energy, out_power,
                                        node_energy, node_power, stream);
 }
 
 int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *rows,
                                   const uint64_t *pod_export, uint64_t n_pods, const uint64_t *node_export,
-                                  uint64_t n_nodes, uint64_t *out_energy, double *out_power, uint64_t *node_energy,
+                                  uint64_t n_nodes, int from_exports, uint64_t *out_energy, double *out_power,
+                                  uint64_t *node_energy,
                                   double *node_power, void *stream) {
   if (!ctx) return KACC_EINVAL;
   const kacc::TimingScope timing(ctx);
@@ -3971,8 +3994,10 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   const uint64_t Z = ctx->cfg.zones;
   // the nodes of the last interval run on the context (a node that left the
   // batch stops exporting, so PromQL's sum drops it; a fresh context sums none);
-  // from an export: its n_nodes rows
-  const uint64_t live = node_export ? n_nodes : std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
+  // from an export: its n_nodes rows (an empty shard's export: none, never the
+  // tables' stale nodes)
+  if (from_exports && n_nodes && !node_export) return fail(ctx, KACC_EINVAL, "node export is NULL");
+  const uint64_t live = from_exports ? n_nodes : std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
   const uint32_t *slots = rows;
   // at most kNodeBlocksMax blocks of a multiple of kBlock nodes each
   const uint64_t groups = (live + kacc::kBlock - 1) / kacc::kBlock;
@@ -4158,7 +4183,11 @@ int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, 
   if (!ctx) return KACC_EINVAL;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
-  if (rc != KACC_OK || b->n_nodes == 0) return rc;
+  if (rc != KACC_OK) return rc;
+  if (b->n_nodes == 0) {  // an emptied batch: no node of it counts in the cluster totals
+    ctx->live_nodes = 0;
+    return KACC_OK;
+  }
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call

@@ -134,11 +134,13 @@ extern "C" int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, cons
                                               uint64_t *node_energy, double *node_power, void *stream);
 
 // The same from an interval's exports (kacc_interval.pod_export / node_export):
-// namespace k sums the export rows rows[off[k] .. off[k+1]) (< n_pods), node
-// totals over the export's n_nodes rows (node_export NULL: the tables, as above).
+// namespace k sums the export rows rows[off[k] .. off[k+1]) (< n_pods); with
+// from_exports the node totals sum the export's n_nodes rows (n_nodes 0: zeros,
+// node_export may be NULL), else the tables' live nodes, as above.
 extern "C" int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *rows,
                                              const uint64_t *pod_export, uint64_t n_pods,
-                                             const uint64_t *node_export, uint64_t n_nodes, uint64_t *out_energy,
+                                             const uint64_t *node_export, uint64_t n_nodes, int from_exports,
+                                             uint64_t *out_energy,
                                              double *out_power, uint64_t *node_energy, double *node_power,
                                              void *stream);
 

@@ -140,3 +140,21 @@ def test_bad_arguments_do_not_crash(lib):
     assert b"zones" in lib.kacc_last_error(None)
     assert lib.kacc_reset(None) == accel.KACC_EINVAL
     assert lib.kacc_run_interval(None, None, None) == accel.KACC_EINVAL
+
+
+def test_loopback_collectives_export_what_the_engine_binds():
+    """tests/c/loopback_rccl.cpp (the two-rank cluster test's stand-in for RCCL, loaded via
+    KACC_RCCL_PATH) exports every entry point kacc_cluster.hip dlsym()s."""
+    import ctypes
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "c")], check=True)
+    lib = ctypes.CDLL(os.path.join(root, "tests", "c", "build", "libkacc_loopback_rccl.so"))
+    with open(os.path.join(root, "kepler_amd", "csrc", "kacc_cluster.hip")) as f:
+        names = re.findall(r'sym\(r\.\w+, "(nccl\w+)"\)', f.read())
+    assert len(names) == 11
+    for n in names:
+        assert hasattr(lib, n), n
+    v = ctypes.c_int()
+    assert lib.ncclGetVersion(ctypes.byref(v)) == 0 and v.value // 10000 == 2

@@ -376,6 +376,54 @@ def test_cluster_node_totals_follow_the_live_nodes():
     np.testing.assert_array_equal(e, we)
     np.testing.assert_allclose(p, wp, rtol=1e-12, atol=0)
     assert not np.array_equal(we, want(L.n_nodes)[0])  # the 3 nodes that left counted before
+    # the batch empties: no node counts any more (the early return of an empty
+    # kacc_run_interval re-arms the live-node count too)
+    acc.run_interval(accel.KaccInterval(), s)
+    acc.sync(s)
+    e, p = totals()
+    assert not e.any() and not p.any()
+    cl.close()
+    acc.close()
+
+
+def test_cluster_node_totals_back_to_back_launches():
+    """The cluster node totals' last-block handoff (cluster_partials_kernel: per-block partials
+    published by device-scope atomic exchanges, the last block acquires and adds them) pinned
+    under back-to-back launches with no host sync: 24 intervals of changing node data, each
+    followed by its partial sums into its own row, 40 node blocks per launch.  A partial of an
+    earlier launch read by the last block would show as a stale total."""
+    from oracle.oracle import Oracle
+
+    n, Z, K = 20000, 2, 24
+    L = fleet.make_layout(n, [3, 1, 0, 2, 5], Z, seed=21, n_namespaces=1)
+    acc = accel.Accel(Z, **L.capacities())
+    ora = Oracle(Z, **L.capacities())
+    sim = fleet.FleetSim(L, seed=21, read_error_frac=0.02)
+    s = current_stream_handle()
+    cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
+    ne = torch.zeros(K, 2 * Z, dtype=torch.int64, device="cuda")
+    npw = torch.zeros(K, 3 * Z, dtype=torch.float64, device="cuda")
+    want_e, want_p, keep = [], [], []
+    for k in range(K):
+        a = sim.next_interval()
+        t = to_device(a)
+        keep.append(t)
+        acc.run_interval(interval_from_tensors(t, L.sizes(), L.fast_flag()), s)
+        cl.partials(0, None, None, None, None, [ne[k].data_ptr()], [npw[k].data_ptr()], streams=[s])
+        ora.interval(a, L.sizes())
+        st = {x: ora.state[x].reshape(-1, Z) for x in ("node_active_total", "node_idle_total", "node_power",
+                                                       "node_active_power", "node_idle_power")}
+        want_e.append(np.concatenate([st[x].sum(axis=0, dtype=np.uint64)
+                                      for x in ("node_active_total", "node_idle_total")]))
+        want_p.append(np.concatenate([st[x].sum(axis=0) for x in ("node_power", "node_active_power",
+                                                                  "node_idle_power")]))
+    acc.sync(s)
+    got_e = ne.cpu().numpy().view(np.uint64)
+    got_p = npw.cpu().numpy()
+    for k in range(K):
+        np.testing.assert_array_equal(got_e[k], want_e[k], err_msg=f"interval {k}")
+        np.testing.assert_allclose(got_p[k], want_p[k], rtol=1e-12, atol=0, err_msg=f"interval {k}")
+    assert len({tuple(x) for x in want_e}) == K  # the data did change every interval
     cl.close()
     acc.close()
 

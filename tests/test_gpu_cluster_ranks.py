@@ -1,0 +1,132 @@
+"""The cluster path with nranks > 1 — two processes on the box's one GPU — MI355X only.
+
+Each rank is a process (tests/cluster_rank_worker.py) that owns one node shard of a fleet,
+joins the cluster with kacc_cluster_join(nranks = 2, rank) and runs the library's cross-rank
+calls: kacc_cluster_partials per interval + ONE kacc_allreduce_sums, kacc_allreduce_namespaces
+and kacc_gather_pods (count all-gather, then one broadcast per rank).  RCCL refuses two ranks
+on one GPU ("Duplicate GPU detected"), so the collectives come from the loopback stand-in
+tests/c/loopback_rccl.cpp, loaded through KACC_RCCL_PATH (kacc_cluster.hip): what runs is the
+library's rank logic — communicator init with real peers, the gather-v offsets and the
+per-rank broadcast order — with host-staged sums in rank order.  Checked against the
+unsharded oracle: namespace and cluster node totals u64 exact and f64 <= 1e-12 relative
+(north star), the K-interval rows bit-identical to the one-call totals, the gathered pods
+bit-exact in (rank, pod) order, on both ranks.  Reference grouping: Pod.Namespace,
+/root/reference/internal/resource/types.go:106-110 (namespace totals are this repo's
+north-star extension; Kepler leaves them to PromQL).
+"""
+
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "cluster_rank_worker.py")
+LOOPBACK = os.path.join(ROOT, "tests", "c", "build", "libkacc_loopback_rccl.so")
+
+
+def _run_ranks(tmp_path, nranks, rccl_path):
+    env = dict(os.environ)
+    env.pop("KACC_RCCL_PATH", None)
+    if rccl_path:
+        env["KACC_RCCL_PATH"] = rccl_path
+    env["KACC_LOOPBACK_TIMEOUT_S"] = "90"
+    procs = [subprocess.Popen([sys.executable, "-u", WORKER, str(r), str(nranks), str(tmp_path)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(nranks)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=200)
+            outs.append(out)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return [p.returncode for p in procs], outs
+
+
+def _oracle(nranks):
+    """The unsharded fleet through the oracle: per interval namespace and node totals, and the
+    last interval's pod tables in fleet pod order."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import cluster_rank_worker as w
+    from kepler_amd import fleet
+    from oracle.oracle import Oracle
+
+    kw = dict(w.FLEET)
+    L = fleet.make_layout(kw.pop("n_nodes"), kw.pop("procs_per_node"), kw.pop("zones"), **kw)
+    ora = Oracle(L.zones, **L.capacities())
+    sim = fleet.FleetSim(L, **w.SIM)
+    Z = L.zones
+    per = []
+    for _ in range(w.INTERVALS):
+        ora.interval(sim.next_interval(), L.sizes())
+        e, p = ora.namespace_totals(*L.namespace_csr())
+        st = ora.state
+        ne = np.concatenate([st[t].reshape(-1, Z).sum(axis=0, dtype=np.uint64)
+                             for t in ("node_active_total", "node_idle_total")])
+        npw = np.concatenate([st[t].reshape(-1, Z).sum(axis=0)
+                              for t in ("node_power", "node_active_power", "node_idle_power")])
+        per.append((e, p, ne, npw))
+    pe = ora.state["pod_energy"].reshape(-1, Z)[L.pod_slot].reshape(-1)
+    pp = ora.state["pod_power"].reshape(-1, Z)[L.pod_slot].reshape(-1)
+    return L, per, pe, pp
+
+
+def test_two_ranks_one_gpu_loopback_collectives(tmp_path):
+    assert os.path.exists(LOOPBACK), "build() makes tests/c/build/libkacc_loopback_rccl.so"
+    nranks = 2
+    rcs, outs = _run_ranks(tmp_path, nranks, LOOPBACK)
+    assert rcs == [0] * nranks, "\n".join(f"--- rank {r} rc={rc}\n{o[-4000:]}" for r, (rc, o) in
+                                          enumerate(zip(rcs, outs)))
+    L, per, want_pe, want_pp = _oracle(nranks)
+    Z, n_ns = L.zones, L.n_namespaces
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(nranks)]
+    his = []
+    for r, d in enumerate(res):
+        assert tuple(d["info"]) == (nranks, r, 1)  # a real peer: nranks 2, this rank, one shard
+        assert "libkacc_loopback_rccl" in str(d["rccl"])
+        his.append((int(d["lo"]), int(d["hi"])))
+        # K intervals' rows reduced by ONE kacc_allreduce_sums
+        for k, (e, p, ne, npw) in enumerate(per):
+            te, tp = d["te"][k], d["tp"][k]
+            np.testing.assert_array_equal(te[:n_ns * Z], e, err_msg=f"rank {r} interval {k} namespace energy")
+            np.testing.assert_allclose(tp[:n_ns * Z], p, rtol=1e-12, atol=0, err_msg=f"rank {r} interval {k}")
+            np.testing.assert_array_equal(te[n_ns * Z:], ne, err_msg=f"rank {r} interval {k} node energy")
+            np.testing.assert_allclose(tp[n_ns * Z:], npw, rtol=1e-12, atol=0, err_msg=f"rank {r} interval {k}")
+        # the one-call entry point == the last interval's reduced row, bit for bit
+        np.testing.assert_array_equal(d["oe"], d["te"][-1][:n_ns * Z])
+        np.testing.assert_array_equal(d["op"].view(np.uint64), d["tp"][-1][:n_ns * Z].view(np.uint64))
+        np.testing.assert_array_equal(d["ne"], d["te"][-1][n_ns * Z:])
+        np.testing.assert_array_equal(d["npw"].view(np.uint64), d["tp"][-1][n_ns * Z:].view(np.uint64))
+        # every pod of the cluster, in (rank, pod) order = the fleet's pod order
+        assert int(d["total"]) == L.n_pods
+        np.testing.assert_array_equal(d["ge"], want_pe, err_msg=f"rank {r} gathered pod energy")
+        np.testing.assert_array_equal(d["gp"].view(np.uint64), want_pp.view(np.uint64),
+                                      err_msg=f"rank {r} gathered pod power")
+    # the ranks cover the fleet in order, and both hold the same cluster result
+    assert his[0][0] == 0 and his[0][1] == his[1][0] and his[-1][1] == L.n_nodes
+    assert [int(res[r]["first"][0]) for r in range(nranks)] == [int(L.pod_off[lo]) for lo, _ in his]
+    for key in ("te", "tp", "ge", "gp"):
+        np.testing.assert_array_equal(res[0][key].view(np.uint64), res[1][key].view(np.uint64))
+    assert np.count_nonzero(per[-1][0]) > 0 and np.count_nonzero(per[-1][1]) > 0
+
+
+def test_two_ranks_one_gpu_system_rccl_refuses_or_agrees(tmp_path):
+    """The system RCCL with the same two processes: it refuses two ranks on one GPU at init
+    ("Duplicate GPU detected", the reason for the loopback above) — or, if a future RCCL
+    accepts them, it must give the same results."""
+    rcs, outs = _run_ranks(tmp_path, 2, None)
+    if rcs != [0, 0]:
+        text = "\n".join(outs)
+        assert "ncclCommInitRank" in text, text[-4000:]
+        pytest.skip("system RCCL refuses two ranks on one GPU: " +
+                    next((ln for ln in text.splitlines() if "ncclCommInitRank" in ln), "")[:300])
+    d = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    for key in ("te", "tp", "ge", "gp"):
+        np.testing.assert_array_equal(d[0][key].view(np.uint64), d[1][key].view(np.uint64))

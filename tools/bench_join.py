@@ -89,20 +89,25 @@ def main():
         e0.record()
         join(k)
         e1.record()
-        acc.run_interval(it, stream)
-        e2.record()
+        # the tracker reads the terminated slots' final values (power derived from their
+        # node's ActivePower) BEFORE the interval rewrites them: process.go:87-99 then :118-148
         if s % 2:  # an export every other interval: Clear() first (process.go:80-84)
             tr.clear(stream)
         track()
+        e2.record()
+        acc.run_interval(it, stream)
         e3.record()
         e3.synchronize()
         tj.append(e0.elapsed_time(e1))
-        tall.append(e0.elapsed_time(e2))
-        ttr.append(e2.elapsed_time(e3))
+        tall.append(e0.elapsed_time(e1) + e2.elapsed_time(e3))  # join + interval
+        ttr.append(e1.elapsed_time(e2))
         tseq.append(e0.elapsed_time(e3))
     acc.sync(stream)
-    # the same pipeline with the tracker on a second stream beside the interval
-    # kernel (it reads only terminated slots, which the interval never writes)
+    # the same pipeline with the tracker on a second stream: it must read the
+    # terminated slots' final values before the interval (a terminated process's
+    # power is derived from its node's ActivePower, which the interval rewrites;
+    # kacc_tracker_add's ordering rule), so the interval waits for it — the second
+    # stream only moves the clear/add launches off the join's stream
     s2 = torch.cuda.Stream()
     tpipe = []
     for s in range(steps):
@@ -115,11 +120,11 @@ def main():
         join(k)
         joined.record()
         s2.wait_event(joined)
-        acc.run_interval(it, stream)
         if s % 2:
             tr.clear(s2.cuda_stream)
         tr.add(sm, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), s2.cuda_stream)
         torch.cuda.current_stream().wait_stream(s2)
+        acc.run_interval(it, stream)
         e3.record()
         e3.synchronize()
         tpipe.append(e0.elapsed_time(e3))
