@@ -12,6 +12,11 @@ extern "C" {
  * 9 = 1|8.  Variants != 0 do not compute the reference semantics.          */
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream, int variant);
 
+/* interval_kernel (Z = 4) with per-workgroup real-time stamps into d_out
+ * [grid][8] u64: start, rows staged, attribution start, end, XCC_ID, HW_ID, block,
+ * 0 (s_memrealtime ticks, 100 MHz; diagnostic, results are the reference's).  */
+int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *dev_batch, void *stream, uint64_t *d_out);
+
 /* Per-wave s_memtime phase totals of the carry kernel (Z = 2; variant 0 or 2) into
  * d_out[n_nodes][8][8] (diagnostic; results are the reference's).             */
 int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *batches, uint32_t count, void *stream,

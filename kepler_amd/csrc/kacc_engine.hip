@@ -67,6 +67,11 @@ constexpr int kVarNoSweep = 2048;      // never sweep the node's slot span (row 
 constexpr int kVarNtAgg = 4096;        // non-temporal stores for the aggregate rows too (round 2)
 constexpr int kVarNtScatter = 8192;    // non-temporal per-row scattered process stores (round 2)
 constexpr int kVarTemporalLoads = 16384;  // plain loads of the streamed inputs and prev totals
+// per-workgroup real-time stamps into DevState::stamps (diagnostic; results are
+// the reference's): [blk][8] = start, rows staged (first barrier), attribution
+// start, end (after a final barrier), XCC_ID, HW_ID, node, 0 — in s_memrealtime
+// ticks (100 MHz, one clock for the whole device)
+constexpr int kVarStamps = 131072;
 // KACC_LATE_AGG: interval_kernel loads the aggregates' previous totals and stores
 // their rows AFTER the process pass (1, round 3) or before it (0, rounds 1-2).
 // Early aggregate rows sit dirty in L2 through the whole process stream and
@@ -188,6 +193,7 @@ struct DevState {
   // the chunk items are generated once (items_kernel) and reused, so the node
   // phase skips them; pod_kernel keeps the list for the next interval
   uint32_t items_given, keep_items;
+  uint64_t *stamps;  // kVarStamps only
 };
 
 struct NodeShared {
@@ -714,6 +720,16 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   __shared__ uint16_t s_inv[kRowsLds];  // slot sweep: slot - smin -> row (0xffff: none)
 
   const int tid = threadIdx.x;
+  constexpr bool kStamp = (V & kVarStamps) != 0;
+  uint64_t *stamp = kStamp ? st.stamps + static_cast<uint64_t>(blk) * 8 : nullptr;
+  if constexpr (kStamp) {
+    if (tid == 0) {
+      stamp[0] = __builtin_amdgcn_s_memrealtime();
+      stamp[4] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      stamp[5] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      stamp[6] = blk;
+    }
+  }
   // the previous interval's pod_kernel has drained the deferred list; this
   // interval's chunk_kernel refills it after this kernel
   if (blk == 0 && tid == 0) st.defer_ctr[0] = 0u;
@@ -900,6 +916,9 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     }
   }
   __syncthreads();
+  if constexpr (kStamp) {
+    if (tid == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+  }
   if (swept) {  // inverse map (s_inv was reset before the barrier; read at E, >= 1 barrier later)
 #pragma unroll
     for (int k = 0; k < kRowsPerThread; ++k) {
@@ -981,6 +1000,9 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
 
   // ---- E: attribution ------------------------------------------------------------
   const Attr<Z> a = make_attr<Z>(sh, b.flags);
+  if constexpr (kStamp) {
+    if (tid == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
+  }
   if (tid == 0) {  // node scalars of the new snapshot
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
@@ -1052,6 +1074,10 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     }
   }
   if constexpr (kLateAgg<V>) aggregate_out();
+  if constexpr (kStamp) {
+    __syncthreads();
+    if (tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 template <int Z, int V>
@@ -3064,6 +3090,7 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.defer_cap = ctx->defer_cap;
   s.items_given = 0;
   s.keep_items = 0;
+  s.stamps = nullptr;
   return s;
 }
 
@@ -4179,6 +4206,24 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint
 
 // Internal (kacc_debug.h): timing ablations of the interval kernel.  A variant
 // other than 0 does NOT compute the reference semantics.
+int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *b, void *stream, uint64_t *d_out) {
+  if (!ctx || !d_out) return KACC_EINVAL;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = check_shape(ctx, b);
+  if (rc != KACC_OK) return rc;
+  if (ctx->cfg.zones != 4) return fail(ctx, KACC_EINVAL, "stamps are built for Z = 4");
+  if (b->n_nodes == 0) return KACC_OK;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
+  (void)hipGetLastError();
+  kacc::DevState ds = dev_state(ctx);
+  ds.stamps = d_out;
+  launch_zv<4, kacc::kVarStamps>(*b, ds, st);
+  KACC_HIP(ctx, hipGetLastError());
+  ctx->live_nodes = b->n_nodes;
+  return KACC_OK;
+}
+
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, int variant) {
   if (!ctx) return KACC_EINVAL;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
