@@ -217,6 +217,32 @@ __device__ __forceinline__ double uniform_f64(double x) {
 }
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 
+// Experiments (timing A/B only; results are identical): KACC_WT_PROC writes the
+// non-temporal row stores through the L2 (sc0 sc1 nt: no dirty line is left for
+// the end-of-kernel write-back), KACC_WT_AGG the aggregate rows likewise.
+#ifndef KACC_WT_PROC
+#define KACC_WT_PROC 0
+#endif
+#ifndef KACC_WT_AGG
+#define KACC_WT_AGG 0
+#endif
+template <typename T>
+__device__ __forceinline__ void wt_store(T v, T *p) {
+  if constexpr (sizeof(T) == 16)
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (sizeof(T) == 8)
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  else
+    asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+}
+template <typename T>
+__device__ __forceinline__ void nt_store(T v, T *p) {
+  if constexpr (KACC_WT_PROC != 0)
+    wt_store(v, p);
+  else
+    __builtin_nontemporal_store(v, p);
+}
+
 template <int Z>
 __device__ __forceinline__ void load_row(const uint64_t *__restrict__ base, uint64_t s,
                                          uint64_t (&out)[Z]) {
@@ -264,7 +290,7 @@ __device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, cons
       x.x = in[2 * k];
       x.y = in[2 * k + 1];
       if constexpr (NT)
-        __builtin_nontemporal_store(x, p + k);
+        nt_store(x, p + k);
       else
         p[k] = x;
     }
@@ -272,7 +298,7 @@ __device__ __forceinline__ void store_row(T *__restrict__ base, uint64_t s, cons
 #pragma unroll
     for (int z = 0; z < Z; ++z) {
       if constexpr (NT)
-        __builtin_nontemporal_store(in[z], base + s * Z + z);
+        nt_store(in[z], base + s * Z + z);
       else
         base[s * Z + z] = in[z];
     }
@@ -374,8 +400,8 @@ __device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const
                                            uint32_t node, bool wnode) {
   store_row<Z, NT, uint64_t>(st.proc_energy, s, E);
   if constexpr (NT) {
-    __builtin_nontemporal_store(ratio, st.proc_ratio + s);
-    if (wnode) __builtin_nontemporal_store(node, st.proc_node + s);
+    nt_store(ratio, st.proc_ratio + s);
+    if (wnode) nt_store(node, st.proc_node + s);
   } else {
     st.proc_ratio[s] = ratio;
     if (wnode) st.proc_node[s] = node;
@@ -425,9 +451,38 @@ __device__ __forceinline__ void export_node_zone(const kacc_interval &b, uint32_
 // An aggregate row's outputs at slot s: energy totals; for a pod its powers,
 // for a container / VM its ratio and node (their power is derived on read as
 // a process's: the same guard, container.go:106-140, vm.go:78-109).
+template <int Z, typename T>
+__device__ __forceinline__ void wt_row(T *__restrict__ base, uint64_t s, const T (&in)[Z]) {
+  if constexpr (Z % 2 == 0) {
+    using v2 = __attribute__((ext_vector_type(2))) T;
+    v2 *p = reinterpret_cast<v2 *>(base + s * Z);
+#pragma unroll
+    for (int k = 0; k < Z / 2; ++k) {
+      v2 x;
+      x.x = in[2 * k];
+      x.y = in[2 * k + 1];
+      wt_store(x, p + k);
+    }
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) wt_store(in[z], base + s * Z + z);
+  }
+}
+
 template <int Z, bool NT>
 __device__ __forceinline__ void store_agg(const DevState &st, uint32_t role, uint64_t s, const uint64_t (&E)[Z],
                                           const double (&P)[Z], double ratio, uint32_t node) {
+  if constexpr (KACC_WT_AGG != 0 && !NT) {
+    if (role == 3) {
+      wt_row<Z, uint64_t>(st.pod_energy, pod_row(s), E);
+      wt_row<Z, double>(st.pod_power, pod_row(s), P);
+      return;
+    }
+    wt_row<Z, uint64_t>(role == 1 ? st.ctr_energy : st.vm_energy, s, E);
+    wt_store(ratio, (role == 1 ? st.ctr_ratio : st.vm_ratio) + s);
+    wt_store(node, (role == 1 ? st.ctr_node : st.vm_node) + s);
+    return;
+  }
   if (role == 3) {
     store_row<Z, NT, uint64_t>(st.pod_energy, pod_row(s), E);
     store_row<Z, NT, double>(st.pod_power, pod_row(s), P);
@@ -437,8 +492,8 @@ __device__ __forceinline__ void store_agg(const DevState &st, uint32_t role, uin
   double *r = role == 1 ? st.ctr_ratio : st.vm_ratio;
   uint32_t *nd = role == 1 ? st.ctr_node : st.vm_node;
   if constexpr (NT) {
-    __builtin_nontemporal_store(ratio, r + s);
-    __builtin_nontemporal_store(node, nd + s);
+    nt_store(ratio, r + s);
+    nt_store(node, nd + s);
   } else {
     r[s] = ratio;
     nd[s] = node;
@@ -555,14 +610,14 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
     ev.x = E[0];
     ev.y = E[1];
     if constexpr (NT)
-      __builtin_nontemporal_store(ev, pe + piece);
+      nt_store(ev, pe + piece);
     else
       pe[piece] = ev;
     if (zp == 0) {  // the slot's ratio and node: contiguous across the group's lanes
       const bool wnode = !a.keep_node || is_new;
       if constexpr (NT) {
-        __builtin_nontemporal_store(ratio, ratio_tab + s0 + idx);
-        if (wnode) __builtin_nontemporal_store(node, node_tab + s0 + idx);
+        nt_store(ratio, ratio_tab + s0 + idx);
+        if (wnode) nt_store(node, node_tab + s0 + idx);
       } else {
         ratio_tab[s0 + idx] = ratio;
         if (wnode) node_tab[s0 + idx] = node;
@@ -2796,7 +2851,7 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 }
 
 // Cluster partial sums of one context in ONE launch (kacc_allreduce_namespaces):
-// blocks [0, ns_blocks) are namespace_kernel's; the others reduce the node
+// the last ns_blocks blocks are namespace_kernel's; the first ones reduce the node
 // tables — block b sums nodes [b·npb, (b+1)·npb) (lane l: nodes l, l+256, …,
 // then the wave trees and the four waves in order) into partials[b]; the last
 // block to finish adds the ≤ kNodeBlocksMax partials in block order (a fixed
@@ -2822,8 +2877,17 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 #error "cluster_partials_kernel's last-block handoff is written for gfx950's agent-scope atomics"
 #endif
 constexpr uint32_t kNodeBlocksMax = 64;
+// Column mode (n_nodes <= kColumnMaxNodes): one block per output value — block c
+// sums column c (table c / Z, zone c % Z) over every node (lane l: nodes l, l+256,
+// ... in order, kColLoads loads in flight, then the wave tree and the four waves
+// in order) and writes it: no cross-block combine, so no partial exchange, block
+// count or last-block reload (four dependent round trips -> one or two: the 1/8
+// shard of config 3 has 1,250 nodes = five loads per lane).
+constexpr uint32_t kColumnMaxNodes = 8192;
+constexpr int kColLoads = 8;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
+  uint32_t columns;   // 1: column mode (5Z blocks, one output value each)
   uint32_t npb;       // nodes per block (a multiple of kBlock)
   const uint64_t *active_total, *idle_total;
   const double *power, *active_power, *idle_power;
@@ -2842,15 +2906,67 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
                                                                   const double *__restrict__ pp, uint64_t pod_slots,
                                                                   uint64_t *out_e, double *out_p, uint32_t *err,
                                                                   const NodeTotalsArgs na) {
-  if (blockIdx.x < ns_blocks) {
-    namespace_block<Z, kW>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+  // the node blocks come FIRST: their chain (loads, partial exchange, count, the last
+  // block's sums) is the longer one, and dispatched after the namespace blocks it
+  // started last (1/8 shard of config 3: namespace sums alone 5.2 us, node totals
+  // alone 6.5 us, both 9.3 us with the node blocks last; profiles/r03/tprobe2)
+  const uint32_t nb = gridDim.x - ns_blocks;
+  if (blockIdx.x >= nb) {
+    namespace_block<Z, kW>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
     return;
   }
   constexpr int kV = 5 * Z;
   __shared__ uint64_t s_w[kBlock / 64][kV];
   __shared__ uint64_t s_part[kNodeBlocksMax * kV];
   __shared__ uint32_t s_last;
-  const uint32_t tid = threadIdx.x, b = blockIdx.x - ns_blocks, nb = gridDim.x - ns_blocks;
+  const uint32_t tid = threadIdx.x, b = blockIdx.x;
+  if (na.columns) {  // block b owns output value b: column b / Z of the five, zone b % Z
+    const uint32_t t = b / Z, z = b % Z;
+    const bool is_u64 = t < 2;
+    const uint64_t *col = na.node_export ? na.node_export + t * Z + z
+                          : t == 0 ? na.active_total + z
+                          : t == 1 ? na.idle_total + z
+                          : reinterpret_cast<const uint64_t *>(t == 2 ? na.power : t == 3 ? na.active_power
+                                                                                          : na.idle_power) + z;
+    const uint64_t stride = na.node_export ? 5ull * Z : static_cast<uint64_t>(Z);
+    unsigned long long e = 0;
+    double p = 0.0;
+    for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kColLoads) {
+      uint64_t v[kColLoads];
+#pragma unroll
+      for (int u = 0; u < kColLoads; ++u) {  // unconditional from clamped nodes: all in flight
+        const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
+        v[u] = col[n * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < kColLoads; ++u) {
+        if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
+        if (is_u64)
+          e += v[u];
+        else
+          p = p + __longlong_as_double(static_cast<long long>(v[u]));
+      }
+    }
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) {
+      e += __shfl_down(e, sft, 64);
+      p = p + __shfl_down(p, sft, 64);
+    }
+    if ((tid & 63u) == 0) s_w[tid >> 6][0] = is_u64 ? e : static_cast<uint64_t>(__double_as_longlong(p));
+    __syncthreads();
+    if (tid == 0) {
+      if (is_u64) {
+        unsigned long long r = s_w[0][0];
+        for (int w = 1; w < kBlock / 64; ++w) r += s_w[w][0];
+        na.out_e[t * Z + z] = r;
+      } else {
+        double r = __longlong_as_double(static_cast<long long>(s_w[0][0]));
+        for (int w = 1; w < kBlock / 64; ++w) r = r + __longlong_as_double(static_cast<long long>(s_w[w][0]));
+        na.out_p[(t - 2) * Z + z] = r;
+      }
+    }
+    return;
+  }
   unsigned long long ve[2 * Z];
   double vp[3 * Z];
 #pragma unroll
@@ -4026,13 +4142,18 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   if (from_exports && n_nodes && !node_export) return fail(ctx, KACC_EINVAL, "node export is NULL");
   const uint64_t live = from_exports ? n_nodes : std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
   const uint32_t *slots = rows;
-  // at most kNodeBlocksMax blocks of a multiple of kBlock nodes each
+  // up to kColumnMaxNodes nodes: one block per output value (no cross-block
+  // combine); more: at most kNodeBlocksMax blocks of a multiple of kBlock nodes
+  // each and the last-block combine
+  const bool columns = live <= kacc::kColumnMaxNodes;
   const uint64_t groups = (live + kacc::kBlock - 1) / kacc::kBlock;
   const uint32_t npb = static_cast<uint32_t>(
       kacc::kBlock * std::max<uint64_t>(1, (groups + kacc::kNodeBlocksMax - 1) / kacc::kNodeBlocksMax));
-  // no live node: one block that writes zero totals
-  const uint32_t node_blocks = node_energy ? std::max<uint32_t>(1, static_cast<uint32_t>((live + npb - 1) / npb)) : 0u;
-  if (node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
+  // no live node: blocks that write zero totals
+  const uint32_t node_blocks = !node_energy ? 0u
+                               : columns    ? static_cast<uint32_t>(5 * Z)
+                                            : std::max<uint32_t>(1, static_cast<uint32_t>((live + npb - 1) / npb));
+  if (!columns && node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
     KACC_HIP(ctx, hipStreamSynchronize(st));
     if (ctx->d_node_part) KACC_HIP(ctx, hipFree(ctx->d_node_part));
     ctx->d_node_part = nullptr;
@@ -4043,6 +4164,7 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   }
   kacc::NodeTotalsArgs na{};
   na.n_nodes = live;
+  na.columns = columns ? 1u : 0u;
   na.npb = npb;
   na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
   na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];

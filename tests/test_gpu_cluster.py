@@ -395,7 +395,7 @@ def test_cluster_node_totals_back_to_back_launches():
     from oracle.oracle import Oracle
 
     n, Z, K = 20000, 2, 24
-    L = fleet.make_layout(n, [3, 1, 0, 2, 5], Z, seed=21, n_namespaces=1)
+    L = fleet.make_layout(n, [3, 1, 0, 2, 5] * (n // 5), Z, seed=21, n_namespaces=1)
     acc = accel.Accel(Z, **L.capacities())
     ora = Oracle(Z, **L.capacities())
     sim = fleet.FleetSim(L, seed=21, read_error_frac=0.02)
