@@ -134,6 +134,10 @@ constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node 
 #ifndef KACC_CHUNK_WAVES
 #define KACC_CHUNK_WAVES 4
 #endif
+#ifndef KACC_CHUNK_LATE_PREV
+#define KACC_CHUNK_LATE_PREV 0
+#endif
+constexpr bool kChunkLatePrev = KACC_CHUNK_LATE_PREV != 0;
 constexpr int kChunkThreads = KACC_CHUNK_THREADS;
 constexpr int kChunkRpt = 4;
 constexpr int kChunkRows = kChunkRpt * kChunkThreads;  // big-node rows per chunk item
@@ -153,6 +157,8 @@ constexpr uint32_t kErrSlot = 1u << 2;
 constexpr uint32_t kErrNs = 1u << 3;
 constexpr uint32_t kErrCapacity = 1u << 4;
 constexpr uint32_t kErrBigNode = 1u << 5;  // oversized node under KACC_F_FAST_NODES
+constexpr uint32_t kErrFused = 1u << 9;    // fused partial sums not done within kFusedMaxSpins (never seen)
+constexpr uint32_t kFusedMaxSpins = 200000;  // x s_sleep(8): ~50 ms, then the node block goes on (flagged)
 static_assert(kRowsLds == KACC_FAST_MAX_PROCS && kTpb<0> == KACC_FAST_MAX_AGGREGATES,
               "KACC_FAST_* must match the fast path's capacity");
 
@@ -161,6 +167,26 @@ static_assert(kRowsLds == KACC_FAST_MAX_PROCS && kTpb<0> == KACC_FAST_MAX_AGGREG
 // chunk's begin (or the node's end for the last chunk).
 struct ChunkItem {
   uint32_t node, chunk, nchunks, ctr_begin, vm_begin, pod_begin, pad[2];
+};
+
+// Cluster node totals (kacc_allreduce_namespaces, kacc_cluster_partials): one
+// block per output value — block c sums column c (node table c / Z of the five,
+// zone c % Z) over every node: lane l < kBlock adds nodes l, l + kBlock, ... in
+// order (kColLoads loads in flight), then the wave tree and the four waves in
+// order — and writes it.  No cross-block combine: no partial exchange, block
+// count or last-block reload (rounds 2-3 summed node ranges per block and let the
+// last block to finish add the partials: four dependent round trips, 6.5 us at
+// the 1/8 shard of config 3 against one or two here; and no reliance on how
+// gfx950 performs agent-scope atomics).  Config 3: 40 loads per lane, hidden
+// under the namespace blocks of the same launch.
+constexpr int kColLoads = 8;
+struct NodeTotalsArgs {
+  uint64_t n_nodes;
+  const uint64_t *active_total, *idle_total;
+  const double *power, *active_power, *idle_power;
+  const uint64_t *node_export;  // else the five tables: an interval's node export [n_nodes][5Z]
+  uint64_t *out_e;              // [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal (u64, modular)
+  double *out_p;                // [3Z]: Σ Power, Σ ActivePower, Σ IdlePower (f64)
 };
 
 struct DevState {
@@ -194,12 +220,26 @@ struct DevState {
   // phase skips them; pod_kernel keeps the list for the next interval
   uint32_t items_given, keep_items;
   uint64_t *stamps;  // kVarStamps only
+  // Deferred cluster partial sums of the PREVIOUS snapshot fused into this launch
+  // (kacc_cluster_partials_deferred): blocks [0, fp_blocks) of interval_kernel are
+  // namespace blocks [0, fp_ns_blocks) and node-total column blocks; every wave of
+  // them adds 1 to *fp_ctr when its loads are done, and a node block waits for
+  // *fp_ctr to reach fp_target before its first store into a table they read (the
+  // five node-total tables, deferred to the end, and the pod records)
+  uint32_t fp_blocks, fp_ns_blocks, fp_n_ns, fp_target;
+  uint32_t *fp_ctr;
+  const uint32_t *fp_off, *fp_slots;
+  uint64_t *fp_out_e;
+  double *fp_out_p;
+  NodeTotalsArgs fp_na;
 };
 
 struct NodeShared {
   uint64_t active_energy[KACC_MAX_ZONES];
   double power[KACC_MAX_ZONES];
   double active_power[KACC_MAX_ZONES];
+  uint64_t active_total[KACC_MAX_ZONES], idle_total[KACC_MAX_ZONES];  // fused partials: stored late
+  double idle_power[KACC_MAX_ZONES];
   double node_delta;
   uint32_t first;
 };
@@ -220,6 +260,11 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t x) { return __builtin_a
 // Experiments (timing A/B only; results are identical): KACC_WT_PROC writes the
 // non-temporal row stores through the L2 (sc0 sc1 nt: no dirty line is left for
 // the end-of-kernel write-back), KACC_WT_AGG the aggregate rows likewise.
+// Experiment: extra dynamic LDS per interval_kernel workgroup (fewer resident
+// workgroups per CU, each with a larger share of the bandwidth: shorter lifetimes)
+#ifndef KACC_FAST_EXTRA_LDS
+#define KACC_FAST_EXTRA_LDS 0
+#endif
 #ifndef KACC_WT_PROC
 #define KACC_WT_PROC 0
 #endif
@@ -629,7 +674,7 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
 // Phase A for one zone (thread z < Z): node.go:10-84 / node.go:101-131.
 template <int Z>
 __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState &st, uint32_t n,
-                                          int z, NodeShared &sh) {
+                                          int z, NodeShared &sh, bool defer_totals = false) {
   const bool first = st.node_has_prev[n] == 0u;
   const uint64_t i = static_cast<uint64_t>(n) * Z + z;
   const double ratio = b.node_usage_ratio[n];
@@ -651,14 +696,20 @@ __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState
     ap = p * ratio;
     ip = p - ap;
   }
-  st.node_active_total[i] = at;
-  st.node_idle_total[i] = it;
   export_node_zone<Z>(b, n, static_cast<uint32_t>(z), at, it, p, ap, ip);
   st.node_energy_total[i] = abs_e;
   st.node_active_energy[i] = active;
-  st.node_power[i] = p;
-  st.node_active_power[i] = ap;
-  st.node_idle_power[i] = ip;
+  if (defer_totals) {  // read by fused partial sums of the previous snapshot: stored by node_totals_out
+    sh.active_total[z] = at;
+    sh.idle_total[z] = it;
+    sh.idle_power[z] = ip;
+  } else {
+    st.node_active_total[i] = at;
+    st.node_idle_total[i] = it;
+    st.node_power[i] = p;
+    st.node_active_power[i] = ap;
+    st.node_idle_power[i] = ip;
+  }
   sh.active_energy[z] = active;
   sh.power[z] = p;
   sh.active_power[z] = ap;
@@ -754,6 +805,181 @@ __device__ __forceinline__ bool fits_fast(const NodeRanges &r) {
          (r.c1 - r.c0) + (r.v1 - r.v0) + (r.q1 - r.q0) <= static_cast<uint32_t>(kTpb<V>);
 }
 
+// Namespace totals: kNsLanes lanes per namespace (4 namespaces per wave);
+// lane l sums pods l, l+16, ... of its namespace in CSR order (loads issued
+// kNsUnroll at a time, adds in order), then the 16 lane sums are halved
+// pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
+// f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
+// kW: 8-byte words between consecutive rows — 2Z both for the state tables
+// (rows = pod slots: one [energy Z | power Z] record per slot, pod_row) and for
+// an interval's pod export (rows = batch pod rows, the same record).
+template <int Z, int kW = 2 * Z, int kThreads = kBlock>
+__device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
+                                                const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
+                                                const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
+                                                double *out_p, uint32_t *err) {
+  const uint32_t k = (blk * kThreads + threadIdx.x) / kNsLanes;
+  const uint32_t lane = threadIdx.x % kNsLanes;
+  const bool active = k < n_ns;  // inactive lanes still join the shuffles
+  unsigned long long e[Z];
+  double p[Z];
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    e[z] = 0;
+    p[z] = 0.0;
+  }
+  const uint32_t beg = active ? off[k] : 0u, end = active ? off[k + 1] : 0u;
+  // loads unconditional from clamped indices (a predicated load makes the
+  // compiler branch around it and wait per element); the adds are masked
+  for (uint32_t j0 = beg + lane; j0 < end; j0 += kNsLanes * kNsUnroll) {
+    uint32_t sl[kNsUnroll];
+#pragma unroll
+    for (int u = 0; u < kNsUnroll; ++u) sl[u] = slots[min(j0 + u * kNsLanes, end - 1)] & KACC_SLOT_MASK;
+    uint64_t er[kNsUnroll][Z];
+    double pr[kNsUnroll][Z];
+#pragma unroll
+    for (int u = 0; u < kNsUnroll; ++u) {
+      uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
+      load_row<Z>(pe + at * kW, 0, er[u]);
+      load_row_f64<Z>(pp + at * kW, 0, pr[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kNsUnroll; ++u) {
+      const bool in = j0 + u * kNsLanes < end;
+      if (in && sl[u] >= pod_slots) raise_err(err, kErrNs);
+      const bool use = in && sl[u] < pod_slots;
+#pragma unroll
+      for (int z = 0; z < Z; ++z) {
+        e[z] += use ? er[u][z] : 0ull;
+        if (use) p[z] = p[z] + pr[u][z];
+      }
+    }
+  }
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+#pragma unroll
+    for (int sft = kNsLanes / 2; sft >= 1; sft >>= 1) {
+      e[z] += __shfl_down(e[z], sft, kNsLanes);
+      p[z] = p[z] + __shfl_down(p[z], sft, kNsLanes);
+    }
+  }
+  if (active && lane == 0) {
+    store_row<Z, false, unsigned long long>(reinterpret_cast<unsigned long long *>(out_e), k, e);
+    store_row<Z, false, double>(out_p, k, p);
+  }
+}
+
+template <int Z>
+__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const uint32_t *__restrict__ off,
+                                                           const uint32_t *__restrict__ slots,
+                                                           const uint64_t *__restrict__ pe,
+                                                           const double *__restrict__ pp, uint64_t pod_slots,
+                                                           uint64_t *out_e, double *out_p, uint32_t *err) {
+  namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+}
+
+// Cluster partial sums of one context in ONE launch (kacc_allreduce_namespaces):
+// the first 5Z blocks are the node-total columns (NodeTotalsArgs), the last
+// ns_blocks blocks are namespace_kernel's.
+// Column mode of the cluster node totals (see NodeTotalsArgs): block b owns output
+// value b — column b / Z of the five node tables, zone b % Z — and lanes tid < kBlock
+// sum it (the same order whatever the caller's block size); s_w: kBlock / 64 words.
+template <int Z>
+__device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint32_t b, uint64_t *s_w) {
+  const uint32_t tid = threadIdx.x;
+  if (tid >= static_cast<uint32_t>(kBlock)) return;  // no barrier below: the idle lanes leave
+  const uint32_t t = b / Z, z = b % Z;
+  const bool is_u64 = t < 2;
+  const uint64_t *col = na.node_export ? na.node_export + t * Z + z
+                        : t == 0 ? na.active_total + z
+                        : t == 1 ? na.idle_total + z
+                        : reinterpret_cast<const uint64_t *>(t == 2 ? na.power : t == 3 ? na.active_power
+                                                                                        : na.idle_power) + z;
+  const uint64_t stride = na.node_export ? 5ull * Z : static_cast<uint64_t>(Z);
+  unsigned long long e = 0;
+  double p = 0.0;
+  for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kColLoads) {
+    uint64_t v[kColLoads];
+#pragma unroll
+    for (int u = 0; u < kColLoads; ++u) {  // unconditional from clamped nodes: all in flight
+      const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
+      v[u] = col[n * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < kColLoads; ++u) {
+      if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
+      if (is_u64)
+        e += v[u];
+      else
+        p = p + __longlong_as_double(static_cast<long long>(v[u]));
+    }
+  }
+#pragma unroll
+  for (int sft = 32; sft >= 1; sft >>= 1) {
+    e += __shfl_down(e, sft, 64);
+    p = p + __shfl_down(p, sft, 64);
+  }
+  if ((tid & 63u) == 0) s_w[tid >> 6] = is_u64 ? e : static_cast<uint64_t>(__double_as_longlong(p));
+  __syncthreads();
+  if (tid == 0) {
+    if (is_u64) {
+      unsigned long long r = s_w[0];
+      for (int w = 1; w < kBlock / 64; ++w) r += s_w[w];
+      na.out_e[t * Z + z] = r;
+    } else {
+      double r = __longlong_as_double(static_cast<long long>(s_w[0]));
+      for (int w = 1; w < kBlock / 64; ++w) r = r + __longlong_as_double(static_cast<long long>(s_w[w]));
+      na.out_p[(t - 2) * Z + z] = r;
+    }
+  }
+}
+
+// Fused deferred partial sums (DevState::fp_*): one block of the previous
+// snapshot's cluster partial sums inside interval_kernel (512 threads: 32
+// namespaces per namespace block; a node-total column block uses lanes < kBlock,
+// so both sum in the standalone kernel's order, bit for bit).  Every wave counts
+// itself once its loads are done: a node block's stores into the tables these
+// blocks read wait for the count (fused_wait), so no snapshot value is read after
+// the new interval overwrote it.
+template <int Z>
+__device__ __forceinline__ void fused_partials_block(const DevState &st, uint32_t pb) {
+  __shared__ uint64_t s_col[kBlock / 64];
+  if (pb < st.fp_ns_blocks)
+    namespace_block<Z, 2 * Z, kTpb<0>>(pb, st.fp_n_ns, st.fp_off, st.fp_slots, st.pod_energy, st.pod_power,
+                                       st.pod_slots, st.fp_out_e, st.fp_out_p, st.err);
+  else
+    node_column_block<Z>(st.fp_na, pb - st.fp_ns_blocks, s_col);
+  // the wave's loads returned (their values are summed): count the wave
+  if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(st.fp_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A node block before its first store into a table the fused partial sums read.
+// The partial-sum blocks come first in the grid and never wait, so the count is
+// reached; the bound only turns a broken assumption into a flagged error, never a hang.
+__device__ __forceinline__ void fused_wait(const DevState &st) {
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (static_cast<int32_t>(__hip_atomic_load(st.fp_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                                st.fp_target) < 0) {
+      if (++spins > kFusedMaxSpins) {
+        raise_err(st.err, kErrFused);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
+}
+// The node-total tables node_zone left in LDS (fused partial sums in flight).
+template <int Z>
+__device__ __forceinline__ void node_totals_out(const DevState &st, uint32_t n, int z, const NodeShared &sh) {
+  const uint64_t i = static_cast<uint64_t>(n) * Z + z;
+  st.node_active_total[i] = sh.active_total[z];
+  st.node_idle_total[i] = sh.idle_total[z];
+  st.node_power[i] = sh.power[z];
+  st.node_active_power[i] = sh.active_power[z];
+  st.node_idle_power[i] = sh.idle_power[z];
+}
+
 // One node snapshot of one interval on workgroup `blk` (interval_kernel).
 template <int Z, int V>
 __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevState &st, const uint32_t blk) {
@@ -819,7 +1045,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   const uint32_t rows = p1 - p0, nc = c1 - c0, nv = v1 - v0, nq = q1 - q0;
 
   // ---- A: node zones (threads z < Z) ------------------------------------------
-  if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
+  const bool fused = st.fp_blocks != 0;  // the previous snapshot's partial sums run in this launch
+  if (tid < Z) node_zone<Z>(b, st, n, tid, sh, fused);
 
   // ======================= fast path: one node fits the block ===================
   // Every global load the node needs is issued here, before the first barrier:
@@ -1078,7 +1305,15 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
     if (role == 3) export_pod<Z>(b, q0 + j, E, P);
   };
-  if constexpr (!kLateAgg<V>) aggregate_out();
+  auto fused_sync = [&]() {  // before the first store into a table the fused partial sums read
+    if (!fused) return;
+    fused_wait(st);
+    if (tid < Z) node_totals_out<Z>(st, n, tid, sh);
+  };
+  if constexpr (!kLateAgg<V>) {
+    fused_sync();
+    aggregate_out();
+  }
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
     if constexpr (kRowSweep) {
 #pragma unroll
@@ -1128,7 +1363,10 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       store_proc<Z, kNtScat>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   }
-  if constexpr (kLateAgg<V>) aggregate_out();
+  if constexpr (kLateAgg<V>) {
+    fused_sync();
+    aggregate_out();
+  }
   if constexpr (kStamp) {
     __syncthreads();
     if (tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
@@ -1141,7 +1379,15 @@ template <int Z, int V>
 #endif
 __global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
 void interval_kernel(const kacc_interval b, const DevState st) {
-  interval_node<Z, V>(b, st, blockIdx.x);
+  uint32_t blk = blockIdx.x;
+  if (st.fp_blocks) {  // the previous snapshot's deferred partial sums first (grid-uniform)
+    if (blk < st.fp_blocks) {
+      fused_partials_block<Z>(st, blk);
+      return;
+    }
+    blk -= st.fp_blocks;
+  }
+  interval_node<Z, V>(b, st, blk);
 }
 
 // ============ K intervals in one launch, state carried on chip ====================
@@ -1491,7 +1737,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     }
     if (status & KACC_NODE_READ_ERROR) {  // node.go:39-44: previous snapshot kept
       if (tid == 0) st.node_status[n] = KACC_NODE_SKIPPED;
-      if (b.pod_export || b.node_export) export_skipped<Z>(b, st, n, rg, tid, kThreads);
     } else if (!fits) {  // the caller's KACC_F_FAST_NODES promise was wrong
       if (tid == 0) raise_err(st.err, kErrBigNode);
     } else {
@@ -1655,7 +1900,6 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         st.node_power[zi] = z_p;
         st.node_active_power[zi] = z_ap;
         st.node_idle_power[zi] = z_ip;
-        export_node_zone<Z>(b, n, tid, c_atot, c_itot, z_p, z_ap, z_ip);
       }
       const Attr<Z> a = make_attr<Z>(sh, b.flags);
       if (tid == 0) {
@@ -1680,12 +1924,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
         const double ratio =
             attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, c_aE, E, P);
         store_agg<Z, kNtAggStores || (V & kCarryNtAgg) != 0>(st, role, a_s, E, P, ratio, n);
-        if (role == 3) export_pod<Z>(b, rg.q0 + (tid - nc - nv), E, P);
 #pragma unroll
         for (int z = 0; z < Z; ++z) c_aE[z] = E[z];
         c_atotal = a_total;
-      } else if (role == 3) {
-        export_pod_zero<Z>(b, rg.q0 + (tid - nc - nv));
       }
       c_role = a_ok ? role : 0u;
       c_aw = a_ok ? a_w : 0xffffffffu;
@@ -2487,28 +2728,33 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     }
     uint64_t prev[kR][Z];
     uint32_t contig = 0;
-    if constexpr ((V & kVarSkipProcs) == 0) {
+    // the rows' previous totals: loaded with the Δ / slot words (KACC_CHUNK_LATE_PREV 0), or
+    // after the aggregates (1: not live across the container / pod phases; slot words from LDS)
+    auto load_prev = [&](const uint32_t (&wsrc)[kR], int u0, int u1) {
+      if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-      for (int u = 0; u < kR; ++u) {
-        const uint64_t sl = w[u] & KACC_SLOT_MASK;
-        if constexpr (kT) {
-          const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
-          const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
-                            s0 + 64 <= st.proc_slots;
-          if (__all(mine)) {
-            contig |= 1u << u;
-            load_group_masked<Z, false, kNtLd>(st.proc_energy, s0, 64u, s0, prev[u]);
-            continue;
+        for (int u = u0; u < u1; ++u) {
+          const uint64_t sl = wsrc[u] & KACC_SLOT_MASK;
+          if constexpr (kT) {
+            const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
+            const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
+                              s0 + 64 <= st.proc_slots;
+            if (__all(mine)) {
+              contig |= 1u << u;
+              load_group_masked<Z, false, kNtLd>(st.proc_energy, s0, 64u, s0, prev[u]);
+              continue;
+            }
+          }
+          if (sl < st.proc_slots) {
+            load_row<Z>(st.proc_energy, sl, prev[u]);
+          } else {
+#pragma unroll
+            for (int z = 0; z < Z; ++z) prev[u][z] = 0;
           }
         }
-        if (sl < st.proc_slots) {
-          load_row<Z>(st.proc_energy, sl, prev[u]);
-        } else {
-#pragma unroll
-          for (int z = 0; z < Z; ++z) prev[u][z] = 0;
-        }
       }
-    }
+    };
+    if constexpr (!kChunkLatePrev) load_prev(w, 0, kR);
     // aggregate j of this chunk: containers [cb, ce), VMs [vb, ve), pods [qb, qe)
     const uint32_t ctr_rows_end = rg.c1 > rg.c0 ? b.ctr_proc_end[rg.c1 - 1] : rg.p0;
     auto agg = [&](uint32_t j, uint32_t &beg, uint32_t &end, uint32_t &wd) -> uint32_t {
@@ -2655,9 +2901,22 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       else
         raise_err(st.err, kErrCapacity);
     }
+    // late previous totals: KACC_CHUNK_LATE_PREV groups of rows at a time
+    constexpr int kLB = kChunkLatePrev ? KACC_CHUNK_LATE_PREV : kR;
+#pragma unroll
+    for (int ub = 0; ub < kR; ub += kLB) {
+    if constexpr (kChunkLatePrev) {
+      uint32_t wl[kR];
+#pragma unroll
+      for (int u = ub; u < ub + kLB; ++u) {
+        const uint32_t r = utid + u * kThreads;
+        wl[u] = r < rows ? s_w[r] : 0xffffffffu;
+      }
+      load_prev(wl, ub, ub + kLB);
+    }
     if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-      for (int u = 0; u < kR; ++u) {
+      for (int u = ub; u < ub + kLB; ++u) {
         const uint32_t r = utid + u * kThreads;
         if constexpr (kT) {
           if (contig & (1u << u)) {
@@ -2680,6 +2939,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
       }
     }
+    }  // ub
     // aggregates beyond one per lane (chunks of mostly empty containers):
     // containers / VMs here, their pods always deferred
     for (uint32_t j = kThreads + utid; j < nagg; j += kThreads) {
@@ -2777,127 +3037,6 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
   }
 }
 
-// Namespace totals: kNsLanes lanes per namespace (4 namespaces per wave);
-// lane l sums pods l, l+16, ... of its namespace in CSR order (loads issued
-// kNsUnroll at a time, adds in order), then the 16 lane sums are halved
-// pairwise (l += l+s, s = 8..1).  u64 energy sums are order independent;
-// f64 power follows this fixed order (mirrored by oracle/kor_namespace_totals).
-// kW: 8-byte words between consecutive rows — 2Z both for the state tables
-// (rows = pod slots: one [energy Z | power Z] record per slot, pod_row) and for
-// an interval's pod export (rows = batch pod rows, the same record).
-template <int Z, int kW = 2 * Z>
-__device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
-                                                const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
-                                                const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
-                                                double *out_p, uint32_t *err) {
-  const uint32_t k = (blk * kBlock + threadIdx.x) / kNsLanes;
-  const uint32_t lane = threadIdx.x % kNsLanes;
-  const bool active = k < n_ns;  // inactive lanes still join the shuffles
-  unsigned long long e[Z];
-  double p[Z];
-#pragma unroll
-  for (int z = 0; z < Z; ++z) {
-    e[z] = 0;
-    p[z] = 0.0;
-  }
-  const uint32_t beg = active ? off[k] : 0u, end = active ? off[k + 1] : 0u;
-  // loads unconditional from clamped indices (a predicated load makes the
-  // compiler branch around it and wait per element); the adds are masked
-  for (uint32_t j0 = beg + lane; j0 < end; j0 += kNsLanes * kNsUnroll) {
-    uint32_t sl[kNsUnroll];
-#pragma unroll
-    for (int u = 0; u < kNsUnroll; ++u) sl[u] = slots[min(j0 + u * kNsLanes, end - 1)] & KACC_SLOT_MASK;
-    uint64_t er[kNsUnroll][Z];
-    double pr[kNsUnroll][Z];
-#pragma unroll
-    for (int u = 0; u < kNsUnroll; ++u) {
-      uint64_t at = sl[u] < pod_slots ? sl[u] : 0u;
-      load_row<Z>(pe + at * kW, 0, er[u]);
-      load_row_f64<Z>(pp + at * kW, 0, pr[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < kNsUnroll; ++u) {
-      const bool in = j0 + u * kNsLanes < end;
-      if (in && sl[u] >= pod_slots) raise_err(err, kErrNs);
-      const bool use = in && sl[u] < pod_slots;
-#pragma unroll
-      for (int z = 0; z < Z; ++z) {
-        e[z] += use ? er[u][z] : 0ull;
-        if (use) p[z] = p[z] + pr[u][z];
-      }
-    }
-  }
-#pragma unroll
-  for (int z = 0; z < Z; ++z) {
-#pragma unroll
-    for (int sft = kNsLanes / 2; sft >= 1; sft >>= 1) {
-      e[z] += __shfl_down(e[z], sft, kNsLanes);
-      p[z] = p[z] + __shfl_down(p[z], sft, kNsLanes);
-    }
-  }
-  if (active && lane == 0) {
-    store_row<Z, false, unsigned long long>(reinterpret_cast<unsigned long long *>(out_e), k, e);
-    store_row<Z, false, double>(out_p, k, p);
-  }
-}
-
-template <int Z>
-__global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const uint32_t *__restrict__ off,
-                                                           const uint32_t *__restrict__ slots,
-                                                           const uint64_t *__restrict__ pe,
-                                                           const double *__restrict__ pp, uint64_t pod_slots,
-                                                           uint64_t *out_e, double *out_p, uint32_t *err) {
-  namespace_block<Z>(blockIdx.x, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
-}
-
-// Cluster partial sums of one context in ONE launch (kacc_allreduce_namespaces):
-// the last ns_blocks blocks are namespace_kernel's; the first ones reduce the node
-// tables — block b sums nodes [b·npb, (b+1)·npb) (lane l: nodes l, l+256, …,
-// then the wave trees and the four waves in order) into partials[b]; the last
-// block to finish adds the ≤ kNodeBlocksMax partials in block order (a fixed
-// order whichever block is last: reproducible f64 sums) into
-//   node_e [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal   (u64, modular)
-//   node_p [3Z]: Σ Power, Σ ActivePower, Σ IdlePower       (f64)
-//
-// The last-block handoff is NOT a C++-memory-model release/acquire pair: the
-// partials are published by relaxed agent-scope atomic exchanges and the block
-// counter by a relaxed agent-scope add.  It is correct on gfx950 (as on gfx942)
-// because of how that hardware executes them: an agent-scope atomic RMW is
-// performed at the device's coherence point beyond the XCD's L2 (sc1), and its
-// RETURNED value only arrives once it has been performed — every lane waits for
-// its exchange's old value before the barrier that precedes thread 0's count,
-// so all partials are performed before the count is; the last block then drops
-// its XCD's L2 (acquire fence) and reads them with agent-scope atomic loads.  A
-// release fetch_add on the counter would make it portable, at the cost of an L2
-// write-back (buffer_wbl2) in every node block: the __threadfence pair that
-// cost 2.2 us of the partial sums (profiles/r03/tprobe).  The build refuses any
-// other target; tests/test_gpu_cluster.py::test_cluster_node_totals_back_to_back_launches
-// pins it over 24 back-to-back launches with changing node data.
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
-#error "cluster_partials_kernel's last-block handoff is written for gfx950's agent-scope atomics"
-#endif
-constexpr uint32_t kNodeBlocksMax = 64;
-// Column mode (n_nodes <= kColumnMaxNodes): one block per output value — block c
-// sums column c (table c / Z, zone c % Z) over every node (lane l: nodes l, l+256,
-// ... in order, kColLoads loads in flight, then the wave tree and the four waves
-// in order) and writes it: no cross-block combine, so no partial exchange, block
-// count or last-block reload (four dependent round trips -> one or two: the 1/8
-// shard of config 3 has 1,250 nodes = five loads per lane).
-constexpr uint32_t kColumnMaxNodes = 8192;
-constexpr int kColLoads = 8;
-struct NodeTotalsArgs {
-  uint64_t n_nodes;
-  uint32_t columns;   // 1: column mode (5Z blocks, one output value each)
-  uint32_t npb;       // nodes per block (a multiple of kBlock)
-  const uint64_t *active_total, *idle_total;
-  const double *power, *active_power, *idle_power;
-  const uint64_t *node_export;  // else the five tables: an interval's node export [n_nodes][5Z]
-  uint64_t *part;     // [blocks][5Z] raw 8-byte words: 2Z u64 then 3Z f64
-  uint32_t *done;     // block counter, re-armed by the last block
-  uint64_t *out_e;
-  double *out_p;
-};
-
 template <int Z, int kW = 2 * Z>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
@@ -2915,146 +3054,8 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
     namespace_block<Z, kW>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
     return;
   }
-  constexpr int kV = 5 * Z;
-  __shared__ uint64_t s_w[kBlock / 64][kV];
-  __shared__ uint64_t s_part[kNodeBlocksMax * kV];
-  __shared__ uint32_t s_last;
-  const uint32_t tid = threadIdx.x, b = blockIdx.x;
-  if (na.columns) {  // block b owns output value b: column b / Z of the five, zone b % Z
-    const uint32_t t = b / Z, z = b % Z;
-    const bool is_u64 = t < 2;
-    const uint64_t *col = na.node_export ? na.node_export + t * Z + z
-                          : t == 0 ? na.active_total + z
-                          : t == 1 ? na.idle_total + z
-                          : reinterpret_cast<const uint64_t *>(t == 2 ? na.power : t == 3 ? na.active_power
-                                                                                          : na.idle_power) + z;
-    const uint64_t stride = na.node_export ? 5ull * Z : static_cast<uint64_t>(Z);
-    unsigned long long e = 0;
-    double p = 0.0;
-    for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kColLoads) {
-      uint64_t v[kColLoads];
-#pragma unroll
-      for (int u = 0; u < kColLoads; ++u) {  // unconditional from clamped nodes: all in flight
-        const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
-        v[u] = col[n * stride];
-      }
-#pragma unroll
-      for (int u = 0; u < kColLoads; ++u) {
-        if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
-        if (is_u64)
-          e += v[u];
-        else
-          p = p + __longlong_as_double(static_cast<long long>(v[u]));
-      }
-    }
-#pragma unroll
-    for (int sft = 32; sft >= 1; sft >>= 1) {
-      e += __shfl_down(e, sft, 64);
-      p = p + __shfl_down(p, sft, 64);
-    }
-    if ((tid & 63u) == 0) s_w[tid >> 6][0] = is_u64 ? e : static_cast<uint64_t>(__double_as_longlong(p));
-    __syncthreads();
-    if (tid == 0) {
-      if (is_u64) {
-        unsigned long long r = s_w[0][0];
-        for (int w = 1; w < kBlock / 64; ++w) r += s_w[w][0];
-        na.out_e[t * Z + z] = r;
-      } else {
-        double r = __longlong_as_double(static_cast<long long>(s_w[0][0]));
-        for (int w = 1; w < kBlock / 64; ++w) r = r + __longlong_as_double(static_cast<long long>(s_w[w][0]));
-        na.out_p[(t - 2) * Z + z] = r;
-      }
-    }
-    return;
-  }
-  unsigned long long ve[2 * Z];
-  double vp[3 * Z];
-#pragma unroll
-  for (int q = 0; q < 2 * Z; ++q) ve[q] = 0;
-#pragma unroll
-  for (int q = 0; q < 3 * Z; ++q) vp[q] = 0.0;
-  const uint64_t n_end = min(static_cast<uint64_t>(b + 1) * na.npb, na.n_nodes);
-  for (uint64_t n = static_cast<uint64_t>(b) * na.npb + tid; n < n_end; n += kBlock) {
-    uint64_t a[Z], i[Z];
-    double pw[Z], ap[Z], ip[Z];
-    if (na.node_export) {  // the same values, from the interval's node export
-      const uint64_t *x = na.node_export + n * (5 * Z);
-      const double *xd = reinterpret_cast<const double *>(x);
-      load_row<Z>(x, 0, a);
-      load_row<Z>(x, 1, i);
-      load_row_f64<Z>(xd, 2, pw);
-      load_row_f64<Z>(xd, 3, ap);
-      load_row_f64<Z>(xd, 4, ip);
-    } else {
-      load_row<Z>(na.active_total, n, a);
-      load_row<Z>(na.idle_total, n, i);
-      load_row_f64<Z>(na.power, n, pw);
-      load_row_f64<Z>(na.active_power, n, ap);
-      load_row_f64<Z>(na.idle_power, n, ip);
-    }
-#pragma unroll
-    for (int z = 0; z < Z; ++z) {
-      ve[z] += a[z];
-      ve[Z + z] += i[z];
-      vp[z] = vp[z] + pw[z];
-      vp[Z + z] = vp[Z + z] + ap[z];
-      vp[2 * Z + z] = vp[2 * Z + z] + ip[z];
-    }
-  }
-#pragma unroll
-  for (int sft = 32; sft >= 1; sft >>= 1) {
-#pragma unroll
-    for (int q = 0; q < 2 * Z; ++q) ve[q] += __shfl_down(ve[q], sft, 64);
-#pragma unroll
-    for (int q = 0; q < 3 * Z; ++q) vp[q] = vp[q] + __shfl_down(vp[q], sft, 64);
-  }
-  if ((tid & 63u) == 0) {
-#pragma unroll
-    for (int q = 0; q < 2 * Z; ++q) s_w[tid >> 6][q] = ve[q];
-#pragma unroll
-    for (int q = 0; q < 3 * Z; ++q) s_w[tid >> 6][2 * Z + q] = static_cast<uint64_t>(__double_as_longlong(vp[q]));
-  }
-  __syncthreads();
-  if (tid < static_cast<uint32_t>(kV)) {  // the four waves in order
-    uint64_t r;
-    if (tid < 2u * Z) {
-      r = s_w[0][tid];
-      for (int w = 1; w < kBlock / 64; ++w) r += s_w[w][tid];
-    } else {
-      double t = __longlong_as_double(static_cast<long long>(s_w[0][tid]));
-      for (int w = 1; w < kBlock / 64; ++w) t = t + __longlong_as_double(static_cast<long long>(s_w[w][tid]));
-      r = static_cast<uint64_t>(__double_as_longlong(t));
-    }
-    // the block partials cross XCDs as device-scope atomic exchanges, performed
-    // beyond L2 (their returned value is waited for, so each is done before the
-    // block counts itself): no L2 write-back per block (a __threadfence pair,
-    // buffer_wbl2 + buffer_inv in every node block, made the node totals the
-    // longest chain of the step: 7.0 of 9.2 us at the 1/8 shard, profiles/r03/tprobe)
-    const unsigned long long old =
-        atomicExch(reinterpret_cast<unsigned long long *>(na.part) + static_cast<uint64_t>(b) * kV + tid,
-                   static_cast<unsigned long long>(r));
-    asm volatile("" ::"v"(old));
-  }
-  __syncthreads();
-  if (tid == 0) s_last = atomicAdd(na.done, 1u) == nb - 1 ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;
-  // the last block only: drop this XCD's L2 copies of the partials (an earlier
-  // launch's), then read every partial at once
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (uint32_t x = tid; x < nb * kV; x += kBlock)
-    s_part[x] = __hip_atomic_load(na.part + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (tid < 2u * Z) {
-    unsigned long long t = 0;
-    for (uint32_t k = 0; k < nb; ++k) t += s_part[k * kV + tid];
-    na.out_e[tid] = t;
-  } else if (tid < static_cast<uint32_t>(kV)) {
-    double t = 0.0;
-    for (uint32_t k = 0; k < nb; ++k) t = t + __longlong_as_double(static_cast<long long>(s_part[k * kV + tid]));
-    na.out_p[tid - 2 * Z] = t;
-  }
-  if (tid == 0) atomicExch(na.done, 0u);  // re-armed for the next launch (stream order)
+  __shared__ uint64_t s_w[kBlock / 64];
+  node_column_block<Z>(na, blockIdx.x, s_w);  // block b owns output value b: column b / Z, zone b % Z
 }
 
 // Elements [first, first + count) of the derived process power table
@@ -3207,6 +3208,12 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.items_given = 0;
   s.keep_items = 0;
   s.stamps = nullptr;
+  s.fp_blocks = s.fp_ns_blocks = s.fp_n_ns = s.fp_target = 0;
+  s.fp_ctr = nullptr;
+  s.fp_off = s.fp_slots = nullptr;
+  s.fp_out_e = nullptr;
+  s.fp_out_p = nullptr;
+  s.fp_na = kacc::NodeTotalsArgs{};
   return s;
 }
 
@@ -3226,8 +3233,8 @@ void launch_small(const kacc_interval &b, const kacc::DevState &s, hipStream_t s
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   if (V == 0 && (b.flags & KACC_F_SMALL_NODES)) return launch_small<Z>(b, s, st);
-  KACC_LAUNCH((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>), 0, st, b,
-                     s);
+  KACC_LAUNCH((kacc::interval_kernel<Z, V>), dim3(b.n_nodes + s.fp_blocks), dim3(kacc::kTpb<V>),
+              KACC_FAST_EXTRA_LDS, st, b, s);
   if (b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES)) return;
   const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
   KACC_LAUNCH((kacc::chunk_kernel<Z, V>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st,
@@ -3284,6 +3291,52 @@ void launch_ns(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, const 
                      slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
                      (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p,
                      ctx->d_err);
+}
+
+// The node-total columns of the context's tables (node_export NULL) or of an export.
+kacc::NodeTotalsArgs node_totals_args(const kacc_ctx *ctx, uint64_t live, const uint64_t *node_export,
+                                      uint64_t *node_energy, double *node_power) {
+  kacc::NodeTotalsArgs na{};
+  na.n_nodes = live;
+  na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
+  na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];
+  na.power = (const double *)ctx->tables[KACC_T_NODE_POWER];
+  na.active_power = (const double *)ctx->tables[KACC_T_NODE_ACTIVE_POWER];
+  na.idle_power = (const double *)ctx->tables[KACC_T_NODE_IDLE_POWER];
+  na.out_e = node_energy;
+  na.out_p = node_power;
+  na.node_export = node_export;
+  return na;
+}
+
+// A deferred partial-sum request (kacc_internal_defer_partials) launched on its own,
+// on the stream it was made on: before anything else writes the tables it reads.
+int flush_deferred(kacc_ctx *ctx) {
+  if (!ctx->deferred.pending) return KACC_OK;
+  const kacc_ctx::Deferred d = ctx->deferred;
+  ctx->deferred.pending = false;
+  return kacc_internal_export_partials(ctx, d.n_ns, d.off, d.slots, nullptr, 0, nullptr, 0, 0, d.out_e, d.out_p,
+                                       d.node_e, d.node_p, d.stream);
+}
+
+// The deferred request fused into this interval_kernel launch (its first blocks).
+void fuse_deferred(kacc_ctx *ctx, kacc::DevState &ds) {
+  const kacc_ctx::Deferred d = ctx->deferred;
+  ctx->deferred.pending = false;
+  const uint32_t ns_per_block = kacc::kTpb<0> / kacc::kNsLanes;
+  ds.fp_ns_blocks = (d.n_ns + ns_per_block - 1) / ns_per_block;
+  const uint32_t col_blocks = d.node_e ? 5u * ctx->cfg.zones : 0u;
+  ds.fp_blocks = ds.fp_ns_blocks + col_blocks;
+  ds.fp_n_ns = d.n_ns;
+  ds.fp_off = d.off;
+  ds.fp_slots = d.slots;
+  ds.fp_out_e = d.out_e;
+  ds.fp_out_p = d.out_p;
+  ds.fp_na = node_totals_args(ctx, std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes), nullptr, d.node_e, d.node_p);
+  ds.fp_ctr = ctx->d_ctr + 3;
+  ctx->fp_issued += ds.fp_blocks * static_cast<uint32_t>(kacc::kTpb<0> / 64);  // every wave counts once
+  ds.fp_target = ctx->fp_issued;
+  if (!ds.fp_blocks) ds.fp_target = 0;
 }
 
 // pod_export NULL: the namespace sums gather the state tables by pod slot;
@@ -3609,7 +3662,6 @@ void kacc_destroy(kacc_ctx *ctx) {
   if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
   if (ctx->d_items) (void)hipFree(ctx->d_items);
   if (ctx->d_defer) (void)hipFree(ctx->d_defer);
-  if (ctx->d_node_part) (void)hipFree(ctx->d_node_part);
   if (ctx->batch_copied) {
     (void)hipEventSynchronize(ctx->batch_copied);
     (void)hipEventDestroy(ctx->batch_copied);
@@ -3640,6 +3692,8 @@ int kacc_reset(kacc_ctx *ctx) {
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->live_nodes = 0;
+  ctx->deferred.pending = false;  // a reset snapshot has no partial sums to compute
+  ctx->fp_issued = 0;             // d_ctr[3] is zero again
   return KACC_OK;
 }
 
@@ -3650,23 +3704,58 @@ int kacc_time_next_launch(kacc_ctx *ctx, void *start_event, void *stop_event) {
   return KACC_OK;
 }
 
+static int run_one(kacc_ctx *ctx, const kacc_interval *b, void *stream);
+
 int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   if (!ctx) return KACC_EINVAL;
   const kacc::TimingScope timing(ctx);
+  return run_one(ctx, b, stream);
+}
+
+// One interval (kacc_run_interval, kacc_run_intervals of one): a pending deferred
+// partial-sum request rides in its launch when it can.
+static int run_one(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  // a deferred partial-sum request of the snapshot so far: fused into this launch
+  // when it is a fast-path launch on the request's stream, else launched first
+  const bool fuse = ctx->deferred.pending && b->n_nodes && st == ctx->deferred.stream &&
+                    (b->flags & KACC_F_FAST_NODES) && !(b->flags & KACC_F_SMALL_NODES);
+  if (!fuse && (rc = flush_deferred(ctx)) != KACC_OK) return rc;
   if (b->n_nodes == 0) {  // an emptied batch: no node of it counts in the cluster totals
     ctx->live_nodes = 0;
     return KACC_OK;
   }
-  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  launch(ctx->cfg.zones, *b, dev_state(ctx), st);
+  kacc::DevState ds = dev_state(ctx);
+  if (fuse) fuse_deferred(ctx, ds);
+  launch(ctx->cfg.zones, *b, ds, st);
   KACC_HIP(ctx, hipGetLastError());
   ctx->live_nodes = b->n_nodes;
   return KACC_OK;
+}
+
+int kacc_internal_defer_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
+                                 uint64_t *out_energy, double *out_power, uint64_t *node_energy, double *node_power,
+                                 void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (n_ns && (!off || !slots || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
+  if ((node_energy != nullptr) != (node_power != nullptr))
+    return fail(ctx, KACC_EINVAL, "node totals need both output arrays");
+  int rc = flush_deferred(ctx);  // one request at a time
+  if (rc != KACC_OK) return rc;
+  if (!n_ns && !node_energy) return KACC_OK;
+  ctx->deferred = kacc_ctx::Deferred{true, n_ns, off, slots, out_energy, out_power, node_energy, node_power,
+                                     stream ? static_cast<hipStream_t>(stream) : ctx->stream};
+  return KACC_OK;
+}
+
+int kacc_internal_flush_partials(kacc_ctx *ctx) {
+  if (!ctx) return KACC_EINVAL;
+  return flush_deferred(ctx);
 }
 
 // K consecutive intervals in one call (fleet replay, BASELINE config 5's 60
@@ -3677,6 +3766,7 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
   if (!ctx) return KACC_EINVAL;
   const kacc::TimingScope timing(ctx);
   if (count && !dev_batches) return fail(ctx, KACC_EINVAL, "dev_batches is NULL");
+  if (count == 1) return run_one(ctx, dev_batches, stream);
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   uint64_t max_nodes = 0, max_procs = 0, max_pods = 0;
   for (uint32_t k = 0; k < count; ++k) {
@@ -3687,8 +3777,9 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
     max_pods = std::max<uint64_t>(max_pods, dev_batches[k].n_pods);
   }
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  int rc = ensure_items(ctx, max_nodes, max_procs, max_pods);
+  int rc = flush_deferred(ctx);
   if (rc != KACC_OK) return rc;
+  if ((rc = ensure_items(ctx, max_nodes, max_procs, max_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
   const kacc::DevState ds = dev_state(ctx);
   // one launch for all K intervals when every node stays in one workgroup's
@@ -3696,9 +3787,11 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
   bool fused = count > 1 && ctx->cfg.zones <= static_cast<uint32_t>(kacc::kCarryMaxZ);
   for (uint32_t k = 0; k < count && fused; ++k) {
     const kacc_interval &b = dev_batches[k];
+    // exports (kacc_interval.pod_export / node_export) are written by the per-interval
+    // kernels only: the carry kernel without them spills less (SGPR pressure, round 4)
     fused = (b.flags & KACC_F_FAST_NODES) && (b.flags & KACC_F_NODE_SLOT_RANGES) &&
             !(b.flags & KACC_F_SMALL_NODES) && !b.node_order && b.n_nodes == dev_batches[0].n_nodes &&
-            b.n_nodes > 0;
+            b.n_nodes > 0 && !b.pod_export && !b.node_export;
   }
   if (fused) {
     if ((rc = stage_batches(ctx, dev_batches, count, st)) != KACC_OK) return rc;
@@ -3934,6 +4027,7 @@ int kacc_batch_alloc(kacc_ctx *ctx, const kacc_shape *shape, kacc_batch **out, k
 // buffers are not overwritten before its previous kernels have read them.
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (!ctx || !bt) return KACC_EINVAL;
+  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   const uint32_t K = bt->cap.intervals;
   const uint64_t Z = ctx->cfg.zones;
   std::vector<kacc_interval> dv(K);
@@ -4055,6 +4149,10 @@ static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
                 (unsigned long long)ctx->counts[t]);
   if (kTables[t].derived && !down)
     return fail(ctx, KACC_EINVAL, "table %d is derived on read and cannot be uploaded", (int)t);
+  if (!down) {  // a deferred partial-sum request reads the tables before they change
+    const int frc = flush_deferred(ctx);
+    if (frc != KACC_OK) return frc;
+  }
   if (!count) return KACC_OK;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -4130,6 +4228,8 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
                                   uint64_t *node_energy,
                                   double *node_power, void *stream) {
   if (!ctx) return KACC_EINVAL;
+  int frc = flush_deferred(ctx);  // a deferred request reads the snapshot first
+  if (frc != KACC_OK) return frc;
   const kacc::TimingScope timing(ctx);
   if (n_ns && (!off || !rows || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
@@ -4142,40 +4242,9 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   if (from_exports && n_nodes && !node_export) return fail(ctx, KACC_EINVAL, "node export is NULL");
   const uint64_t live = from_exports ? n_nodes : std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes);
   const uint32_t *slots = rows;
-  // up to kColumnMaxNodes nodes: one block per output value (no cross-block
-  // combine); more: at most kNodeBlocksMax blocks of a multiple of kBlock nodes
-  // each and the last-block combine
-  const bool columns = live <= kacc::kColumnMaxNodes;
-  const uint64_t groups = (live + kacc::kBlock - 1) / kacc::kBlock;
-  const uint32_t npb = static_cast<uint32_t>(
-      kacc::kBlock * std::max<uint64_t>(1, (groups + kacc::kNodeBlocksMax - 1) / kacc::kNodeBlocksMax));
-  // no live node: blocks that write zero totals
-  const uint32_t node_blocks = !node_energy ? 0u
-                               : columns    ? static_cast<uint32_t>(5 * Z)
-                                            : std::max<uint32_t>(1, static_cast<uint32_t>((live + npb - 1) / npb));
-  if (!columns && node_blocks > ctx->node_part_cap) {  // partial sums scratch (grown between calls)
-    KACC_HIP(ctx, hipStreamSynchronize(st));
-    if (ctx->d_node_part) KACC_HIP(ctx, hipFree(ctx->d_node_part));
-    ctx->d_node_part = nullptr;
-    ctx->node_part_cap = 0;
-    KACC_HIP(ctx, hipMalloc(&ctx->d_node_part, 8 * 5 * Z * node_blocks + 16));
-    KACC_HIP(ctx, hipMemsetAsync(ctx->d_node_part, 0, 8 * 5 * Z * node_blocks + 16, st));
-    ctx->node_part_cap = node_blocks;
-  }
-  kacc::NodeTotalsArgs na{};
-  na.n_nodes = live;
-  na.columns = columns ? 1u : 0u;
-  na.npb = npb;
-  na.active_total = (const uint64_t *)ctx->tables[KACC_T_NODE_ACTIVE_TOTAL];
-  na.idle_total = (const uint64_t *)ctx->tables[KACC_T_NODE_IDLE_TOTAL];
-  na.power = (const double *)ctx->tables[KACC_T_NODE_POWER];
-  na.active_power = (const double *)ctx->tables[KACC_T_NODE_ACTIVE_POWER];
-  na.idle_power = (const double *)ctx->tables[KACC_T_NODE_IDLE_POWER];
-  na.done = static_cast<uint32_t *>(ctx->d_node_part);  // [0]; partials after 16 B
-  na.part = reinterpret_cast<uint64_t *>(static_cast<char *>(ctx->d_node_part) + 16);
-  na.out_e = node_energy;
-  na.out_p = node_power;
-  na.node_export = node_export;
+  // one block per output value (no live node: they write zero totals)
+  const uint32_t node_blocks = node_energy ? static_cast<uint32_t>(5 * Z) : 0u;
+  const kacc::NodeTotalsArgs na = node_totals_args(ctx, live, node_export, node_energy, node_power);
   if (!n_ns && !node_blocks) return KACC_OK;
   (void)hipGetLastError();
 #define KACC_PARTIALS(Z_)                                                                                  \
@@ -4281,6 +4350,7 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
 int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream, int variant,
                             uint64_t *d_out) {
   if (!ctx || !b || count == 0 || !d_out) return KACC_EINVAL;
+  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -4303,6 +4373,7 @@ int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t coun
 int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream,
                                      int variant) {
   if (!ctx || !b || count == 0) return KACC_EINVAL;
+  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -4330,6 +4401,7 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint
 // other than 0 does NOT compute the reference semantics.
 int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *b, void *stream, uint64_t *d_out) {
   if (!ctx || !d_out) return KACC_EINVAL;
+  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;
@@ -4348,6 +4420,7 @@ int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *b, void *stre
 
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, int variant) {
   if (!ctx) return KACC_EINVAL;
+  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;

@@ -21,7 +21,10 @@ tools/gpu_steps.sh \
   $O/bench_c3 600 "python bench.py --json-out gpurun_out/$O/bench_c3.json" \
   $O/bench_c3_shard8 300 "python bench.py --shard-of 8 --steps 50 --warmup 10 --no-cpu-baseline --json-out gpurun_out/$O/bench_c3_shard8.json" \
   $O/bench_c1 300 "python bench.py --config 1 --no-cpu-baseline --frag-line 0 --json-out gpurun_out/$O/bench_c1.json" \
-  $O/bench_c2_k60 300 "python bench.py --config 2 --intervals 60 --no-cpu-baseline --frag-line 0 --json-out gpurun_out/$O/bench_c2_k60.json" || exit $?
+  $O/bench_c2_k60 300 "python bench.py --config 2 --intervals 60 --no-cpu-baseline --frag-line 0 --json-out gpurun_out/$O/bench_c2_k60.json" \
+  $O/s8_ns 300 "python bench.py --shard-of 8 --steps 40 --warmup 5 --no-cpu-baseline --totals-probe ns --json-out gpurun_out/$O/bench_s8_ns.json" \
+  $O/s8_nodes 300 "python bench.py --shard-of 8 --steps 40 --warmup 5 --no-cpu-baseline --totals-probe nodes --json-out gpurun_out/$O/bench_s8_nodes.json" \
+  $O/stamps 300 "python tools/bench_stamps.py > gpurun_out/$O/stamps.jsonl" || exit $?
 for f in gpurun_out/$O/bench_c*.json; do
   python -c "import json;d=json.load(open('$f'));r=d['roofline'];print('$f', 'value %.2fG step %.1f kern %.1f tot %.1f frac %.3f' % (d['value']/1e9, d['ms_per_step']*1e3, d['kernel_ms']*1e3, d['totals_compute_ms']*1e3, r['frac']))"
 done
