@@ -110,11 +110,6 @@ def parse():
                          "totals_compute_ms; inline = those launch events inside the timed region; markers = "
                          "hipEventRecord markers around them inside the timed region (round 2).  Every event "
                          "packet costs a stream gap: ~9 us per step, profiles/r03/events")
-    ap.add_argument("--fuse-partials", choices=["on", "off"], default="on",
-                    help="tables mode, one interval per step on the fast path: on = each step's cluster partial "
-                         "sums are deferred and computed inside the next step's interval launch (its first "
-                         "workgroups, kacc_cluster_partials_deferred; the last step's by kacc_cluster_flush), so "
-                         "a step is ONE launch; off = a partial-sum launch after every interval (round 3)")
     ap.add_argument("--slot-nodes", choices=["stable", "write"], default="stable",
                     help="stable: KACC_F_STABLE_SLOT_NODES (a process slot keeps its node; only NEW rows store "
                          "it); write: every row stores its node (ablation)")
@@ -681,15 +676,6 @@ def measure(args, w, rank, world, stream, comm_stream):
                     P([w.ns_p[b].data_ptr()]), None if no_nodes else P([w.nd_e[b].data_ptr()]),
                     None if no_nodes else P([w.nd_p[b].data_ptr()]), P([stream])) for b in range(w.n_bufs)]
         reduce_fn = lib.kacc_cluster_partials
-    # --fuse-partials: each step DEFERS its partial sums; the next step's interval launch computes
-    # them in its first workgroups (kacc_cluster_partials_deferred), the region's last step's in a
-    # launch of their own (kacc_cluster_flush) — inside the timed region.  A group's all-reduce is
-    # issued once the launch that computed its last step's sums is queued.
-    fuse = (args.fuse_partials == "on" and not w.exports and K == 1
-            and bool(w.flags & accel.KACC_F_FAST_NODES) and not w.flags & accel.KACC_F_SMALL_NODES)
-    if fuse:
-        reduce_fn = lib.kacc_cluster_partials_deferred
-    w.fused_partials = fuse
     done = [torch.cuda.Event() for _ in range(w.n_bufs)]
     used = [False] * w.n_bufs
     compute = torch.cuda.current_stream()
@@ -748,28 +734,18 @@ def measure(args, w, rank, world, stream, comm_stream):
         if ev is not None:
             if markers:
                 ev[1].record()
-            elif not fuse:  # the totals' partial-sum kernel (compute stream)
+            else:  # the totals' partial-sum kernel (compute stream)
                 time_next(acc.ctx, ev[2], ev[3])
-        if fuse and k - 1 in group_of:  # step k - 1's partial sums ran inside this launch
-            flush(group_of[k - 1], k - 1)
         rc = reduce_fn(cl.handle, 0 if args.totals_probe == "nodes" else w.n_ns, *ns_args[b])
         if rc != accel.KACC_OK:
             cl._check(rc)
         if ev is not None and markers:
             ev[2].record()  # the compute stream's part of the totals (partial sums, tables mode)
-        if not fuse and not w.exports and k in group_of:
+        if not w.exports and k in group_of:
             flush(group_of[k], k)
         if comm and w.exports:
             done[b].record(comm_stream)
         used[b] = True
-
-    def finish(last):
-        """Fused partials: the region's last step's partial sums in a launch of their own, then its
-        group's all-reduce."""
-        if fuse:
-            cl._check(lib.kacc_cluster_flush(cl.handle))
-            if last in group_of:
-                flush(group_of[last], last)
 
     def timed(first, evs=None, markers=False):
         """`steps` steps from step index `first`, bracketed by barrier + synchronize: wall seconds."""
@@ -780,7 +756,6 @@ def measure(args, w, rank, world, stream, comm_stream):
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(first + i, evs[i] if evs else None, markers)
-        finish(first + args.steps - 1)
         torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
         if world > 1:
             dist.barrier()
@@ -791,7 +766,6 @@ def measure(args, w, rank, world, stream, comm_stream):
     plan(0, args.warmup)
     for k in range(args.warmup):
         step(k)
-    finish(args.warmup - 1)
     acc.sync(stream)
     torch.cuda.synchronize()
     tevs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
@@ -812,8 +786,7 @@ def measure(args, w, rank, world, stream, comm_stream):
         totals_ms = [b.elapsed_time(c) for _, b, c, _ in tevs]
     else:  # kernels only: interval start -> end, partial sums start -> end
         kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
-        # fused: the partial sums run inside the interval launch (kernel_ms includes them)
-        totals_ms = [0.0 for _ in tevs] if fuse else [c.elapsed_time(d) for _, _, c, d in tevs]
+        totals_ms = [c.elapsed_time(d) for _, _, c, d in tevs]
     if isinstance(handoff_ev, ctypes.c_void_p):  # the raw device-scope handoff event (ablation)
         torch.cuda.synchronize()
         lib.hipEventDestroy(handoff_ev)
@@ -926,13 +899,8 @@ def main():
             "shard_of": args.shard_of,
             "cluster_totals": ("kacc_allreduce_exports (interval exports; partial sums + RCCL on the comm stream)"
                                if args.totals == "exports" else
-                               (f"kacc_cluster_partials_deferred every step (the partial sums of step k inside step "
-                                f"k+1's interval launch, the last step's by kacc_cluster_flush) + one "
-                                f"kacc_allreduce_sums per {max(1, args.allreduce_every)} steps (comm stream)"
-                                if w.fused_partials else
-                                f"kacc_cluster_partials every step (from the tables, compute stream) + one "
-                                f"kacc_allreduce_sums per {max(1, args.allreduce_every)} steps (comm stream)")),
-            "fused_partials": w.fused_partials,
+                               f"kacc_cluster_partials every step (from the tables, compute stream) + one "
+                               f"kacc_allreduce_sums per {max(1, args.allreduce_every)} steps (comm stream)"),
             "allreduce_every": None if args.totals == "exports" else max(1, args.allreduce_every),
             "parallelism": f"node-sharded x{world} (shard.plan_node_ranges); namespace + cluster node "
                            f"totals all-reduced over RCCL inside libkepler_accel",
@@ -941,8 +909,7 @@ def main():
         "kernel_ms": k_avg_ms,
         "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
         "step_minus_kernel_ms": wall_max * 1e3 / args.steps - k_avg_ms * K,
-        # the partial-sum kernel (launch) / interval end -> its end; 0 when fused into the interval launch
-        "totals_compute_ms": float(np.mean(totals_ms)),
+        "totals_compute_ms": float(np.mean(totals_ms)),  # the partial-sum kernel (launch) / interval end -> its end
         "kernel_timing": {
             "step_events": args.step_events,
             "ms_per_step_timing_pass": wall_ev * 1e3 / args.steps,

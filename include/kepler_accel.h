@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define KACC_ABI_VERSION 5u
+#define KACC_ABI_VERSION 4u
 #define KACC_MAX_ZONES 8u
 
 /* Status codes. */
@@ -465,27 +465,6 @@ int kacc_cluster_partials(kacc_cluster *c, uint32_t n_ns, const uint32_t *const 
                           double *const *out_node_power, void *const *streams);
 int kacc_allreduce_sums(kacc_cluster *c, uint64_t *const *energy, uint64_t n_e, double *const *power,
                         uint64_t n_p, void *const *streams, void *const *comm_streams);
-/* kacc_cluster_partials, deferred (ABI 5): arguments as kacc_cluster_partials,
- * but nothing is launched now.  Each shard records the request, and the partial
- * sums of its snapshot AS IT IS NOW are computed inside the shard's next
- * kacc_run_interval / kacc_run_intervals(count 1) launch on the same stream when
- * that interval takes the fast path (KACC_F_FAST_NODES without
- * KACC_F_SMALL_NODES): the request's workgroups come first in that grid and the
- * new interval's workgroups wait for them before overwriting what they read (no
- * extra launch, and the sums overlap the interval).  Otherwise — another
- * stream, another kernel, kacc_table_upload, kacc_reset (which drops it), a
- * second request — the request is launched on its own first, on the stream it
- * was made on.  kacc_cluster_flush launches every shard's pending request now.
- * The out_* rows are complete when that launch is; results are bit-identical
- * to kacc_cluster_partials'.  A cluster that reduces K intervals with one
- * kacc_allreduce_sums defers each interval's partial sums and issues the
- * collective of intervals k0..k1 after interval k1 + 1 is queued (or after a
- * flush).                                                                  */
-int kacc_cluster_partials_deferred(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
-                                   const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
-                                   double *const *out_power, uint64_t *const *out_node_energy,
-                                   double *const *out_node_power, void *const *streams);
-int kacc_cluster_flush(kacc_cluster *c);
 /* The same cluster totals from the interval's exports (kacc_interval.pod_export
  * / node_export) instead of the state tables: nothing runs on streams[s]
  * except an event record — the partial sums run on comm_streams[s] after the

@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KACC_LIB", os.path.join(_HERE, "lib", "libkepler_accel.so"))  # KACC_LIB: A/B builds
 
-KACC_ABI_VERSION = 5
+KACC_ABI_VERSION = 4
 KACC_MAX_ZONES = 8
 KACC_OK = 0
 KACC_EINVAL = -1
@@ -146,8 +146,6 @@ EXPORTS = [
     "kacc_cluster_info",
     "kacc_allreduce_namespaces",
     "kacc_cluster_partials",
-    "kacc_cluster_partials_deferred",
-    "kacc_cluster_flush",
     "kacc_allreduce_sums",
     "kacc_allreduce_exports",
     "kacc_gather_pods",
@@ -305,8 +303,6 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_cluster_rccl.argtypes = [POINTER(c_int), c_char_p, ctypes.c_size_t]
     lib.kacc_allreduce_namespaces.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 8
     lib.kacc_cluster_partials.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 7
-    lib.kacc_cluster_partials_deferred.argtypes = [c_void_p, c_uint32] + [POINTER(c_void_p)] * 7
-    lib.kacc_cluster_flush.argtypes = [c_void_p]
     lib.kacc_allreduce_sums.argtypes = [c_void_p, POINTER(c_void_p), c_uint64, POINTER(c_void_p), c_uint64,
                                         POINTER(c_void_p), POINTER(c_void_p)]
     lib.kacc_allreduce_exports.argtypes = [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_uint32),
@@ -930,24 +926,6 @@ class Cluster:
             _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
             _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
             _ptrs(streams) if streams else None))
-
-    def partials_deferred(self, n_ns: int, ns_pod_off, ns_pod_slot, out_energy, out_power, out_node_energy=None,
-                          out_node_power=None, streams=None) -> None:
-        """kacc_cluster_partials_deferred: the partial sums of the snapshot as it is now, computed inside
-        each shard's next fast-path interval launch on the same stream (or on their own: flush)."""
-        n = len(self.shards)
-        if n_ns and not (len(ns_pod_off) == len(ns_pod_slot) == len(out_energy) == len(out_power) == n):
-            raise ValueError("one namespace CSR and output pair per local shard")
-        node = out_node_energy is not None
-        self._check(self.lib.kacc_cluster_partials_deferred(
-            self.handle, n_ns, _ptrs(ns_pod_off) if n_ns else None, _ptrs(ns_pod_slot) if n_ns else None,
-            _ptrs(out_energy) if n_ns else None, _ptrs(out_power) if n_ns else None,
-            _ptrs(out_node_energy) if node else None, _ptrs(out_node_power) if node else None,
-            _ptrs(streams) if streams else None))
-
-    def flush(self) -> None:
-        """kacc_cluster_flush: every shard's pending deferred partial sums, launched now."""
-        self._check(self.lib.kacc_cluster_flush(self.handle))
 
     def allreduce_sums(self, energy, n_e: int, power, n_p: int, streams=None, comm_streams=None) -> None:
         """kacc_allreduce_sums: in-place sum over shards and ranks of per-shard u64 [n_e] / f64 [n_p]

@@ -518,45 +518,6 @@ int kacc_cluster_partials(kacc_cluster *c, uint32_t n_ns, const uint32_t *const 
                         streams);
 }
 
-int kacc_cluster_partials_deferred(kacc_cluster *c, uint32_t n_ns, const uint32_t *const *ns_pod_off,
-                                   const uint32_t *const *ns_pod_slot, uint64_t *const *out_energy,
-                                   double *const *out_power, uint64_t *const *out_node_energy,
-                                   double *const *out_node_power, void *const *streams) {
-  if (!c) return KACC_EINVAL;
-  kacc_ctx *c0 = c->shards[0];
-  const size_t ns = c->shards.size();
-  const bool nodes = out_node_energy && out_node_power;
-  if ((out_node_energy != nullptr) != (out_node_power != nullptr))
-    return kacc_fail(c0, KACC_EINVAL, "node totals need both output arrays");
-  if (n_ns && (!ns_pod_off || !ns_pod_slot || !out_energy || !out_power))
-    return kacc_fail(c0, KACC_EINVAL, "NULL argument");
-  for (size_t s = 0; s < ns; ++s) {
-    if (n_ns && (!ns_pod_off[s] || !ns_pod_slot[s] || !out_energy[s] || !out_power[s]))
-      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL namespace array", s);
-    if (nodes && (!out_node_energy[s] || !out_node_power[s]))
-      return kacc_fail(c0, KACC_EINVAL, "shard %zu: NULL node-total array", s);
-  }
-  for (size_t s = 0; s < ns; ++s) {
-    kacc_ctx *x = c->shards[s];
-    const int rc = kacc_internal_defer_partials(
-        x, n_ns, n_ns ? ns_pod_off[s] : nullptr, n_ns ? ns_pod_slot[s] : nullptr, n_ns ? out_energy[s] : nullptr,
-        n_ns ? out_power[s] : nullptr, nodes ? out_node_energy[s] : nullptr, nodes ? out_node_power[s] : nullptr,
-        shard_stream(c, streams, s));
-    if (rc != KACC_OK) return kacc_fail(c0, rc, "shard %zu: %s", s, std::string(x->err).c_str());
-  }
-  return KACC_OK;
-}
-
-int kacc_cluster_flush(kacc_cluster *c) {
-  if (!c) return KACC_EINVAL;
-  for (size_t s = 0; s < c->shards.size(); ++s) {
-    kacc_ctx *x = c->shards[s];
-    const int rc = kacc_internal_flush_partials(x);
-    if (rc != KACC_OK) return kacc_fail(c->shards[0], rc, "shard %zu: %s", s, std::string(x->err).c_str());
-  }
-  return KACC_OK;
-}
-
 int kacc_allreduce_sums(kacc_cluster *c, uint64_t *const *energy, uint64_t n_e, double *const *power, uint64_t n_p,
                         void *const *streams, void *const *comm_streams) {
   if (!c) return KACC_EINVAL;

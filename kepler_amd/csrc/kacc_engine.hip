@@ -134,10 +134,6 @@ constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node 
 #ifndef KACC_CHUNK_WAVES
 #define KACC_CHUNK_WAVES 4
 #endif
-#ifndef KACC_CHUNK_LATE_PREV
-#define KACC_CHUNK_LATE_PREV 0
-#endif
-constexpr bool kChunkLatePrev = KACC_CHUNK_LATE_PREV != 0;
 constexpr int kChunkThreads = KACC_CHUNK_THREADS;
 constexpr int kChunkRpt = 4;
 constexpr int kChunkRows = kChunkRpt * kChunkThreads;  // big-node rows per chunk item
@@ -157,8 +153,6 @@ constexpr uint32_t kErrSlot = 1u << 2;
 constexpr uint32_t kErrNs = 1u << 3;
 constexpr uint32_t kErrCapacity = 1u << 4;
 constexpr uint32_t kErrBigNode = 1u << 5;  // oversized node under KACC_F_FAST_NODES
-constexpr uint32_t kErrFused = 1u << 9;    // fused partial sums not done within kFusedMaxSpins (never seen)
-constexpr uint32_t kFusedMaxSpins = 200000;  // x s_sleep(8): ~50 ms, then the node block goes on (flagged)
 static_assert(kRowsLds == KACC_FAST_MAX_PROCS && kTpb<0> == KACC_FAST_MAX_AGGREGATES,
               "KACC_FAST_* must match the fast path's capacity");
 
@@ -220,26 +214,12 @@ struct DevState {
   // phase skips them; pod_kernel keeps the list for the next interval
   uint32_t items_given, keep_items;
   uint64_t *stamps;  // kVarStamps only
-  // Deferred cluster partial sums of the PREVIOUS snapshot fused into this launch
-  // (kacc_cluster_partials_deferred): blocks [0, fp_blocks) of interval_kernel are
-  // namespace blocks [0, fp_ns_blocks) and node-total column blocks; every wave of
-  // them adds 1 to *fp_ctr when its loads are done, and a node block waits for
-  // *fp_ctr to reach fp_target before its first store into a table they read (the
-  // five node-total tables, deferred to the end, and the pod records)
-  uint32_t fp_blocks, fp_ns_blocks, fp_n_ns, fp_target;
-  uint32_t *fp_ctr;
-  const uint32_t *fp_off, *fp_slots;
-  uint64_t *fp_out_e;
-  double *fp_out_p;
-  NodeTotalsArgs fp_na;
 };
 
 struct NodeShared {
   uint64_t active_energy[KACC_MAX_ZONES];
   double power[KACC_MAX_ZONES];
   double active_power[KACC_MAX_ZONES];
-  uint64_t active_total[KACC_MAX_ZONES], idle_total[KACC_MAX_ZONES];  // fused partials: stored late
-  double idle_power[KACC_MAX_ZONES];
   double node_delta;
   uint32_t first;
 };
@@ -674,7 +654,7 @@ __device__ __forceinline__ void attribute_group_masked(const Attr<Z> &a, const N
 // Phase A for one zone (thread z < Z): node.go:10-84 / node.go:101-131.
 template <int Z>
 __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState &st, uint32_t n,
-                                          int z, NodeShared &sh, bool defer_totals = false) {
+                                          int z, NodeShared &sh) {
   const bool first = st.node_has_prev[n] == 0u;
   const uint64_t i = static_cast<uint64_t>(n) * Z + z;
   const double ratio = b.node_usage_ratio[n];
@@ -696,20 +676,14 @@ __device__ __forceinline__ void node_zone(const kacc_interval &b, const DevState
     ap = p * ratio;
     ip = p - ap;
   }
+  st.node_active_total[i] = at;
+  st.node_idle_total[i] = it;
   export_node_zone<Z>(b, n, static_cast<uint32_t>(z), at, it, p, ap, ip);
   st.node_energy_total[i] = abs_e;
   st.node_active_energy[i] = active;
-  if (defer_totals) {  // read by fused partial sums of the previous snapshot: stored by node_totals_out
-    sh.active_total[z] = at;
-    sh.idle_total[z] = it;
-    sh.idle_power[z] = ip;
-  } else {
-    st.node_active_total[i] = at;
-    st.node_idle_total[i] = it;
-    st.node_power[i] = p;
-    st.node_active_power[i] = ap;
-    st.node_idle_power[i] = ip;
-  }
+  st.node_power[i] = p;
+  st.node_active_power[i] = ap;
+  st.node_idle_power[i] = ip;
   sh.active_energy[z] = active;
   sh.power[z] = p;
   sh.active_power[z] = ap;
@@ -934,52 +908,6 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
   }
 }
 
-// Fused deferred partial sums (DevState::fp_*): one block of the previous
-// snapshot's cluster partial sums inside interval_kernel (512 threads: 32
-// namespaces per namespace block; a node-total column block uses lanes < kBlock,
-// so both sum in the standalone kernel's order, bit for bit).  Every wave counts
-// itself once its loads are done: a node block's stores into the tables these
-// blocks read wait for the count (fused_wait), so no snapshot value is read after
-// the new interval overwrote it.
-template <int Z>
-__device__ __forceinline__ void fused_partials_block(const DevState &st, uint32_t pb) {
-  __shared__ uint64_t s_col[kBlock / 64];
-  if (pb < st.fp_ns_blocks)
-    namespace_block<Z, 2 * Z, kTpb<0>>(pb, st.fp_n_ns, st.fp_off, st.fp_slots, st.pod_energy, st.pod_power,
-                                       st.pod_slots, st.fp_out_e, st.fp_out_p, st.err);
-  else
-    node_column_block<Z>(st.fp_na, pb - st.fp_ns_blocks, s_col);
-  // the wave's loads returned (their values are summed): count the wave
-  if ((threadIdx.x & 63u) == 0) __hip_atomic_fetch_add(st.fp_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// A node block before its first store into a table the fused partial sums read.
-// The partial-sum blocks come first in the grid and never wait, so the count is
-// reached; the bound only turns a broken assumption into a flagged error, never a hang.
-__device__ __forceinline__ void fused_wait(const DevState &st) {
-  if (threadIdx.x == 0) {
-    uint32_t spins = 0;
-    while (static_cast<int32_t>(__hip_atomic_load(st.fp_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                                st.fp_target) < 0) {
-      if (++spins > kFusedMaxSpins) {
-        raise_err(st.err, kErrFused);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);
-    }
-  }
-  __syncthreads();
-}
-// The node-total tables node_zone left in LDS (fused partial sums in flight).
-template <int Z>
-__device__ __forceinline__ void node_totals_out(const DevState &st, uint32_t n, int z, const NodeShared &sh) {
-  const uint64_t i = static_cast<uint64_t>(n) * Z + z;
-  st.node_active_total[i] = sh.active_total[z];
-  st.node_idle_total[i] = sh.idle_total[z];
-  st.node_power[i] = sh.power[z];
-  st.node_active_power[i] = sh.active_power[z];
-  st.node_idle_power[i] = sh.idle_power[z];
-}
-
 // One node snapshot of one interval on workgroup `blk` (interval_kernel).
 template <int Z, int V>
 __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevState &st, const uint32_t blk) {
@@ -1045,8 +973,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   const uint32_t rows = p1 - p0, nc = c1 - c0, nv = v1 - v0, nq = q1 - q0;
 
   // ---- A: node zones (threads z < Z) ------------------------------------------
-  const bool fused = st.fp_blocks != 0;  // the previous snapshot's partial sums run in this launch
-  if (tid < Z) node_zone<Z>(b, st, n, tid, sh, fused);
+  if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
 
   // ======================= fast path: one node fits the block ===================
   // Every global load the node needs is issued here, before the first barrier:
@@ -1305,15 +1232,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
     if (role == 3) export_pod<Z>(b, q0 + j, E, P);
   };
-  auto fused_sync = [&]() {  // before the first store into a table the fused partial sums read
-    if (!fused) return;
-    fused_wait(st);
-    if (tid < Z) node_totals_out<Z>(st, n, tid, sh);
-  };
-  if constexpr (!kLateAgg<V>) {
-    fused_sync();
-    aggregate_out();
-  }
+  if constexpr (!kLateAgg<V>) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
     if constexpr (kRowSweep) {
 #pragma unroll
@@ -1363,10 +1282,7 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       store_proc<Z, kNtScat>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   }
-  if constexpr (kLateAgg<V>) {
-    fused_sync();
-    aggregate_out();
-  }
+  if constexpr (kLateAgg<V>) aggregate_out();
   if constexpr (kStamp) {
     __syncthreads();
     if (tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
@@ -1379,15 +1295,7 @@ template <int Z, int V>
 #endif
 __global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
 void interval_kernel(const kacc_interval b, const DevState st) {
-  uint32_t blk = blockIdx.x;
-  if (st.fp_blocks) {  // the previous snapshot's deferred partial sums first (grid-uniform)
-    if (blk < st.fp_blocks) {
-      fused_partials_block<Z>(st, blk);
-      return;
-    }
-    blk -= st.fp_blocks;
-  }
-  interval_node<Z, V>(b, st, blk);
+  interval_node<Z, V>(b, st, blockIdx.x);
 }
 
 // ============ K intervals in one launch, state carried on chip ====================
@@ -2728,33 +2636,28 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     }
     uint64_t prev[kR][Z];
     uint32_t contig = 0;
-    // the rows' previous totals: loaded with the Δ / slot words (KACC_CHUNK_LATE_PREV 0), or
-    // after the aggregates (1: not live across the container / pod phases; slot words from LDS)
-    auto load_prev = [&](const uint32_t (&wsrc)[kR], int u0, int u1) {
-      if constexpr ((V & kVarSkipProcs) == 0) {
+    if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-        for (int u = u0; u < u1; ++u) {
-          const uint64_t sl = wsrc[u] & KACC_SLOT_MASK;
-          if constexpr (kT) {
-            const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
-            const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
-                              s0 + 64 <= st.proc_slots;
-            if (__all(mine)) {
-              contig |= 1u << u;
-              load_group_masked<Z, false, kNtLd>(st.proc_energy, s0, 64u, s0, prev[u]);
-              continue;
-            }
-          }
-          if (sl < st.proc_slots) {
-            load_row<Z>(st.proc_energy, sl, prev[u]);
-          } else {
-#pragma unroll
-            for (int z = 0; z < Z; ++z) prev[u][z] = 0;
+      for (int u = 0; u < kR; ++u) {
+        const uint64_t sl = w[u] & KACC_SLOT_MASK;
+        if constexpr (kT) {
+          const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
+          const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
+                            s0 + 64 <= st.proc_slots;
+          if (__all(mine)) {
+            contig |= 1u << u;
+            load_group_masked<Z, false, kNtLd>(st.proc_energy, s0, 64u, s0, prev[u]);
+            continue;
           }
         }
+        if (sl < st.proc_slots) {
+          load_row<Z>(st.proc_energy, sl, prev[u]);
+        } else {
+#pragma unroll
+          for (int z = 0; z < Z; ++z) prev[u][z] = 0;
+        }
       }
-    };
-    if constexpr (!kChunkLatePrev) load_prev(w, 0, kR);
+    }
     // aggregate j of this chunk: containers [cb, ce), VMs [vb, ve), pods [qb, qe)
     const uint32_t ctr_rows_end = rg.c1 > rg.c0 ? b.ctr_proc_end[rg.c1 - 1] : rg.p0;
     auto agg = [&](uint32_t j, uint32_t &beg, uint32_t &end, uint32_t &wd) -> uint32_t {
@@ -2901,22 +2804,9 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       else
         raise_err(st.err, kErrCapacity);
     }
-    // late previous totals: KACC_CHUNK_LATE_PREV groups of rows at a time
-    constexpr int kLB = kChunkLatePrev ? KACC_CHUNK_LATE_PREV : kR;
-#pragma unroll
-    for (int ub = 0; ub < kR; ub += kLB) {
-    if constexpr (kChunkLatePrev) {
-      uint32_t wl[kR];
-#pragma unroll
-      for (int u = ub; u < ub + kLB; ++u) {
-        const uint32_t r = utid + u * kThreads;
-        wl[u] = r < rows ? s_w[r] : 0xffffffffu;
-      }
-      load_prev(wl, ub, ub + kLB);
-    }
     if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-      for (int u = ub; u < ub + kLB; ++u) {
+      for (int u = 0; u < kR; ++u) {
         const uint32_t r = utid + u * kThreads;
         if constexpr (kT) {
           if (contig & (1u << u)) {
@@ -2939,7 +2829,6 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
       }
     }
-    }  // ub
     // aggregates beyond one per lane (chunks of mostly empty containers):
     // containers / VMs here, their pods always deferred
     for (uint32_t j = kThreads + utid; j < nagg; j += kThreads) {
@@ -3208,12 +3097,6 @@ kacc::DevState dev_state(const kacc_ctx *ctx) {
   s.items_given = 0;
   s.keep_items = 0;
   s.stamps = nullptr;
-  s.fp_blocks = s.fp_ns_blocks = s.fp_n_ns = s.fp_target = 0;
-  s.fp_ctr = nullptr;
-  s.fp_off = s.fp_slots = nullptr;
-  s.fp_out_e = nullptr;
-  s.fp_out_p = nullptr;
-  s.fp_na = kacc::NodeTotalsArgs{};
   return s;
 }
 
@@ -3233,7 +3116,7 @@ void launch_small(const kacc_interval &b, const kacc::DevState &s, hipStream_t s
 template <int Z, int V>
 void launch_zv(const kacc_interval &b, const kacc::DevState &s, hipStream_t st) {
   if (V == 0 && (b.flags & KACC_F_SMALL_NODES)) return launch_small<Z>(b, s, st);
-  KACC_LAUNCH((kacc::interval_kernel<Z, V>), dim3(b.n_nodes + s.fp_blocks), dim3(kacc::kTpb<V>),
+  KACC_LAUNCH((kacc::interval_kernel<Z, V>), dim3(b.n_nodes), dim3(kacc::kTpb<V>),
               KACC_FAST_EXTRA_LDS, st, b, s);
   if (b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES)) return;
   const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
@@ -3307,36 +3190,6 @@ kacc::NodeTotalsArgs node_totals_args(const kacc_ctx *ctx, uint64_t live, const 
   na.out_p = node_power;
   na.node_export = node_export;
   return na;
-}
-
-// A deferred partial-sum request (kacc_internal_defer_partials) launched on its own,
-// on the stream it was made on: before anything else writes the tables it reads.
-int flush_deferred(kacc_ctx *ctx) {
-  if (!ctx->deferred.pending) return KACC_OK;
-  const kacc_ctx::Deferred d = ctx->deferred;
-  ctx->deferred.pending = false;
-  return kacc_internal_export_partials(ctx, d.n_ns, d.off, d.slots, nullptr, 0, nullptr, 0, 0, d.out_e, d.out_p,
-                                       d.node_e, d.node_p, d.stream);
-}
-
-// The deferred request fused into this interval_kernel launch (its first blocks).
-void fuse_deferred(kacc_ctx *ctx, kacc::DevState &ds) {
-  const kacc_ctx::Deferred d = ctx->deferred;
-  ctx->deferred.pending = false;
-  const uint32_t ns_per_block = kacc::kTpb<0> / kacc::kNsLanes;
-  ds.fp_ns_blocks = (d.n_ns + ns_per_block - 1) / ns_per_block;
-  const uint32_t col_blocks = d.node_e ? 5u * ctx->cfg.zones : 0u;
-  ds.fp_blocks = ds.fp_ns_blocks + col_blocks;
-  ds.fp_n_ns = d.n_ns;
-  ds.fp_off = d.off;
-  ds.fp_slots = d.slots;
-  ds.fp_out_e = d.out_e;
-  ds.fp_out_p = d.out_p;
-  ds.fp_na = node_totals_args(ctx, std::min<uint64_t>(ctx->live_nodes, ctx->cfg.nodes), nullptr, d.node_e, d.node_p);
-  ds.fp_ctr = ctx->d_ctr + 3;
-  ctx->fp_issued += ds.fp_blocks * static_cast<uint32_t>(kacc::kTpb<0> / 64);  // every wave counts once
-  ds.fp_target = ctx->fp_issued;
-  if (!ds.fp_blocks) ds.fp_target = 0;
 }
 
 // pod_export NULL: the namespace sums gather the state tables by pod slot;
@@ -3692,8 +3545,6 @@ int kacc_reset(kacc_ctx *ctx) {
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->live_nodes = 0;
-  ctx->deferred.pending = false;  // a reset snapshot has no partial sums to compute
-  ctx->fp_issued = 0;             // d_ctr[3] is zero again
   return KACC_OK;
 }
 
@@ -3712,51 +3563,24 @@ int kacc_run_interval(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   return run_one(ctx, b, stream);
 }
 
-// One interval (kacc_run_interval, kacc_run_intervals of one): a pending deferred
-// partial-sum request rides in its launch when it can.
+// One interval (kacc_run_interval, kacc_run_intervals of one).
 static int run_one(kacc_ctx *ctx, const kacc_interval *b, void *stream) {
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  // a deferred partial-sum request of the snapshot so far: fused into this launch
-  // when it is a fast-path launch on the request's stream, else launched first
-  const bool fuse = ctx->deferred.pending && b->n_nodes && st == ctx->deferred.stream &&
-                    (b->flags & KACC_F_FAST_NODES) && !(b->flags & KACC_F_SMALL_NODES);
-  if (!fuse && (rc = flush_deferred(ctx)) != KACC_OK) return rc;
   if (b->n_nodes == 0) {  // an emptied batch: no node of it counts in the cluster totals
     ctx->live_nodes = 0;
     return KACC_OK;
   }
   if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  kacc::DevState ds = dev_state(ctx);
-  if (fuse) fuse_deferred(ctx, ds);
-  launch(ctx->cfg.zones, *b, ds, st);
+  launch(ctx->cfg.zones, *b, dev_state(ctx), st);
   KACC_HIP(ctx, hipGetLastError());
   ctx->live_nodes = b->n_nodes;
   return KACC_OK;
 }
 
-int kacc_internal_defer_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
-                                 uint64_t *out_energy, double *out_power, uint64_t *node_energy, double *node_power,
-                                 void *stream) {
-  if (!ctx) return KACC_EINVAL;
-  if (n_ns && (!off || !slots || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
-  if ((node_energy != nullptr) != (node_power != nullptr))
-    return fail(ctx, KACC_EINVAL, "node totals need both output arrays");
-  int rc = flush_deferred(ctx);  // one request at a time
-  if (rc != KACC_OK) return rc;
-  if (!n_ns && !node_energy) return KACC_OK;
-  ctx->deferred = kacc_ctx::Deferred{true, n_ns, off, slots, out_energy, out_power, node_energy, node_power,
-                                     stream ? static_cast<hipStream_t>(stream) : ctx->stream};
-  return KACC_OK;
-}
-
-int kacc_internal_flush_partials(kacc_ctx *ctx) {
-  if (!ctx) return KACC_EINVAL;
-  return flush_deferred(ctx);
-}
 
 // K consecutive intervals in one call (fleet replay, BASELINE config 5's 60
 // batched intervals): interval k+1 reads the state interval k wrote, so the
@@ -3777,9 +3601,8 @@ int kacc_run_intervals(kacc_ctx *ctx, const kacc_interval *dev_batches, uint32_t
     max_pods = std::max<uint64_t>(max_pods, dev_batches[k].n_pods);
   }
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  int rc = flush_deferred(ctx);
+  int rc = ensure_items(ctx, max_nodes, max_procs, max_pods);
   if (rc != KACC_OK) return rc;
-  if ((rc = ensure_items(ctx, max_nodes, max_procs, max_pods)) != KACC_OK) return rc;
   (void)hipGetLastError();  // clear a stale error of an earlier call
   const kacc::DevState ds = dev_state(ctx);
   // one launch for all K intervals when every node stays in one workgroup's
@@ -4027,7 +3850,6 @@ int kacc_batch_alloc(kacc_ctx *ctx, const kacc_shape *shape, kacc_batch **out, k
 // buffers are not overwritten before its previous kernels have read them.
 int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
   if (!ctx || !bt) return KACC_EINVAL;
-  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   const uint32_t K = bt->cap.intervals;
   const uint64_t Z = ctx->cfg.zones;
   std::vector<kacc_interval> dv(K);
@@ -4149,10 +3971,6 @@ static int table_copy(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
                 (unsigned long long)ctx->counts[t]);
   if (kTables[t].derived && !down)
     return fail(ctx, KACC_EINVAL, "table %d is derived on read and cannot be uploaded", (int)t);
-  if (!down) {  // a deferred partial-sum request reads the tables before they change
-    const int frc = flush_deferred(ctx);
-    if (frc != KACC_OK) return frc;
-  }
   if (!count) return KACC_OK;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -4228,8 +4046,6 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
                                   uint64_t *node_energy,
                                   double *node_power, void *stream) {
   if (!ctx) return KACC_EINVAL;
-  int frc = flush_deferred(ctx);  // a deferred request reads the snapshot first
-  if (frc != KACC_OK) return frc;
   const kacc::TimingScope timing(ctx);
   if (n_ns && (!off || !rows || !out_energy || !out_power)) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
@@ -4350,7 +4166,6 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
 int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream, int variant,
                             uint64_t *d_out) {
   if (!ctx || !b || count == 0 || !d_out) return KACC_EINVAL;
-  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -4373,7 +4188,6 @@ int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t coun
 int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream,
                                      int variant) {
   if (!ctx || !b || count == 0) return KACC_EINVAL;
-  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
@@ -4401,7 +4215,6 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint
 // other than 0 does NOT compute the reference semantics.
 int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *b, void *stream, uint64_t *d_out) {
   if (!ctx || !d_out) return KACC_EINVAL;
-  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;
@@ -4420,7 +4233,6 @@ int kacc_debug_interval_stamps(kacc_ctx *ctx, const kacc_interval *b, void *stre
 
 int kacc_debug_run_variant(kacc_ctx *ctx, const kacc_interval *b, void *stream, int variant) {
   if (!ctx) return KACC_EINVAL;
-  if (const int frc = flush_deferred(ctx); frc != KACC_OK) return frc;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   int rc = check_shape(ctx, b);
   if (rc != KACC_OK) return rc;

@@ -24,7 +24,7 @@ struct kacc_ctx {
   void *tables[KACC_T_COUNT] = {};
   uint64_t counts[KACC_T_COUNT] = {};
   uint32_t *d_err = nullptr;
-  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods, [3] fused partial-sum waves
+  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
   kacc::ChunkItem *d_items = nullptr;
   uint32_t item_cap = 0;
   uint2 *d_defer = nullptr;
@@ -35,20 +35,6 @@ struct kacc_ctx {
   hipEvent_t batch_copied = nullptr;
   uint32_t live_nodes = 0;  // n_nodes of the last interval run: the nodes the cluster totals sum
   hipEvent_t time_start = nullptr, time_stop = nullptr;  // kacc_time_next_launch (one call)
-  // kacc_cluster_partials_deferred: the partial sums of the snapshot as it is now,
-  // fused into the next fast-path kacc_run_interval on `stream` (its first blocks),
-  // or launched on their own before anything else writes the tables
-  struct Deferred {
-    bool pending;
-    uint32_t n_ns;
-    const uint32_t *off, *slots;
-    uint64_t *out_e;
-    double *out_p;
-    uint64_t *node_e;
-    double *node_p;
-    hipStream_t stream;
-  } deferred{};
-  uint32_t fp_issued = 0;  // waves of fused partial-sum blocks so far (d_ctr[3] counts them on the device)
   std::string err;
 };
 
@@ -144,14 +130,6 @@ struct kacc_slotmap {
 extern "C" int kacc_internal_cluster_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off,
                                               const uint32_t *slots, uint64_t *out_energy, double *out_power,
                                               uint64_t *node_energy, double *node_power, void *stream);
-
-// The same, deferred: recorded on the context and computed by the next fast-path
-// kacc_run_interval on `stream` inside its own launch, else launched on its own
-// (kacc_internal_flush_partials, or before any call that writes the tables).
-extern "C" int kacc_internal_defer_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *off, const uint32_t *slots,
-                                            uint64_t *out_energy, double *out_power, uint64_t *node_energy,
-                                            double *node_power, void *stream);
-extern "C" int kacc_internal_flush_partials(kacc_ctx *ctx);
 
 // The same from an interval's exports (kacc_interval.pod_export / node_export):
 // namespace k sums the export rows rows[off[k] .. off[k+1]) (< n_pods); with

@@ -428,79 +428,6 @@ def test_cluster_node_totals_back_to_back_launches():
     acc.close()
 
 
-def _fused_pair_run(L, K, mode, seed=53):
-    """Two contexts on the same inputs: A computes the partial sums of each group's last interval
-    with kacc_cluster_partials right after it; B defers them (kacc_cluster_partials_deferred), so
-    the next launch computes them in its first workgroups.  Groups: one interval each ("fused",
-    "upload": a table upload after some intervals, which flushes the request) or, in "multi", every
-    third group two intervals through one kacc_run_intervals (not fusable: the request is launched
-    first).  Returns, per context, the [K] rows of totals and the state tables at the end."""
-    Z, n_ns = L.zones, L.n_namespaces
-    s = current_stream_handle()
-    off, slots = L.namespace_csr()
-    csr = to_device({"o": off, "s": slots})
-    ne, npw = n_ns * Z + 2 * Z, n_ns * Z + 3 * Z
-    groups, k = [], 0
-    while k < K:
-        n = 2 if mode == "multi" and len(groups) % 3 == 2 and k + 1 < K else 1
-        groups.append(list(range(k, k + n)))
-        k += n
-    flags = L.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
-    res = []
-    for deferred in (False, True):
-        acc = accel.Accel(Z, **L.capacities())
-        cl = accel.Cluster.join(acc, accel.Cluster.unique_id(), 1, 0)
-        sim = fleet.FleetSim(L, seed=seed, churn=0.04, read_error_frac=0.05)
-        te = torch.zeros(K, ne, dtype=torch.int64, device="cuda")
-        tp = torch.zeros(K, npw, dtype=torch.float64, device="cuda")
-        keep = []
-        for gi, g in enumerate(groups):
-            ivs = []
-            for _ in g:
-                t = to_device(sim.next_interval())
-                keep.append(t)
-                ivs.append(interval_from_tensors(t, L.sizes(), flags))
-            if len(ivs) == 1:
-                acc.run_interval(ivs[0], s)
-            else:
-                acc.run_intervals(ivs, s)
-            j = g[-1]
-            args = (n_ns, [csr["o"].data_ptr()], [csr["s"].data_ptr()], [te[j].data_ptr()], [tp[j].data_ptr()],
-                    [te[j, n_ns * Z:].data_ptr()], [tp[j, n_ns * Z:].data_ptr()])
-            if deferred:
-                cl.partials_deferred(*args, streams=[s])
-                if mode == "upload" and gi % 4 == 1:  # a write to the tables flushes the request first
-                    acc.upload("node_idle_total", acc.download("node_idle_total"))
-            else:
-                cl.partials(*args, streams=[s])
-        cl.flush()
-        acc.sync(s)
-        res.append((te.cpu().numpy().view(np.uint64).copy(), tp.cpu().numpy().view(np.uint64).copy(),
-                    {name: acc.download(name) for name, _ in accel.TABLES}))
-        cl.close()
-        acc.close()
-    return res
-
-
-@pytest.mark.parametrize("mode", ["fused", "multi", "upload"])
-def test_deferred_partials_bit_identical_to_standalone(mode):
-    """kacc_cluster_partials_deferred fused into the next interval launch (its first workgroups
-    read the snapshot while the new interval's workgroups wait before overwriting the node-total
-    tables and pod records) == kacc_cluster_partials right after each interval, bit for bit: every
-    interval's namespace and node totals, and every state table afterwards.  Also when the
-    request cannot ride (a two-interval kacc_run_intervals, a table upload): it is launched first."""
-    L = fleet.make_layout(40, [2000, 300, 1, 0, 1500, 64, 2048, 900] * 5, 4, seed=53, n_namespaces=11,
-                          shuffle_slots=True)
-    assert L.fast_flag() & accel.KACC_F_FAST_NODES and not L.fast_flag() & accel.KACC_F_SMALL_NODES
-    K = 9
-    (ea, pa, ta), (eb, pb, tb) = _fused_pair_run(L, K, mode)
-    np.testing.assert_array_equal(eb, ea)
-    np.testing.assert_array_equal(pb, pa)
-    for name, _ in accel.TABLES:
-        np.testing.assert_array_equal(tb[name], ta[name], err_msg=name)
-    assert np.count_nonzero(ea[-1]) > 0
-
-
 EXPORT_FLEETS = [
     ("fast-z4", dict(n_nodes=40, procs_per_node=[2000, 300, 1, 0, 1500] * 8, zones=4, shuffle_slots=True), 0),
     ("small-z2", dict(n_nodes=64, procs_per_node=[500, 64, 3, 0] * 16, zones=2), 0),
