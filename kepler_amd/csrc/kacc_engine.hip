@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <atomic>
 #include <thread>
+#include <type_traits>
 #include <cstdarg>
 #include <cstddef>
 #include <cstdio>
@@ -172,8 +173,10 @@ struct ChunkItem {
 // last block to finish add the partials: four dependent round trips, 6.5 us at
 // the 1/8 shard of config 3 against one or two here; and no reliance on how
 // gfx950 performs agent-scope atomics).  Config 3: 40 loads per lane, hidden
-// under the namespace blocks of the same launch.
-constexpr int kColLoads = 8;
+// under the namespace blocks of the same launch.  Past 2 x kColLoads rounds the
+// lanes keep kColLoadsWide loads in flight (config 1, 40k nodes: 157 loads per
+// lane in 5 round trips instead of 20).
+constexpr int kColLoads = 8, kColLoadsWide = 32;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
   const uint64_t *active_total, *idle_total;
@@ -872,22 +875,31 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
   const uint64_t stride = na.node_export ? 5ull * Z : static_cast<uint64_t>(Z);
   unsigned long long e = 0;
   double p = 0.0;
-  for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kColLoads) {
-    uint64_t v[kColLoads];
+  // lane tid adds nodes tid, tid + kBlock, ... in that order whatever the loads per
+  // round: the wide rounds of big fleets give the same bits with fewer round trips
+  auto rounds = [&](auto loads) {
+    constexpr int kL = decltype(loads)::value;
+    for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kL) {
+      uint64_t v[kL];
 #pragma unroll
-    for (int u = 0; u < kColLoads; ++u) {  // unconditional from clamped nodes: all in flight
-      const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
-      v[u] = col[n * stride];
-    }
+      for (int u = 0; u < kL; ++u) {  // unconditional from clamped nodes: all in flight
+        const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
+        v[u] = col[n * stride];
+      }
 #pragma unroll
-    for (int u = 0; u < kColLoads; ++u) {
-      if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
-      if (is_u64)
-        e += v[u];
-      else
-        p = p + __longlong_as_double(static_cast<long long>(v[u]));
+      for (int u = 0; u < kL; ++u) {
+        if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
+        if (is_u64)
+          e += v[u];
+        else
+          p = p + __longlong_as_double(static_cast<long long>(v[u]));
+      }
     }
-  }
+  };
+  if (na.n_nodes > static_cast<uint64_t>(kBlock) * kColLoads * 2)
+    rounds(std::integral_constant<int, kColLoadsWide>{});
+  else
+    rounds(std::integral_constant<int, kColLoads>{});
 #pragma unroll
   for (int sft = 32; sft >= 1; sft >>= 1) {
     e += __shfl_down(e, sft, 64);

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "kacc_debug.h"
@@ -58,6 +59,7 @@ struct Args {
   uint32_t n_nodes, n_rows;
   uint32_t stop_after;  // timing ablation (kacc_debug_join_variant): 0 = full join
   uint32_t reuse;       // KACC_JOIN_REUSE_TERMINATED
+  uint32_t fmt6;        // PID tables of small nodes are 6-B buckets (join_small's kJ6B)
   const uint32_t *row_off;
   const void *keys;
   const uint32_t *node_status;
@@ -119,16 +121,36 @@ struct Tab<uint64_t> {
   __device__ void clear(uint32_t b) const { k[b] = kEmpty; }
 };
 
-template <typename K>
-__device__ __forceinline__ bool is_live(uint64_t raw) {
-  const auto k = Tab<K>::key_of(raw);
-  return k != Tab<K>::kEmpty && k != Tab<K>::kTomb;
+// The PID table of a small node (H <= kLdsBuckets) in 6-B buckets: H u32 keys,
+// then H u16 node-relative slots (S <= 2730), in the node's 8H-byte region;
+// a claim is a CAS on the key, then the slot store (as Tab<uint64_t>).
+struct TabP {
+  static constexpr uint32_t kEmpty = 0xffffffffu, kTomb = 0xfffffffeu;
+  uint32_t *k;
+  uint16_t *s;
+  __device__ uint32_t raw(uint32_t b) const { return k[b]; }
+  __device__ static uint32_t key_of(uint32_t r) { return r; }
+  __device__ uint32_t key(uint32_t b) const { return k[b]; }
+  __device__ uint32_t slot(uint32_t b) const { return s[b]; }
+  __device__ void tomb(uint32_t b) const { k[b] = kTomb; }
+  __device__ bool claim(uint32_t b, uint32_t seen, uint32_t kk, uint32_t ss) const {
+    if (atomicCAS(k + b, seen, kk) != seen) return false;
+    s[b] = static_cast<uint16_t>(ss);
+    return true;
+  }
+  __device__ void clear(uint32_t b) const { k[b] = kEmpty; }
+};
+
+template <typename T, typename R>
+__device__ __forceinline__ bool is_live(R raw) {
+  const auto k = T::key_of(raw);
+  return k != T::kEmpty && k != T::kTomb;
 }
 
 // Linear-probing operations shared by both kernels (hmask = H - 1).
-template <typename K>
+template <typename K, typename T = Tab<K>>
 struct Probe {
-  Tab<K> t;
+  T t;
   uint32_t shift, hmask, H;
   // bucket holding k, or ~0u (stops at the first empty bucket, skips tombstones)
   __device__ uint32_t find(K k) const {
@@ -136,7 +158,7 @@ struct Probe {
     for (uint32_t p = 0; p < H; ++p, b = (b + 1) & hmask) {
       const K kk = static_cast<K>(t.key(b));
       if (kk == k) return b;
-      if (kk == Tab<K>::kEmpty) break;
+      if (kk == T::kEmpty) break;
     }
     return ~0u;
   }
@@ -145,11 +167,11 @@ struct Probe {
   __device__ uint32_t insert(K k, uint32_t rel, uint32_t *fresh = nullptr) const {
     uint32_t b = bucket(k, shift);
     for (uint32_t p = 0; p < H;) {
-      const uint64_t raw = t.raw(b);
-      const K kk = static_cast<K>(Tab<K>::key_of(raw));
-      if (kk == Tab<K>::kEmpty || kk == Tab<K>::kTomb) {
+      const auto raw = t.raw(b);
+      const K kk = static_cast<K>(T::key_of(raw));
+      if (kk == T::kEmpty || kk == T::kTomb) {
         if (t.claim(b, raw, k, rel)) {
-          if (fresh) *fresh += kk == Tab<K>::kEmpty ? 1u : 0u;
+          if (fresh) *fresh += kk == T::kEmpty ? 1u : 0u;
           return b;
         }
         continue;  // lost the race for this bucket: look at it again
@@ -221,7 +243,9 @@ __device__ __forceinline__ bool node_view(const Args &a, uint32_t n, NodeView &v
     v.r1 = min(v.r1, a.n_rows);
     v.r0 = min(v.r0, v.r1);
   }
-  if ((v.H <= kLdsBuckets && v.r1 - v.r0 <= kSmallRows) != kSmall) return false;
+  // under fmt6 every small-table node is join_small's (more rows than kSmallRows
+  // cannot fit its <= 2730 slots: an ERANGE there)
+  if ((v.H <= kLdsBuckets && (a.fmt6 || v.r1 - v.r0 <= kSmallRows)) != kSmall) return false;
   v.S = s1 - v.s0;
   v.shift = 32u - static_cast<uint32_t>(__builtin_ctz(v.H));
   return true;
@@ -266,6 +290,9 @@ constexpr int kJErrReg = 2;    // error bits gathered in a register, one atomic 
 constexpr int kJLdsBar = 4;    // LDS-only barriers (never wait for the node's global stores)
 constexpr int kJInsDup = 8;    // duplicates found by the insert itself (no re-probe pass)
 constexpr int kJScan2 = 16;    // the two block scans of step 3 share their barrier
+constexpr int kJ6B = 32;       // PID tables in 6-B buckets (u32 keys, u16 slots), vector table loads
+constexpr int kJSeenNR = 64;   // seen marks without return; duplicates found by counting (step 3)
+constexpr int kJVec = 128;     // a lane's keys loaded / slot words stored as vectors
 
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -321,14 +348,19 @@ __device__ __forceinline__ void block_scan2(uint32_t v0, uint32_t v1, uint32_t *
 
 template <typename K, int V>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof(K) == 8 ? 4 : 8))) void join_small(const Args a) {
-  using T = Tab<K>;
   constexpr bool kWide = sizeof(K) == 8;
+  constexpr bool k6 = !kWide && (V & kJ6B) != 0;
+  constexpr bool kSplit = kWide || k6;  // a key array and a slot array (else packed entries)
   constexpr bool kLock = (V & kJLock) != 0, kErrReg = (V & kJErrReg) != 0, kInsDup = (V & kJInsDup) != 0;
-  constexpr bool kScan2 = (V & kJScan2) != 0;
-  __shared__ uint64_t s_ent[kLdsBuckets];              // entries (u32 keys) / keys (u64)
-  __shared__ uint32_t s_slot[kWide ? kLdsBuckets : 1];  // slots (u64 keys)
+  constexpr bool kScan2 = (V & kJScan2) != 0, kSeenNR = (V & kJSeenNR) != 0, kVec = (V & kJVec) != 0;
+  using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
+  using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
+  using SlotT = std::conditional_t<k6, uint16_t, uint32_t>;
+  __shared__ __align__(16) EntT s_ent[kLdsBuckets];               // entries (packed PIDs) / keys
+  __shared__ __align__(16) SlotT s_slot[kSplit ? kLdsBuckets : 1];  // slots (split tables)
   __shared__ uint32_t s_used[kSmallWords];  // bit s: slot s held by a live ID
   __shared__ uint32_t s_seen[kSmallWords];  // bit s: a row found slot s
+  __shared__ uint32_t s_dup[kSeenNR ? kSmallWords : 1];  // kSeenNR's error path: marks with return
   __shared__ uint32_t s_fmask[kSmallWords], s_tmask[kSmallWords];  // free / terminated bits
   __shared__ uint32_t s_wpre[kSmallWords];                          // (free << 16 | term) before w
   __shared__ uint16_t s_free[kNewCap];                              // the first free slots
@@ -344,6 +376,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   if (!node_view<true>(a, n, v)) return;
   const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H, hmask = H - 1;
   const uint32_t W = (S + 31) / 32;
+  if constexpr (k6) {
+    if (R > kSmallRows) {  // more rows than the table's <= 2730 slots: ERANGE, map unchanged
+      for (uint32_t r = tid; r < R; r += kThreads) a.out_slot[v.r0 + r] = kInvalid;
+      if (tid == 0) {
+        atomicOr(a.err, kErrRange);
+        a.term_count[n] = 0u;
+        if (a.out_span) {
+          a.out_span[2 * n] = 1u;
+          a.out_span[2 * n + 1] = 0u;
+        }
+      }
+      return;
+    }
+  }
   const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
   T G, L;
   if constexpr (kWide) {
@@ -351,12 +397,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     G.s = a.slots + v.hb;
     L.k = s_ent;
     L.s = s_slot;
+  } else if constexpr (k6) {
+    G.k = reinterpret_cast<uint32_t *>(a.ent + v.hb);
+    G.s = reinterpret_cast<uint16_t *>(G.k + H);
+    L.k = s_ent;
+    L.s = s_slot;
   } else {
     G.e = a.ent + v.hb;
     L.e = s_ent;
   }
   auto lslot = [&](uint32_t b) -> uint32_t { return L.slot(b); };
-  const Probe<K> pr{L, v.shift, hmask, H};
+  const Probe<K, T> pr{L, v.shift, hmask, H};
   uint32_t errs = 0;  // kErrReg: this lane's error bits
   auto raise = [&](uint32_t bits) {
     if constexpr (kErrReg)
@@ -368,18 +419,30 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // ---- 1: table -> LDS, keys -> registers, marks cleared ---------------------------
   // All loads of the phase are issued before the first LDS store (register
   // staging): the node pays one memory round trip, not one per bucket.
+  // kJ6B: lane tid owns buckets [kPer tid, kPer tid + kPer) — 32 B of keys and
+  // 16 B of slots, 16-B aligned (H >= 64 and every node's hb a multiple of 64)
   constexpr int kPer = kLdsBuckets / kThreads;
+  auto bucket_of = [&](int j) -> uint32_t { return k6 ? tid * kPer + j : tid + j * kThreads; };
   K key[kRpl];
   uint32_t res[kRpl];
+  if (kVec && tid * kRpl + kRpl <= R) {  // the lane's rows as one vector (4-B aligned)
+    __builtin_memcpy(key, keys + tid * kRpl, sizeof(key));
+  } else {
 #pragma unroll
-  for (int j = 0; j < kRpl; ++j) {
-    const uint32_t r = tid * kRpl + j;
-    key[j] = r < R ? keys[r] : T::kEmpty;
+    for (int j = 0; j < kRpl; ++j) {
+      const uint32_t r = tid * kRpl + j;
+      key[j] = r < R ? keys[r] : T::kEmpty;
+    }
   }
-  uint64_t ev[kPer];
-  uint32_t sv[kWide ? kPer : 1];
+  EntT ev[kPer];
+  SlotT sv[kSplit ? kPer : 1];
   {
-    if (H) {  // node-uniform; clamped addresses keep the loads unconditional
+    if constexpr (k6) {
+      if (tid * kPer < H) {
+        __builtin_memcpy(ev, __builtin_assume_aligned(G.k + tid * kPer, 16), sizeof(ev));
+        __builtin_memcpy(sv, __builtin_assume_aligned(G.s + tid * kPer, 16), sizeof(sv));
+      }
+    } else if (H) {  // node-uniform; clamped addresses keep the loads unconditional
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const uint32_t b = tid + j * kThreads, bb = b < H ? b : 0u;
@@ -394,10 +457,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     for (uint32_t i = tid; i < W; i += kThreads) {
       s_used[i] = 0u;
       s_seen[i] = 0u;
+      if constexpr (kSeenNR) s_dup[i] = 0u;
     }
     for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
     if (tid == 0) s_occ = 0u;
-    if (H) {
+    if constexpr (k6) {
+      if (tid * kPer < H) {
+        __builtin_memcpy(s_ent + tid * kPer, ev, sizeof(ev));
+        __builtin_memcpy(s_slot + tid * kPer, sv, sizeof(sv));
+      }
+    } else if (H) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j) {
         const uint32_t b = tid + j * kThreads;
@@ -416,13 +485,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     uint32_t occ = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      const uint32_t b = tid + j * kThreads;
-      if (b >= H) break;
+      if (bucket_of(j) >= H) break;
       const auto k = T::key_of(ev[j]);
       occ += k != T::kEmpty ? 1u : 0u;
       if (k == T::kEmpty || k == T::kTomb) continue;
       uint32_t sl;
-      if constexpr (kWide)
+      if constexpr (kSplit)
         sl = sv[j];
       else
         sl = static_cast<uint32_t>(ev[j]);
@@ -431,7 +499,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     occ = wave_sum(occ);
     if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
   }
-  uint32_t mine = 0;  // new rows of this lane
+  uint32_t mine = 0;   // new rows of this lane
+  uint32_t found = 0;  // kSeenNR: rows of this lane that found their ID
   if constexpr (kLock) {
     // every row of the lane probes in lock-step: unconditional LDS reads per depth
     uint32_t pb[kRpl];
@@ -476,7 +545,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         const uint32_t sl = lslot(pb[j]);
         if (sl >= S) continue;
         const uint32_t bit = 1u << (sl & 31);
-        if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
+        if constexpr (kSeenNR) {
+          atomicOr(&s_seen[sl >> 5], bit);
+          ++found;
+        } else if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
           raise(kErrKey);
           continue;
         }
@@ -503,7 +575,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       const uint32_t sl = lslot(b);
       if (sl >= S) continue;
       const uint32_t bit = 1u << (sl & 31);
-      if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
+      if constexpr (kSeenNR) {
+        atomicOr(&s_seen[sl >> 5], bit);
+        ++found;
+      } else if (atomicOr(&s_seen[sl >> 5], bit) & bit) {  // a second row with this ID
         raise(kErrKey);
         continue;
       }
@@ -524,14 +599,32 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     packed = (static_cast<uint32_t>(__popc(fm)) << 16) | static_cast<uint32_t>(__popc(tm));
   }
   uint32_t ptot, ntot, pex, rank0;  // rank0: this lane's first new-row rank
+  // kSeenNR: the found rows ride in the new-row channel's high half (<= 3072 each)
+  const uint32_t chan = kSeenNR ? mine | (found << 16) : mine;
   if constexpr (kScan2) {
-    block_scan2<V>(packed, mine, s_wave, pex, rank0, ptot, ntot);
+    block_scan2<V>(packed, chan, s_wave, pex, rank0, ptot, ntot);
   } else {
     pex = block_scan(packed, s_wave, ptot);
-    rank0 = block_scan(mine, s_wave, ntot);
+    rank0 = block_scan(chan, s_wave, ntot);
   }
   if (tid < W) s_wpre[tid] = pex;
-  const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot;
+  const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot & 0xffffu;
+  if constexpr (kSeenNR) {
+    rank0 &= 0xffffu;
+    // every found row set its slot's seen bit and the seen slots are exactly the
+    // held ones not terminated: fewer of those than found rows = an ID given twice
+    if ((ntot >> 16) != S - total_free - n_term) {  // block-uniform; the error path only
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        if (res[j] >= kPending) continue;
+        const uint32_t sl = res[j] - s0, bit = 1u << (sl & 31);
+        if (atomicOr(&s_dup[sl >> 5], bit) & bit) {  // a second row with this ID
+          raise(kErrKey);
+          res[j] = kInvalid;
+        }
+      }
+    }
+  }
   // KACC_JOIN_REUSE_TERMINATED: new rows take this call's terminated slots first
   // (slot order), then the free ones; otherwise terminated slots are held
   const uint32_t t_first = a.reuse ? n_term : 0u, n_avail = total_free + t_first;
@@ -542,7 +635,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // ---- 4: terminated list (slot order) + tombstones; the first free slots ------------
   if (n_term) {
     for (uint32_t b = tid; b < H; b += kThreads) {
-      if (!is_live<K>(L.raw(b))) continue;
+      if (!is_live<T>(L.raw(b))) continue;
       const uint32_t sl = lslot(b);
       if (sl >= S) continue;
       const uint32_t w = sl >> 5, bit = 1u << (sl & 31);
@@ -699,7 +792,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     jbar<V>();
     for (uint32_t b = tid; b < H; b += kThreads) {
-      if constexpr (kWide) {
+      if constexpr (kSplit) {
         G.k[b] = s_ent[b];
         G.s[b] = s_slot[b];
       } else {
@@ -710,7 +803,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     for (uint32_t w = tid; w < H / 32; w += kThreads) {
       for (uint32_t d = s_dirty[w]; d; d &= d - 1) {
         const uint32_t b = w * 32 + __builtin_ctz(d);
-        if constexpr (kWide) {
+        if constexpr (kSplit) {
           G.k[b] = s_ent[b];
           G.s[b] = s_slot[b];
         } else {
@@ -720,10 +813,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
   }
   uint32_t *__restrict__ out = a.out_slot + v.r0;
+  if (kVec && tid * kRpl + kRpl <= R) {
+    __builtin_memcpy(out + tid * kRpl, res, sizeof(res));
+  } else {
+#pragma unroll
+    for (int j = 0; j < kRpl; ++j)
+      if (tid * kRpl + j < R) out[tid * kRpl + j] = res[j];
+  }
   uint32_t lo = 0xffffffffu, hi = 0u;
 #pragma unroll
   for (int j = 0; j < kRpl; ++j) {
-    if (tid * kRpl + j < R) out[tid * kRpl + j] = res[j];
     if (res[j] != kInvalid) {
       lo = min(lo, res[j] & KACC_SLOT_MASK);
       hi = max(hi, res[j] & KACC_SLOT_MASK);
@@ -783,7 +882,7 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
   } else {
     L.e = a.ent + v.hb;
   }
-  const Probe<K> pr{L, v.shift, H - 1, H};
+  const Probe<K, T> pr{L, v.shift, H - 1, H};
   auto bit_set = [](uint32_t *bm, uint32_t i) {
     return (atomicOr(&bm[i >> 5], 1u << (i & 31)) >> (i & 31)) & 1u;
   };
@@ -797,7 +896,7 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
   __syncthreads();
   if (a.stop_after == 1) return;
   for (uint32_t b = tid; b < H; b += kThreads) {
-    if (!is_live<K>(L.raw(b))) continue;
+    if (!is_live<T>(L.raw(b))) continue;
     const uint32_t s = L.slot(b);
     if (s < S) atomicOr(&s_used[s >> 5], 1u << (s & 31));
   }
@@ -841,7 +940,7 @@ __global__ __launch_bounds__(kThreads) void join_big(const Args a) {
   __syncthreads();
   if (carry) {
     for (uint32_t b = tid; b < H; b += kThreads) {
-      if (!is_live<K>(L.raw(b))) continue;
+      if (!is_live<T>(L.raw(b))) continue;
       const uint32_t s = L.slot(b);
       if (s >= S) continue;
       const uint32_t w = s >> 5, bit = 1u << (s & 31);
@@ -1063,9 +1162,22 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
                      uint32_t stop_after);
 
 namespace {
-constexpr int kJoinDefault = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
-                             kacc::join::kJInsDup | kacc::join::kJScan2;
+// round 2's kernel (8-B packed PID buckets) and the production one
+constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
+                        kacc::join::kJInsDup | kacc::join::kJScan2;
+constexpr int kJoinDefault = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec;
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
+// the variant join_small is launched with (the instantiated ones; else production)
+int launched_variant(int v) {
+  switch (v) {
+    case 0: case 1: case 3: case 6: case 7: case 15: case kJoinR2:
+    case kJoinR2 | kacc::join::kJ6B:
+    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
+    case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
+      return v;
+    default: return kJoinDefault;
+  }
+}
 }  // namespace
 
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
@@ -1131,15 +1243,26 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   (void)hipGetLastError();  // a stale error of an earlier call must not be blamed on this launch
   using namespace kacc::join;
   const dim3 grid(m->n_nodes), block(kThreads);
+  // the table format follows the variant: a map keeps one variant from its reset on
+  const int var = launched_variant(g_join_variant);
+  a.fmt6 = m->kind == KACC_KIND_PROC && (var & kJ6B) ? 1u : 0u;
   auto small = [&](auto key) {
     using K = decltype(key);
-    switch (g_join_variant) {
+    switch (var) {
       case 0: hipLaunchKernelGGL((join_small<K, 0>), grid, block, 0, st, a); break;
       case 1: hipLaunchKernelGGL((join_small<K, 1>), grid, block, 0, st, a); break;
       case 3: hipLaunchKernelGGL((join_small<K, 3>), grid, block, 0, st, a); break;
       case 7: hipLaunchKernelGGL((join_small<K, 7>), grid, block, 0, st, a); break;
       case 15: hipLaunchKernelGGL((join_small<K, 15>), grid, block, 0, st, a); break;
       case 6: hipLaunchKernelGGL((join_small<K, 6>), grid, block, 0, st, a); break;
+      case kJoinR2: hipLaunchKernelGGL((join_small<K, kJoinR2>), grid, block, 0, st, a); break;
+      case kJoinR2 | kJ6B: hipLaunchKernelGGL((join_small<K, kJoinR2 | kJ6B>), grid, block, 0, st, a); break;
+      case kJoinR2 | kJ6B | kJSeenNR:
+        hipLaunchKernelGGL((join_small<K, kJoinR2 | kJ6B | kJSeenNR>), grid, block, 0, st, a);
+        break;
+      case kJoinR2 | kJSeenNR | kJVec:
+        hipLaunchKernelGGL((join_small<K, kJoinR2 | kJSeenNR | kJVec>), grid, block, 0, st, a);
+        break;
       default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
     }
   };
