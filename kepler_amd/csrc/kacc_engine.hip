@@ -1549,7 +1549,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   const uint64_t zi = static_cast<uint64_t>(n) * Z + (tid < static_cast<uint32_t>(Z) ? tid : 0u);
   uint32_t c_has_prev = st.node_has_prev[n];
   int64_t c_ts = st.node_ts[n];
-  uint64_t c_etot = st.node_energy_total[zi], c_atot = st.node_active_total[zi], c_itot = st.node_idle_total[zi];
+  // the zone totals (lanes < Z) are carried in LDS, each lane its own entries: out of
+  // the registers live across the interval loop (a spill at Z = 2, 256 threads)
+  __shared__ uint64_t s_zc[3 * kCarryMaxZ];  // [etot | atot | itot] per zone
+  if (tid < static_cast<uint32_t>(Z)) {
+    s_zc[tid] = st.node_energy_total[zi];
+    s_zc[Z + tid] = st.node_active_total[zi];
+    s_zc[2 * Z + tid] = st.node_idle_total[zi];
+  }
   // carried aggregate (one per lane)
   uint32_t c_role = 0, c_aw = 0xffffffffu;
   uint64_t c_aE[Z];
@@ -1721,6 +1728,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
       uint64_t z_active = 0;
       double z_p = 0.0, z_ap = 0.0, z_ip = 0.0;
       if (tid < static_cast<uint32_t>(Z)) {
+        const uint64_t c_etot = s_zc[tid];
+        uint64_t c_atot = s_zc[Z + tid], c_itot = s_zc[2 * Z + tid];
         if (first) {
           z_active = go_f64_to_u64(u2f(ze) * ratio);
           c_atot = z_active;
@@ -1735,7 +1744,9 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
           z_ap = z_p * ratio;
           z_ip = z_p - z_ap;
         }
-        c_etot = ze;
+        s_zc[tid] = ze;
+        s_zc[Z + tid] = c_atot;
+        s_zc[2 * Z + tid] = c_itot;
         sh.active_energy[tid] = z_active;
         sh.power[tid] = z_p;
         sh.active_power[tid] = z_ap;
@@ -1813,8 +1824,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
       }
       mark(4);
       if (tid < static_cast<uint32_t>(Z)) {
-        st.node_active_total[zi] = c_atot;
-        st.node_idle_total[zi] = c_itot;
+        st.node_active_total[zi] = s_zc[Z + tid];
+        st.node_idle_total[zi] = s_zc[2 * Z + tid];
         st.node_energy_total[zi] = ze;
         st.node_active_energy[zi] = z_active;
         st.node_power[zi] = z_p;

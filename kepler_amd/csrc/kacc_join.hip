@@ -293,6 +293,7 @@ constexpr int kJScan2 = 16;    // the two block scans of step 3 share their barr
 constexpr int kJ6B = 32;       // PID tables in 6-B buckets (u32 keys, u16 slots), vector table loads
 constexpr int kJSeenNR = 64;   // seen marks without return; duplicates found by counting (step 3)
 constexpr int kJVec = 128;     // a lane's keys loaded / slot words stored as vectors
+constexpr int kJGroup = 256;   // kJ6B lookups read four buckets per LDS read
 
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -353,6 +354,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   constexpr bool kSplit = kWide || k6;  // a key array and a slot array (else packed entries)
   constexpr bool kLock = (V & kJLock) != 0, kErrReg = (V & kJErrReg) != 0, kInsDup = (V & kJInsDup) != 0;
   constexpr bool kScan2 = (V & kJScan2) != 0, kSeenNR = (V & kJSeenNR) != 0, kVec = (V & kJVec) != 0;
+  constexpr bool kGroup = k6 && (V & kJGroup) != 0;
   using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
   using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
   using SlotT = std::conditional_t<k6, uint16_t, uint32_t>;
@@ -517,6 +519,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       }
       state |= 1u << (2 * j);
     }
+    if constexpr (kGroup) {
+      // four consecutive buckets per LDS read (16 B, aligned): the probe ends at the
+      // first bucket at or after pb holding the key or empty (where linear probing
+      // stops; tombstones are skipped); <= H / 4 + 1 groups cover the whole table
+      for (uint32_t depth = 0; depth <= H; depth += 4) {
+        uint4 g[kRpl];
+#pragma unroll
+        for (int j = 0; j < kRpl; ++j) g[j] = *reinterpret_cast<const uint4 *>(s_ent + (pb[j] & ~3u));
+        uint32_t probing = 0;
+#pragma unroll
+        for (int j = 0; j < kRpl; ++j) {
+          const uint32_t k = static_cast<uint32_t>(key[j]), e = T::kEmpty;
+          const uint32_t hm = (g[j].x == k ? 1u : 0u) | (g[j].y == k ? 2u : 0u) | (g[j].z == k ? 4u : 0u) |
+                              (g[j].w == k ? 8u : 0u);
+          const uint32_t em = (g[j].x == e ? 1u : 0u) | (g[j].y == e ? 2u : 0u) | (g[j].z == e ? 4u : 0u) |
+                              (g[j].w == e ? 8u : 0u);
+          const uint32_t o = pb[j] & 3u;
+          const uint32_t f = static_cast<uint32_t>(__builtin_ctz((((hm | em) >> o) << o) | 16u));
+          const bool act = ((state >> (2 * j)) & 3u) == 1u, end = f < 4u, hit = end && ((hm >> f) & 1u);
+          const uint32_t nv = hit ? 2u : end ? 3u : 1u;  // found / absent / next group
+          state = act ? (state & ~(3u << (2 * j))) | (nv << (2 * j)) : state;
+          pb[j] = !act ? pb[j] : end ? (pb[j] & ~3u) + f : ((pb[j] | 3u) + 1u) & hmask;
+          probing |= act && !end ? 1u : 0u;
+        }
+        if (__ballot(probing) == 0) break;
+      }
+    } else
     for (uint32_t depth = 0; depth < H; ++depth) {
       K kk[kRpl];
 #pragma unroll
@@ -1165,7 +1194,8 @@ namespace {
 // round 2's kernel (8-B packed PID buckets) and the production one
 constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
                         kacc::join::kJInsDup | kacc::join::kJScan2;
-constexpr int kJoinDefault = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec;
+constexpr int kJoinDefault =
+    kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
 int launched_variant(int v) {
@@ -1174,6 +1204,7 @@ int launched_variant(int v) {
     case kJoinR2 | kacc::join::kJ6B:
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
     case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
+    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
       return v;
     default: return kJoinDefault;
   }
@@ -1262,6 +1293,9 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
         break;
       case kJoinR2 | kJSeenNR | kJVec:
         hipLaunchKernelGGL((join_small<K, kJoinR2 | kJSeenNR | kJVec>), grid, block, 0, st, a);
+        break;
+      case kJoinR2 | kJ6B | kJSeenNR | kJVec:
+        hipLaunchKernelGGL((join_small<K, kJoinR2 | kJ6B | kJSeenNR | kJVec>), grid, block, 0, st, a);
         break;
       default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
     }

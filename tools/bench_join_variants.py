@@ -21,9 +21,10 @@ def main():
     from kepler_amd.torch_batch import current_stream_handle
 
     cfg = int(os.environ.get("CONFIG", "3"))
-    # 31: round 2's kernel (8-B PID buckets); 63 / 127 / 223: with 6-B buckets, + seen marks
-    # without return, seen marks + vector rows without 6-B buckets; -1: production
-    variants = [int(x) for x in os.environ.get("VARIANTS", "31,63,127,223,-1").split(",")]
+    # 31: round 2's kernel (8-B PID buckets); 63 / 127 / 255: + 6-B buckets, + seen marks
+    # without return, + vector rows; 223: seen marks + vector rows on 8-B buckets; -1:
+    # production (255 + lookups reading four buckets per LDS read)
+    variants = [int(x) for x in os.environ.get("VARIANTS", "31,127,255,-1").split(",")]
     rounds = int(os.environ.get("ROUNDS", "3"))
     torch.cuda.set_device(0)
     torch.cuda.set_stream(torch.cuda.Stream())
