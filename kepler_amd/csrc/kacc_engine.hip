@@ -1584,8 +1584,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
   CarryRows<Z> rw;
   fill_tables<Z, T>(bs, K, 0u, n, tab);
   lds_barrier();
-  {
-    uint32_t bad;
+  if constexpr (kPrefetch) {  // otherwise every interval loads its own rows at its top: rw
+    uint32_t bad;             // is then dead across the loop's back edge (no carried VGPRs)
     load_rows<Z, T>(bs[0], carry_ranges(bs[0], tab.off, bad), rw);
   }
   for (uint32_t k = 0, c = 0; k < K; ++k) {
@@ -1598,10 +1598,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(4, 4))) void 
     const uint32_t e = k - c;
     const kacc_interval &b = bs[k];
     if constexpr (!kPrefetch) {
-      if (k > 0) {
-        uint32_t bad;
-        load_rows<Z, T>(b, carry_ranges(b, tab.off + e * 8, bad), rw);
-      }
+      uint32_t bad;
+      load_rows<Z, T>(b, carry_ranges(b, tab.off + e * 8, bad), rw);
     }
     uint32_t bad_offsets;
     const NodeRanges rg = carry_ranges(b, tab.off + e * 8, bad_offsets);

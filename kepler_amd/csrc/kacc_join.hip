@@ -294,6 +294,7 @@ constexpr int kJ6B = 32;       // PID tables in 6-B buckets (u32 keys, u16 slots
 constexpr int kJSeenNR = 64;   // seen marks without return; duplicates found by counting (step 3)
 constexpr int kJVec = 128;     // a lane's keys loaded / slot words stored as vectors
 constexpr int kJGroup = 256;   // kJ6B lookups read four buckets per LDS read
+constexpr int kJDpp = 1024;    // block scans by DPP moves instead of LDS permutes
 
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -309,6 +310,37 @@ __device__ __forceinline__ void jbar() {
     __syncthreads();
 }
 
+// Inclusive scan over the 64 lanes of a wave in DPP moves (no LDS round trips): within
+// rows of 16 by row_shr 1, 2, 4, 8, then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3.  A lane without a source (or outside the row mask)
+// adds the `old` operand, 0.
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t x, uint32_t identity, Op op) {
+  int v = static_cast<int>(x);
+  const int id = static_cast<int>(identity);
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return static_cast<uint32_t>(v);
+}
+struct DppAdd {
+  __device__ int operator()(int a, int b) const { return static_cast<int>(static_cast<uint32_t>(a) + static_cast<uint32_t>(b)); }
+};
+struct DppMin {
+  __device__ int operator()(int a, int b) const { return static_cast<int>(min(static_cast<uint32_t>(a), static_cast<uint32_t>(b))); }
+};
+struct DppMax {
+  __device__ int operator()(int a, int b) const { return static_cast<int>(max(static_cast<uint32_t>(a), static_cast<uint32_t>(b))); }
+};
+// the wave's reduction (lane 63 of the inclusive scan), uniform
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce_dpp(uint32_t x, uint32_t identity, Op op) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_scan_dpp(x, identity, op)), 63));
+}
+
 // Two exclusive block-wide scans at once (one barrier; s_wave [2 * waves]).
 // The caller puts a barrier between this and the next write of s_wave.
 template <int V>
@@ -317,12 +349,17 @@ __device__ __forceinline__ void block_scan2(uint32_t v0, uint32_t v1, uint32_t *
   constexpr int kW = kThreads / 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t x0 = v0, x1 = v1;
+  if constexpr ((V & kJDpp) != 0) {
+    x0 = wave_scan_dpp(x0, 0u, DppAdd{});
+    x1 = wave_scan_dpp(x1, 0u, DppAdd{});
+  } else {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y0 = __shfl_up(x0, d, 64), y1 = __shfl_up(x1, d, 64);
-    if (lane >= d) {
-      x0 += y0;
-      x1 += y1;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y0 = __shfl_up(x0, d, 64), y1 = __shfl_up(x1, d, 64);
+      if (lane >= d) {
+        x0 += y0;
+        x1 += y1;
+      }
     }
   }
   if (lane == 63) {
@@ -498,7 +535,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         sl = static_cast<uint32_t>(ev[j]);
       if (sl < S) atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
     }
-    occ = wave_sum(occ);
+    occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
     if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
   }
   uint32_t mine = 0;   // new rows of this lane
@@ -861,10 +898,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     if (errs) atomicOr(a.err, errs);
   }
   if (a.out_span) {
+    if constexpr ((V & kJDpp) != 0) {
+      lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
+      hi = wave_reduce_dpp(hi, 0u, DppMax{});
+    } else {
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
-      hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
+      for (int d = 32; d >= 1; d >>= 1) {
+        lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
+        hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
+      }
     }
     if ((tid & 63) == 0) {
       s_lo[tid >> 6] = lo;
@@ -1194,8 +1236,8 @@ namespace {
 // round 2's kernel (8-B packed PID buckets) and the production one
 constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
                         kacc::join::kJInsDup | kacc::join::kJScan2;
-constexpr int kJoinDefault =
-    kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
+constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
+constexpr int kJoinDefault = kJoinGroup;
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
 int launched_variant(int v) {
@@ -1205,6 +1247,7 @@ int launched_variant(int v) {
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
     case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
+    case kJoinGroup | kacc::join::kJDpp:
       return v;
     default: return kJoinDefault;
   }
@@ -1297,6 +1340,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinR2 | kJ6B | kJSeenNR | kJVec:
         hipLaunchKernelGGL((join_small<K, kJoinR2 | kJ6B | kJSeenNR | kJVec>), grid, block, 0, st, a);
         break;
+      case kJoinGroup | kJDpp: hipLaunchKernelGGL((join_small<K, kJoinGroup | kJDpp>), grid, block, 0, st, a); break;
       default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
     }
   };

@@ -22,9 +22,10 @@ def main():
 
     cfg = int(os.environ.get("CONFIG", "3"))
     # 31: round 2's kernel (8-B PID buckets); 63 / 127 / 255: + 6-B buckets, + seen marks
-    # without return, + vector rows; 223: seen marks + vector rows on 8-B buckets; -1:
-    # production (255 + lookups reading four buckets per LDS read)
-    variants = [int(x) for x in os.environ.get("VARIANTS", "31,127,255,-1").split(",")]
+    # without return, + vector rows; 223: seen marks + vector rows on 8-B buckets; 511: 255 +
+    # lookups reading four buckets per LDS read = production (-1); 1535: + DPP scans and
+    # reductions (measured no faster: profiles/r04/join_group)
+    variants = [int(x) for x in os.environ.get("VARIANTS", "31,127,1535,-1").split(",")]
     rounds = int(os.environ.get("ROUNDS", "3"))
     torch.cuda.set_device(0)
     torch.cuda.set_stream(torch.cuda.Stream())

@@ -4,7 +4,7 @@
 # per-phase stops, and the per-phase SQ counters of the production join.
 set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=${OUT:-r04j}
+O=${OUT:-r04l}
 mkdir -p gpurun_out/$O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_join.py tests/test_gpu_packer.py tests/test_gpu_tracker.py \
