@@ -137,6 +137,39 @@ def test_join_errors_raise_erange():
     assert term == []
 
 
+def test_join_found_duplicate_and_overfull_small_table():
+    """The 6-B small-table PID join's own error paths: an ID already in the table given
+    twice in one call (found twice: caught by counting the found rows against the held,
+    not-terminated slots, then re-marked) and a small-table node (<= 4096 buckets) with
+    more rows than join_small holds (3100 > its 2700 slots: ERANGE in join_small, never
+    join_big)."""
+    slot_off = np.array([0, 100, 2800], dtype=np.uint32)  # node 1: 2700 slots, 4096 buckets
+    acc = accel.Accel(1, **caps_for(slot_off))
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, slot_off)
+    ora = OracleSlotMap(slot_off, 0)
+    row_off = np.array([0, 50, 2050], dtype=np.uint32)
+    keys = np.r_[np.arange(1, 51), np.arange(1000, 3000)].astype(np.uint64)
+    rc, want, _, _, _ = ora.join(row_off, keys, None)
+    assert rc == 0
+    got, term = gpu.join(row_off, keys)
+    np.testing.assert_array_equal(got, want)
+    dup = np.r_[np.arange(1, 51), [7], np.arange(1000, 3000)].astype(np.uint64)  # 7 found twice
+    with pytest.raises(accel.AccelError) as ei:
+        gpu.join(np.array([0, 51, 2051], dtype=np.uint32), dup)
+    assert ei.value.code == accel.KACC_ERANGE
+    gpu.m.reset()
+    big = np.r_[np.arange(1, 51), np.arange(5000, 8100)].astype(np.uint64)  # node 1: 3100 rows
+    with pytest.raises(accel.AccelError) as ei:
+        gpu.join(np.array([0, 50, 3150], dtype=np.uint32), big)
+    assert ei.value.code == accel.KACC_ERANGE
+    gpu.m.reset()  # and the same valid batch afterwards, from empty tables
+    ora = OracleSlotMap(slot_off, 0)
+    rc, want, _, _, _ = ora.join(row_off, keys, None)
+    got, term = gpu.join(row_off, keys)
+    np.testing.assert_array_equal(got, want)
+    assert term == []
+
+
 @pytest.mark.parametrize("churn_model", ["keyed", "proc"])
 @pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
 def test_join_feeds_interval_bit_exact(policy, churn_model):
