@@ -174,9 +174,14 @@ struct ChunkItem {
 // the 1/8 shard of config 3 against one or two here; and no reliance on how
 // gfx950 performs agent-scope atomics).  Config 3: 40 loads per lane, hidden
 // under the namespace blocks of the same launch.  Past 2 x kColLoads rounds the
-// lanes keep kColLoadsWide loads in flight (config 1, 40k nodes: 157 loads per
-// lane in 5 round trips instead of 20).
+// Past kColWideNodes the lanes keep kColLoadsWide loads in flight (config 1,
+// 40k nodes: 157 loads per lane in 5 round trips instead of 20: sums 36.8 ->
+// 27.8 us).  That is a kernel of its own (cluster_partials_kernel<Z, kW, true>):
+// its 166 VGPRs would hold the namespace blocks of every fleet at three waves per
+// SIMD instead of eight (config 3, 10k nodes: 17.5 against 16.6 us with 8 loads;
+// profiles/r04/colw).
 constexpr int kColLoads = 8, kColLoadsWide = 32;
+constexpr uint64_t kColWideNodes = 16384;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
   const uint64_t *active_total, *idle_total;
@@ -861,7 +866,7 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 // Column mode of the cluster node totals (see NodeTotalsArgs): block b owns output
 // value b — column b / Z of the five node tables, zone b % Z — and lanes tid < kBlock
 // sum it (the same order whatever the caller's block size); s_w: kBlock / 64 words.
-template <int Z>
+template <int Z, bool kWideCols = false>
 __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint32_t b, uint64_t *s_w) {
   const uint32_t tid = threadIdx.x;
   if (tid >= static_cast<uint32_t>(kBlock)) return;  // no barrier below: the idle lanes leave
@@ -896,7 +901,7 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
       }
     }
   };
-  if (na.n_nodes > static_cast<uint64_t>(kBlock) * kColLoads * 2)
+  if constexpr (kWideCols)
     rounds(std::integral_constant<int, kColLoadsWide>{});
   else
     rounds(std::integral_constant<int, kColLoads>{});
@@ -2947,7 +2952,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
   }
 }
 
-template <int Z, int kW = 2 * Z>
+template <int Z, int kW = 2 * Z, bool kWideCols = false>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
                                                                   const uint32_t *__restrict__ slots,
@@ -2965,7 +2970,7 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
     return;
   }
   __shared__ uint64_t s_w[kBlock / 64];
-  node_column_block<Z>(na, blockIdx.x, s_w);  // block b owns output value b: column b / Z, zone b % Z
+  node_column_block<Z, kWideCols>(na, blockIdx.x, s_w);  // block b owns output value b: column b / Z, zone b % Z
 }
 
 // Elements [first, first + count) of the derived process power table
@@ -3221,15 +3226,17 @@ void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t 
                              hipStream_t st, const uint64_t *pod_export = nullptr, uint64_t n_pods = 0) {
   const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
   const uint32_t ns_blocks = (n_ns + per_block - 1) / per_block;
-  if (pod_export)
-    KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0,
-                       st, ns_blocks, n_ns, off, slots, pod_export, reinterpret_cast<const double *>(pod_export + Z),
-                       n_pods, out_e, out_p, ctx->d_err, na);
-  else  // the pod tables: one [energy | power] record per slot, like an export row
+  // pod_export NULL: the pod tables, one [energy | power] record per slot like an export row
+  const uint64_t *pe = pod_export ? pod_export : (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY];
+  const double *pp = pod_export ? reinterpret_cast<const double *>(pod_export + Z)
+                                : (const double *)ctx->tables[KACC_T_POD_POWER];
+  const uint64_t rows = pod_export ? n_pods : ctx->cfg.pod_slots;
+  if (na.n_nodes > kacc::kColWideNodes && node_blocks)
+    KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, true>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock),
+                0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+  else
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
-                       ns_blocks, n_ns, off, slots, (const uint64_t *)ctx->tables[KACC_T_POD_ENERGY],
-                       (const double *)ctx->tables[KACC_T_POD_POWER], ctx->cfg.pod_slots, out_e, out_p, ctx->d_err,
-                       na);
+                ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
 }
 
 // Chunk-item list sized for the worst case of a batch (every node oversized,
