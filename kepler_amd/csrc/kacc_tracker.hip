@@ -95,6 +95,36 @@ __device__ void bitonic(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t n) {
   }
 }
 
+// The same network for n <= 64 in one wave's registers (lane j holds triple j, lanes
+// >= n the +inf padding): compare-exchange with the lane at distance `stride` by
+// shuffles, no workgroup barriers; the first n triples written back.  Caller: the
+// lanes of wave 0 only.
+__device__ void bitonic_wave(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t a1 = lane < n ? k1[lane] : ~0ull;
+  uint32_t a2 = lane < n ? k2[lane] : ~0u;
+  uint32_t a3 = lane < n ? ix[lane] : 0xffffu;
+  for (uint32_t size = 2; size <= 64; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t b1 = __shfl_xor(a1, static_cast<int>(stride), 64);
+      const uint32_t b2 = __shfl_xor(a2, static_cast<int>(stride), 64);
+      const uint32_t b3 = __shfl_xor(a3, static_cast<int>(stride), 64);
+      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
+      const bool a_gt = a1 > b1 || (a1 == b1 && a2 > b2), b_gt = b1 > a1 || (b1 == a1 && b2 > a2);
+      // the pair's lower lane keeps the min when ascending (up), the max otherwise
+      const bool take = lower == up ? a_gt : b_gt;
+      a1 = take ? b1 : a1;
+      a2 = take ? b2 : a2;
+      a3 = take ? b3 : a3;
+    }
+  }
+  if (lane < n) {
+    k1[lane] = a1;
+    k2[lane] = a2;
+    ix[lane] = static_cast<uint16_t>(a3);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
   __shared__ uint64_t s_key[kChunk];    // survivors (filter order), then sort keys ~energy
   __shared__ uint64_t s_e[kChunk];
@@ -169,7 +199,12 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       s_ix[j] = static_cast<uint16_t>(j);
     }
     __syncthreads();
-    bitonic(s_k1, s_k2, s_ix, m);
+    if (m <= 64) {  // block-uniform: one wave, no barriers inside
+      if (tid < 64) bitonic_wave(s_k1, s_k2, s_ix, m);
+      __syncthreads();
+    } else {
+      bitonic(s_k1, s_k2, s_ix, m);
+    }
     // ---- ranks (before anything moves) ----------------------------------------------
     uint32_t new_size = size + m;
     if (a.max_size > 0) {
