@@ -4,7 +4,7 @@
 # this build and on the build before (ab_prev/trk0), interleaved, two rounds each.
 set -u -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=${OUT:-r04t}
+O=${OUT:-r04u}
 mkdir -p gpurun_out/$O
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_tracker.py tests/test_gpu_join.py > gpurun_out/$O/pytest.log 2>&1 \
