@@ -387,11 +387,11 @@ def test_cluster_node_totals_follow_the_live_nodes():
 
 
 def test_cluster_node_totals_back_to_back_launches():
-    """The cluster node totals' last-block handoff (cluster_partials_kernel: per-block partials
-    published by device-scope atomic exchanges, the last block acquires and adds them) pinned
-    under back-to-back launches with no host sync: 24 intervals of changing node data, each
-    followed by its partial sums into its own row, 40 node blocks per launch.  A partial of an
-    earlier launch read by the last block would show as a stale total."""
+    """The cluster node totals under back-to-back launches with no host sync: 24 intervals of
+    changing node data, each followed by its partial sums into its own row.  20k nodes: past
+    kColWideNodes, so the wide column-mode instance (cluster_partials_kernel<Z, kW, true>,
+    32 loads in flight per lane) runs; a stale or mixed-up total would show against the oracle
+    (the round-3 last-block handoff this pinned is gone)."""
     from oracle.oracle import Oracle
 
     n, Z, K = 20000, 2, 24
