@@ -524,7 +524,8 @@ int kacc_gather_pods(kacc_cluster *c, const uint32_t *n_pods, const uint32_t *co
  * reserved key, more live IDs than the node's range) are raised as
  * KACC_ERANGE at kacc_sync; the affected rows get slot word 0xffffffff (of
  * two rows carrying one ID, which one keeps a slot is unspecified: the whole
- * call is reported as failed).                                               */
+ * call is reported as failed).  A PID node with <= 2730 slots given more than
+ * 3072 rows fails whole: every row 0xffffffff, its map unchanged.            */
 typedef enum kacc_kind {
   KACC_KIND_PROC = 0, /* key: uint32_t PID — process.go:120 StringID        */
   KACC_KIND_CTR = 1,  /* key: uint64_t ID of the container ID string        */
