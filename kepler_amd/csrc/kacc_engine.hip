@@ -1956,8 +1956,14 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Waves per SIMD small_kernel is compiled for: what its LDS allows (a workgroup is four waves,
+// one per SIMD; 160 KiB per CU): 25.4 KiB -> six workgroups at Z <= 3 without the
+// slot-order buffer (SW false), 29.5 KiB -> five with it (Z <= 3), 37.7 KiB -> four
+// at Z = 4.  Asking for more only failed the target (build warnings, round 3).
 template <int Z, bool SW>
-__global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(Z <= 2 ? 6 : Z <= 4 ? 5 : 1))) void small_kernel(
+constexpr int kSmallWavesPerEu = Z <= 3 ? (SW || Z == 3 ? 5 : 6) : Z == 4 ? 4 : 1;
+template <int Z, bool SW>
+__global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_eu(kSmallWavesPerEu<Z, SW>))) void small_kernel(
     const kacc_interval b, const DevState st) {
   constexpr bool kNT = true, kNtLd = true;  // as interval_kernel's production variant
   __shared__ double s_d_all[kSmallWaves][kSmallRows];
