@@ -78,9 +78,12 @@ def _oracle(nranks):
     return L, per, pe, pp
 
 
-def test_two_ranks_one_gpu_loopback_collectives(tmp_path):
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_ranks_one_gpu_loopback_collectives(tmp_path, nranks):
+    """nranks processes on the one GPU (8: the rank count of the driver's 8-GPU run, here
+    through the loopback stand-in): every rank holds the unsharded oracle's totals and the
+    pods gathered in (rank, pod) order."""
     assert os.path.exists(LOOPBACK), "build() makes tests/c/build/libkacc_loopback_rccl.so"
-    nranks = 2
     rcs, outs = _run_ranks(tmp_path, nranks, LOOPBACK)
     assert rcs == [0] * nranks, "\n".join(f"--- rank {r} rc={rc}\n{o[-4000:]}" for r, (rc, o) in
                                           enumerate(zip(rcs, outs)))
@@ -109,11 +112,13 @@ def test_two_ranks_one_gpu_loopback_collectives(tmp_path):
         np.testing.assert_array_equal(d["ge"], want_pe, err_msg=f"rank {r} gathered pod energy")
         np.testing.assert_array_equal(d["gp"].view(np.uint64), want_pp.view(np.uint64),
                                       err_msg=f"rank {r} gathered pod power")
-    # the ranks cover the fleet in order, and both hold the same cluster result
-    assert his[0][0] == 0 and his[0][1] == his[1][0] and his[-1][1] == L.n_nodes
+    # the ranks cover the fleet in order, and all hold the same cluster result
+    assert his[0][0] == 0 and his[-1][1] == L.n_nodes
+    assert all(his[r][1] == his[r + 1][0] for r in range(nranks - 1))
     assert [int(res[r]["first"][0]) for r in range(nranks)] == [int(L.pod_off[lo]) for lo, _ in his]
-    for key in ("te", "tp", "ge", "gp"):
-        np.testing.assert_array_equal(res[0][key].view(np.uint64), res[1][key].view(np.uint64))
+    for r in range(1, nranks):
+        for key in ("te", "tp", "ge", "gp"):
+            np.testing.assert_array_equal(res[0][key].view(np.uint64), res[r][key].view(np.uint64))
     assert np.count_nonzero(per[-1][0]) > 0 and np.count_nonzero(per[-1][1]) > 0
 
 
