@@ -173,8 +173,7 @@ struct ChunkItem {
 // last block to finish add the partials: four dependent round trips, 6.5 us at
 // the 1/8 shard of config 3 against one or two here; and no reliance on how
 // gfx950 performs agent-scope atomics).  Config 3: 40 loads per lane, hidden
-// under the namespace blocks of the same launch.  Past 2 x kColLoads rounds the
-// Past kColWideNodes the lanes keep kColLoadsWide loads in flight (config 1,
+// under the namespace blocks of the same launch.  Past kColWideNodes the lanes keep kColLoadsWide loads in flight (config 1,
 // 40k nodes: 157 loads per lane in 5 round trips instead of 20: sums 36.8 ->
 // 27.8 us).  That is a kernel of its own (cluster_partials_kernel<Z, kW, true>):
 // its 166 VGPRs would hold the namespace blocks of every fleet at three waves per
@@ -2966,10 +2965,12 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
                                                                   const double *__restrict__ pp, uint64_t pod_slots,
                                                                   uint64_t *out_e, double *out_p, uint32_t *err,
                                                                   const NodeTotalsArgs na) {
-  // the node blocks come FIRST: their chain (loads, partial exchange, count, the last
-  // block's sums) is the longer one, and dispatched after the namespace blocks it
-  // started last (1/8 shard of config 3: namespace sums alone 5.2 us, node totals
-  // alone 6.5 us, both 9.3 us with the node blocks last; profiles/r03/tprobe2)
+  // the first 5Z blocks are the cluster node totals in column mode: block c owns
+  // output value c (column c / Z of the five node tables, zone c % Z) and writes it,
+  // with no cross-block combine; they come first because their per-lane chain of
+  // loads is the longer one (node blocks dispatched last finished last:
+  // profiles/r03/tprobe2).  The remaining ns_blocks blocks are the namespace sums.
+  // The block count and the 5Z column blocks are the only coupling between blocks.
   const uint32_t nb = gridDim.x - ns_blocks;
   if (blockIdx.x >= nb) {
     namespace_block<Z, kW>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
@@ -4196,6 +4197,15 @@ uint64_t kacc_interval_bytes(uint32_t Z, uint64_t N, uint64_t P, uint64_t C, uin
   return N * node + P * proc + C * ctr + V * vm + Q * pod;
 }
 
+// The carry kernel writes no exports (kacc_run_intervals never launches it for a
+// batch that asks for them): its debug entry points refuse such batches too.
+static int reject_carry_exports(kacc_ctx *ctx, const kacc_interval *b, uint32_t count) {
+  for (uint32_t k = 0; k < count; ++k)
+    if (b[k].pod_export || b[k].node_export)
+      return fail(ctx, KACC_EINVAL, "interval %u: the carry kernel writes no pod / node exports", k);
+  return KACC_OK;
+}
+
 // Internal (kacc_debug.h): timing ablations of the one-launch K-interval kernel.
 int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t count, void *stream, int variant,
                             uint64_t *d_out) {
@@ -4203,7 +4213,9 @@ int kacc_debug_carry_stamps(kacc_ctx *ctx, const kacc_interval *b, uint32_t coun
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  int rc = stage_batches(ctx, b, count, st);
+  int rc = reject_carry_exports(ctx, b, count);
+  if (rc != KACC_OK) return rc;
+  rc = stage_batches(ctx, b, count, st);
   if (rc != KACC_OK) return rc;
   kacc::DevState ds = dev_state(ctx);
   ds.items = reinterpret_cast<kacc::ChunkItem *>(d_out);  // [n_nodes][8 waves][8 phases] u64
@@ -4225,7 +4237,9 @@ int kacc_debug_run_intervals_variant(kacc_ctx *ctx, const kacc_interval *b, uint
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   if (ctx->cfg.zones != 2) return fail(ctx, KACC_EINVAL, "carry variants are built for Z = 2");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  int rc = stage_batches(ctx, b, count, st);
+  int rc = reject_carry_exports(ctx, b, count);
+  if (rc != KACC_OK) return rc;
+  rc = stage_batches(ctx, b, count, st);
   if (rc != KACC_OK) return rc;
   const kacc::DevState ds = dev_state(ctx);
   const bool medium = all_medium(b, count);

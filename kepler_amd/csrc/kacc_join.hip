@@ -243,9 +243,11 @@ __device__ __forceinline__ bool node_view(const Args &a, uint32_t n, NodeView &v
     v.r1 = min(v.r1, a.n_rows);
     v.r0 = min(v.r0, v.r1);
   }
-  // under fmt6 every small-table node is join_small's (more rows than kSmallRows
-  // cannot fit its <= 2730 slots: an ERANGE there)
-  if ((v.H <= kLdsBuckets && (a.fmt6 || v.r1 - v.r0 <= kSmallRows)) != kSmall) return false;
+  // every small-table node is join_small's, whatever its kind and row count: more
+  // rows than kSmallRows cannot fit its <= 2730 slots, an ERANGE there (join_big
+  // only runs for maps with a big table, so routing such a node to it would leave
+  // its slot words and terminated count unwritten for the other maps)
+  if ((v.H <= kLdsBuckets) != kSmall) return false;
   v.S = s1 - v.s0;
   v.shift = 32u - static_cast<uint32_t>(__builtin_ctz(v.H));
   return true;
@@ -415,19 +417,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   if (!node_view<true>(a, n, v)) return;
   const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H, hmask = H - 1;
   const uint32_t W = (S + 31) / 32;
-  if constexpr (k6) {
-    if (R > kSmallRows) {  // more rows than the table's <= 2730 slots: ERANGE, map unchanged
-      for (uint32_t r = tid; r < R; r += kThreads) a.out_slot[v.r0 + r] = kInvalid;
-      if (tid == 0) {
-        atomicOr(a.err, kErrRange);
-        a.term_count[n] = 0u;
-        if (a.out_span) {
-          a.out_span[2 * n] = 1u;
-          a.out_span[2 * n + 1] = 0u;
-        }
+  if (R > kSmallRows) {  // more rows than the table's <= 2730 slots: ERANGE, map unchanged
+    for (uint32_t r = tid; r < R; r += kThreads) a.out_slot[v.r0 + r] = kInvalid;
+    if (tid == 0) {
+      atomicOr(a.err, kErrRange);
+      a.term_count[n] = 0u;
+      if (a.out_span) {
+        a.out_span[2 * n] = 1u;
+        a.out_span[2 * n + 1] = 0u;
       }
-      return;
     }
+    return;
   }
   const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
   T G, L;
@@ -1147,6 +1147,28 @@ uint64_t node_buckets(uint32_t S) {
 
 }  // namespace
 
+namespace {
+// round 2's kernel (8-B packed PID buckets) and the production one
+constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
+                        kacc::join::kJInsDup | kacc::join::kJScan2;
+constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
+constexpr int kJoinDefault = kJoinGroup;
+int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
+// the variant join_small is launched with (the instantiated ones; else production)
+int launched_variant(int v) {
+  switch (v) {
+    case 0: case 1: case 3: case 6: case 7: case 15: case kJoinR2:
+    case kJoinR2 | kacc::join::kJ6B:
+    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
+    case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
+    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
+    case kJoinGroup | kacc::join::kJDpp:
+      return v;
+    default: return kJoinDefault;
+  }
+}
+}  // namespace
+
 extern "C" {
 
 int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const uint32_t *slot_off,
@@ -1222,6 +1244,9 @@ int kacc_slotmap_reset(kacc_slotmap *m) {
   kacc_ctx *ctx = m->ctx;
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   const size_t nb = std::max<uint64_t>(m->buckets, 1);
+  // the bucket format of the PID small tables follows the join variant in force now;
+  // slot_join refuses a later launch in the other format (it would misread the table)
+  m->fmt6 = m->kind == KACC_KIND_PROC && (launched_variant(g_join_variant) & kacc::join::kJ6B) != 0;
   KACC_HIP(ctx, hipMemsetAsync(m->d_ent, 0xff, 8 * nb, ctx->stream));  // every bucket empty
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return KACC_OK;
@@ -1232,27 +1257,6 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
                      uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream,
                      uint32_t stop_after);
 
-namespace {
-// round 2's kernel (8-B packed PID buckets) and the production one
-constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
-                        kacc::join::kJInsDup | kacc::join::kJScan2;
-constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
-constexpr int kJoinDefault = kJoinGroup;
-int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
-// the variant join_small is launched with (the instantiated ones; else production)
-int launched_variant(int v) {
-  switch (v) {
-    case 0: case 1: case 3: case 6: case 7: case 15: case kJoinR2:
-    case kJoinR2 | kacc::join::kJ6B:
-    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
-    case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
-    case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
-    case kJoinGroup | kacc::join::kJDpp:
-      return v;
-    default: return kJoinDefault;
-  }
-}
-}  // namespace
 
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
@@ -1317,9 +1321,14 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   (void)hipGetLastError();  // a stale error of an earlier call must not be blamed on this launch
   using namespace kacc::join;
   const dim3 grid(m->n_nodes), block(kThreads);
-  // the table format follows the variant: a map keeps one variant from its reset on
+  // the table format follows the variant: a map keeps the format of its reset
   const int var = launched_variant(g_join_variant);
   a.fmt6 = m->kind == KACC_KIND_PROC && (var & kJ6B) ? 1u : 0u;
+  if ((a.fmt6 != 0) != m->fmt6)
+    return kacc_fail(ctx, KACC_EINVAL,
+                     "slot join: the join variant's table format (%s buckets) differs from the map's "
+                     "(%s, fixed at its last reset): reset the map first",
+                     a.fmt6 ? "6-B" : "8-B", m->fmt6 ? "6-B" : "8-B");
   auto small = [&](auto key) {
     using K = decltype(key);
     switch (var) {

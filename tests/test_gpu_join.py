@@ -170,6 +170,34 @@ def test_join_found_duplicate_and_overfull_small_table():
     assert term == []
 
 
+@pytest.mark.parametrize("kind", [accel.KACC_KIND_CTR, accel.KACC_KIND_POD])
+def test_join_overfull_small_table_u64_kinds(kind):
+    """A small-table node (<= 4096 buckets) with more rows than join_small holds, for
+    the u64-keyed kinds of a map with no big node (join_big is never launched): the
+    call raises ERANGE and the node's slot words are written invalid — none is left
+    stale — and the map still joins a valid batch afterwards."""
+    slot_off = np.array([0, 100, 2800], dtype=np.uint32)  # node 1: 2700 slots, 4096 buckets
+    acc = accel.Accel(1, nodes=2, proc_slots=1, ctr_slots=2800, vm_slots=1, pod_slots=2800)
+    gpu = GpuJoin(acc, kind, slot_off)
+    big = np.r_[np.arange(1, 51), np.arange(5000, 8100)].astype(np.uint64)  # node 1: 3100 rows
+    out = torch.full((3150,), 0x1234, dtype=torch.int32, device="cuda")
+    with pytest.raises(accel.AccelError) as ei:
+        gpu.join(np.array([0, 50, 3150], dtype=np.uint32), big, out=out)
+    assert ei.value.code == accel.KACC_ERANGE
+    words = out.cpu().numpy().view(np.uint32)
+    assert (words[50:] == 0xFFFFFFFF).all()  # join_small's invalid word on every row of node 1
+    assert int(gpu.cnt[1].item()) == 0
+    gpu.m.reset()
+    ora = OracleSlotMap(slot_off, 0)
+    row_off = np.array([0, 50, 2050], dtype=np.uint32)
+    keys = np.r_[np.arange(1, 51), np.arange(1000, 3000)].astype(np.uint64)
+    rc, want, _, _, _ = ora.join(row_off, keys, None)
+    assert rc == 0
+    got, term = gpu.join(row_off, keys)
+    np.testing.assert_array_equal(got, want)
+    assert term == []
+
+
 @pytest.mark.parametrize("churn_model", ["keyed", "proc"])
 @pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
 def test_join_feeds_interval_bit_exact(policy, churn_model):
