@@ -82,13 +82,16 @@ def parse():
                          "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
     ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
                     help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
-    ap.add_argument("--totals", choices=["tables", "exports", "tables+writes"], default="tables",
+    ap.add_argument("--totals", choices=["fused", "tables", "exports", "tables+writes"], default="tables",
                     help="cluster totals from the state tables, partial sums on the compute stream and the RCCL "
                          "all-reduce on the comm stream (kacc_allreduce_namespaces, the default: measured fastest), "
                          "or from the interval's exports with everything on the comm stream (kacc_allreduce_exports: "
                          "the export stores cost 26 us and the concurrent partial sums slow the next interval more "
                          "than they save at config 3, profiles/r03/exports_ablation); tables+writes = the export "
-                         "stores alone (ablation)")
+                         "stores alone (ablation); fused = each interval writes its exports in namespace order "
+                         "(pod_export_pos) and its launch also computes the previous interval's partial sums "
+                         "(kacc_run_interval_sums: one launch per step; the region's last step's sums by "
+                         "kacc_run_export_sums inside the timed region)")
     ap.add_argument("--allreduce-every", type=int, default=8,
                     help="tables mode: the cluster totals of this many consecutive steps are all-reduced by ONE "
                          "kacc_allreduce_sums (each step's partial sums have their own rows; SURVEY 5: one "
@@ -517,6 +520,162 @@ def host_path_line(args, steps=10):
                     "pcie_copy: torch pinned -> device copy of the same bytes (the ceiling)"}
 
 
+def _pack(arrays):
+    """One contiguous byte image of named arrays (16-B aligned segments): {name: (offset, dtype, n)}."""
+    off, layout = 0, {}
+    for name, a in arrays.items():
+        a = np.ascontiguousarray(a)
+        layout[name] = (off, a.dtype, a.size)
+        off += (a.nbytes + 15) // 16 * 16
+    img = np.zeros(max(off, 16), dtype=np.uint8)
+    for name, a in arrays.items():
+        o, _, _ = layout[name]
+        img[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    return img, layout
+
+
+def host_path_ticks_line(args, steps=10):
+    """End-to-end with the CPU-tick input format (kepler_accel.h "CPU-tick input format"): per
+    interval ONE pinned host image crosses PCIe — node readings and CSR, per process row its PID
+    (4 B, for the device slot join) and its tick increment (2 B; 1 % escapes as int64), the
+    aggregates' CSR ends and slot words — then, on the device, kacc_slot_join (PIDs -> slot words,
+    KACC_JOIN_REUSE_TERMINATED) -> kacc_ticks_delta (Go's CPUTimeDelta from the tick map) ->
+    kacc_run_interval.  Two staging buffers: interval i + 1's copy (copy stream) overlaps interval
+    i's kernels (compute stream).  Reported beside the headline, never as `value`."""
+    import ctypes
+
+    import torch
+
+    from kepler_amd import accel, fleet
+    from kepler_amd.torch_batch import interval_from_tensors
+
+    _, _, layout = fleet.config_shard(args.config, 1, 0, bench_nodes(args.config, 1, args.nodes))
+    sizes = layout.sizes()
+    N, P = layout.n_nodes, sizes["n_procs"]
+    rows = np.diff(layout.proc_off.astype(np.int64))
+    slot_off = np.r_[0, np.cumsum(np.ceil(rows * 1.05).astype(np.int64) + 8)].astype(np.uint32)
+    caps = layout.capacities()
+    caps["proc_slots"] = int(slot_off[-1])
+    acc = accel.Accel(layout.zones, **caps)
+    sm = accel.SlotMap(acc, accel.KACC_KIND_PROC, slot_off)
+    sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
+    tm = accel.TickMap(acc)
+    sim = fleet.FleetSim(layout, seed=fleet.SEED)
+    churn = fleet.ProcChurn(layout, churn=0.02)
+    rng = np.random.default_rng(5)
+    statics = layout.static_arrays()
+    imgs = []
+    for k in range(2):
+        node = sim.next_node_inputs()
+        keys = churn.next_keys()
+        dt = rng.integers(0, 3000, size=P).astype(np.uint16)
+        esc = np.flatnonzero(rng.random(P) < 0.01).astype(np.uint32)
+        dt[esc] = accel.KACC_TICKS_ESCAPED
+        arrays = dict(node_ts_ns=node["node_ts_ns"], node_usage_ratio=node["node_usage_ratio"],
+                      node_status=node["node_status"], zone_energy=node["zone_energy"], zone_max=node["zone_max"],
+                      proc_off=statics["proc_off"], ctr_off=statics["ctr_off"], vm_off=statics["vm_off"],
+                      pod_off=statics["pod_off"], pid=keys, dticks=dt,
+                      esc_off=np.searchsorted(esc, layout.proc_off.astype(np.int64)).astype(np.uint32),
+                      esc_row=esc, esc_ticks=rng.integers(1 << 16, 1 << 40, size=esc.size).astype(np.int64),
+                      ctr_proc_end=statics["ctr_proc_end"], ctr_slot=layout.ctr_slot,
+                      vm_proc_end=statics["vm_proc_end"], vm_slot=layout.vm_slot,
+                      pod_ctr_end=statics["pod_ctr_end"], pod_slot=layout.pod_slot)
+        imgs.append(_pack(arrays))
+    nbytes = max(im.nbytes for im, _ in imgs)
+    host = [torch.from_numpy(im).pin_memory() for im, _ in imgs]
+    dev = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_slot = torch.zeros(P, dtype=torch.int32, device="cuda")
+    d_delta = torch.zeros(P, dtype=torch.float64, device="cuda")
+    cap = int(slot_off[-1])
+    tk = torch.zeros(cap, dtype=torch.int64, device="cuda")
+    ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda")
+    span = torch.zeros(2 * N, dtype=torch.int32, device="cuda")
+    tdt = {np.dtype(np.uint32): torch.int32, np.dtype(np.uint64): torch.int64, np.dtype(np.int64): torch.int64,
+           np.dtype(np.float64): torch.float64, np.dtype(np.uint16): torch.int16, np.dtype(np.int32): torch.int32}
+
+    def views(b, lay):
+        return {n: dev[b][o:o + cnt_ * dt_.itemsize].view(tdt[dt_]) for n, (o, dt_, cnt_) in lay.items()}
+
+    descs = []
+    for b in range(2):
+        v = views(b, imgs[b][1])
+        t = {n: v[n] for n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max",
+                               "proc_off", "ctr_off", "vm_off", "pod_off", "ctr_proc_end", "ctr_slot",
+                               "vm_proc_end", "vm_slot", "pod_ctr_end", "pod_slot")}
+        t.update(proc_cpu_delta=d_delta, proc_slot=d_slot, node_proc_span=span)
+        iv = interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
+                                   | accel.KACC_F_STABLE_SLOT_NODES)
+        tks = accel.KaccTicks(N, P, int(v["esc_row"].numel()), 0, v["proc_off"].data_ptr(),
+                              v["node_status"].data_ptr(), d_slot.data_ptr(), v["dticks"].data_ptr(),
+                              v["esc_off"].data_ptr(), v["esc_row"].data_ptr(), v["esc_ticks"].data_ptr(),
+                              d_delta.data_ptr())
+        descs.append((iv, tks, v, t))
+    compute = torch.cuda.current_stream()
+    copy = torch.cuda.Stream()
+    cs = compute.cuda_stream
+    copied = [torch.cuda.Event() for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+    used = [False, False]
+
+    def one(i):
+        b = i % 2
+        if used[b]:
+            copy.wait_event(done[b])  # staging b is free once interval i - 2 has run
+        with torch.cuda.stream(copy):
+            dev[b][:imgs[b][0].nbytes].copy_(host[b], non_blocking=True)
+        copied[b].record(copy)
+        compute.wait_event(copied[b])
+        iv, tks, v, _ = descs[b]
+        sm.join(P, v["proc_off"].data_ptr(), v["pid"].data_ptr(), v["node_status"].data_ptr(), d_slot.data_ptr(),
+                tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), cs, span.data_ptr())
+        tm.delta(tks, cs)
+        acc.run_interval(iv, cs)
+        done[b].record(compute)
+        used[b] = True
+
+    try:
+        for i in range(4):  # first read + warm-up
+            one(i)
+        torch.cuda.synchronize()
+        acc.sync(cs)
+        walls = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(steps):
+                one(i)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) / steps)
+        acc.sync(cs)
+        tp = float(np.median(walls))
+        src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        cps = []
+        for _ in range(6):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            cps.append(time.perf_counter() - t0)
+        t_copy = float(np.median(cps[1:]))
+        del src, dst
+    finally:
+        tm.close()
+        sm.close()
+        acc.close()
+    n_esc = int(descs[0][2]["esc_row"].numel())
+    return {"label": "END-TO-END (PCIe-inclusive; CPU-tick format: PIDs + 2-B tick increments -> H2D -> device "
+                     "slot join -> kacc_ticks_delta -> interval kernel), not `value`",
+            "proc_attr_per_s": P / tp, "node_snapshots_per_s": N / tp, "ms_per_interval": tp * 1e3,
+            "h2d_bytes_per_interval": nbytes, "bytes_per_process_row": nbytes / P, "escapes": n_esc,
+            "pcie_copy_ms": t_copy * 1e3, "pcie_copy_GBps": nbytes / t_copy / 1e9,
+            "frac_of_pcie_copy": t_copy / tp, "buffers_in_flight": 2, "intervals": steps,
+            "note": "one pinned image per interval (node readings + CSR, PID u32 + tick increment u16 per "
+                    "process, 1 % int64 escapes, aggregate CSR ends + slot words); copy stream / compute stream "
+                    "overlap, two staging buffers; the join's churn is fleet.ProcChurn (2 %)"}
+
+
 def bench_nodes(config, world, nodes=None, scaling="strong"):
     """Fleet size of a config at `world` GPUs.  Strong scaling (the north star's "10k-node x
     2k-process fleet interval" at 1/2/4/8 GPUs): one fixed fleet cut into `world` node ranges.
@@ -578,13 +737,24 @@ class Workload:
         # interval, double-buffered by step parity: step k's totals are reduced on the comm
         # stream while step k+1 runs (kacc_allreduce_exports)
         self.exports = args.totals == "exports"
+        # --totals fused: interval k's launch also sums interval k-1's exports (kacc_run_interval_sums)
+        self.fused_sums = args.totals == "fused"
+        if self.fused_sums and K != 1:
+            raise SystemExit("--totals fused: one interval per step (K = 1)")
         self.pex = [torch.zeros(max(sizes["n_pods"], 1) * 2 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
         self.nex = [torch.zeros(max(sizes["n_nodes"], 1) * 5 * Z, dtype=torch.int64, device="cuda") for _ in range(2)]
+        ns_off, ns_slot = layout.namespace_csr()
+        _, ns_row = layout.namespace_csr_rows()
+        ns_pos = np.zeros(max(sizes["n_pods"], 1), dtype=np.uint32)  # pod row -> its place in namespace order
+        ns_pos[ns_row] = np.arange(len(ns_row), dtype=np.uint32)
+        self.ns_t = to_device({"off": ns_off, "slot": ns_slot, "row": ns_row, "pos": ns_pos})
         if args.totals != "tables":  # "tables+writes": the exports are written, the totals come from the tables
             # (an ablation: the cost of the export stores alone)
             for st in range(n_steps):
                 t = self.iv_tensors[st * K + K - 1]
                 t["pod_export"], t["node_export"] = self.pex[st % 2], self.nex[st % 2]
+                if self.fused_sums:  # namespace-ordered exports: the partial sums stream contiguous records
+                    t["pod_export_pos"] = self.ns_t["pos"]
         # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
         # runs K > 1 fast-node intervals as one launch
         # (KACC_F_STABLE_SLOT_NODES: a slot stays with its node; only NEW rows write their node)
@@ -592,9 +762,6 @@ class Workload:
                       | (accel.KACC_F_STABLE_SLOT_NODES if args.slot_nodes == "stable" else 0))
         self.ivs = [interval_from_tensors(t, sizes, self.flags) for t in self.iv_tensors]
         self.iv_arrays = [(accel.KaccInterval * K)(*self.ivs[k * K:(k + 1) * K]) for k in range(n_steps)]
-        ns_off, ns_slot = layout.namespace_csr()
-        _, ns_row = layout.namespace_csr_rows()
-        self.ns_t = to_device({"off": ns_off, "slot": ns_slot, "row": ns_row})
         self.n_ns = len(ns_off) - 1
         # cluster totals.  Tables mode: step k's partial sums go to row k of tot_e / tot_p
         # ([namespaces Z | node totals 2Z] u64, [namespaces Z | node totals 3Z] f64; 640 KB per
@@ -669,6 +836,20 @@ def measure(args, w, rank, world, stream, comm_stream):
                     P([w.ns_e[b].data_ptr()]), P([w.ns_p[b].data_ptr()]), P([w.nd_e[b].data_ptr()]),
                     P([w.nd_p[b].data_ptr()]), P([stream]), P([comm_stream.cuda_stream])) for b in range(2)]
         reduce_fn = lib.kacc_allreduce_exports
+    elif w.fused_sums:  # step k's partial sums inside step k + 1's launch, into step k's rows
+        no_nodes = args.totals_probe == "ns"
+        xsums = []
+        for k in range(w.n_bufs):
+            x = accel.KaccExportSums()
+            x.n_ns = 0 if args.totals_probe == "nodes" else w.n_ns
+            x.n_pods, x.n_nodes, x.ns_ordered = w.sizes["n_pods"], w.sizes["n_nodes"], 1
+            x.ns_pod_off = w.ns_t["off"].data_ptr()
+            x.pod_export, x.node_export = w.pex[k % 2].data_ptr(), None if no_nodes else w.nex[k % 2].data_ptr()
+            x.out_energy, x.out_power = w.ns_e[k].data_ptr(), w.ns_p[k].data_ptr()
+            x.out_node_energy = None if no_nodes else w.nd_e[k].data_ptr()
+            x.out_node_power = None if no_nodes else w.nd_p[k].data_ptr()
+            xsums.append(x)
+        ns_args, reduce_fn = None, None
     else:  # partial sums from the state tables on the compute stream (kacc_cluster_partials); the
         # all-reduce of a group of steps' rows on the comm stream (kacc_allreduce_sums, flush())
         no_nodes = args.totals_probe == "ns"
@@ -718,8 +899,37 @@ def measure(args, w, rank, world, stream, comm_stream):
             cl._check(rc)
 
     time_next = lib.kacc_time_next_launch
+    region = [0]  # first step of the running region (fused: its first step has no previous sums)
+
+    def step_fused(k, ev=None, markers=False):
+        """--totals fused: interval k and, in the same launch, step k - 1's partial sums (from its
+        namespace-ordered exports) into step k - 1's rows; a group whose last step is k - 1 is then
+        complete and its all-reduce is issued."""
+        prev = ctypes.byref(xsums[k - 1]) if k > region[0] else None
+        if ev is not None:
+            if markers:
+                ev[0].record()
+            else:
+                time_next(acc.ctx, ev[0], ev[1])
+        rc = lib.kacc_run_interval_sums(acc.ctx, w.iv_arrays[k], prev, cstream)
+        if rc != accel.KACC_OK:
+            acc._check(rc)
+        if ev is not None and markers:
+            ev[1].record()
+        if k > region[0] and (k - 1) in group_of:
+            flush(group_of[k - 1], k - 1)
+
+    def finish_fused(last):
+        """The region's last step's partial sums (one launch), then its group's all-reduce."""
+        rc = lib.kacc_run_export_sums(acc.ctx, ctypes.byref(xsums[last]), cstream)
+        if rc != accel.KACC_OK:
+            acc._check(rc)
+        if last in group_of:
+            flush(group_of[last], last)
 
     def step(k, ev=None, markers=False):
+        if w.fused_sums:
+            return step_fused(k, ev, markers)
         b = k % w.n_bufs
         if used[b] and comm and w.exports:  # exports ablation: wait for step k-2's all-reduce (its buffers are reused)
             compute.wait_event(done[b])
@@ -753,9 +963,12 @@ def measure(args, w, rank, world, stream, comm_stream):
             dist.barrier()
         torch.cuda.synchronize()
         plan(first, args.steps)
+        region[0] = first
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(first + i, evs[i] if evs else None, markers)
+        if w.fused_sums:
+            finish_fused(first + args.steps - 1)
         torch.cuda.synchronize()  # every all-reduce of the timed steps is inside the timed region
         if world > 1:
             dist.barrier()
@@ -764,8 +977,11 @@ def measure(args, w, rank, world, stream, comm_stream):
         return wall
 
     plan(0, args.warmup)
+    region[0] = 0
     for k in range(args.warmup):
         step(k)
+    if w.fused_sums and args.warmup:
+        finish_fused(args.warmup - 1)
     acc.sync(stream)
     torch.cuda.synchronize()
     tevs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(args.steps)]
@@ -781,7 +997,10 @@ def measure(args, w, rank, world, stream, comm_stream):
         wall_ev = timed(args.warmup + args.steps, hev)  # kernel timing: the same steps with launch events
     else:
         wall = wall_ev = timed(args.warmup, hev, markers)
-    if markers:  # interval, then interval end -> partial sums end
+    if w.fused_sums:  # one launch per step: interval + the previous step's sums (no totals launch)
+        kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
+        totals_ms = []
+    elif markers:  # interval, then interval end -> partial sums end
         kernel_ms = [a.elapsed_time(b) / K for a, b, _, _ in tevs]
         totals_ms = [b.elapsed_time(c) for _, b, c, _ in tevs]
     else:  # kernels only: interval start -> end, partial sums start -> end
@@ -858,10 +1077,12 @@ def main():
     fused = accel.fused_intervals(w.flags, K, args.node_order, Z, exports=args.totals != "tables")
     bytes_per_launch = accel.intervals_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"], sizes["n_vms"],
                                              sizes["n_pods"], K, fused, w.flags) / K
+    sums_bytes = export_sums_bytes(Z, sizes["n_nodes"], sizes["n_pods"], w.n_ns) if w.fused_sums else 0
+    bytes_per_launch += sums_bytes
     k_avg_ms = float(np.mean(kernel_ms))
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
 
-    traffic, traffic_source = pmc_traffic(args, sizes, K, fused)
+    traffic, traffic_source = pmc_traffic(args, sizes, K, fused, w.fused_sums)
     rccl_version, rccl_path = accel.Cluster.rccl()
     emulated = args.shard_of > 1
     result = {
@@ -899,6 +1120,10 @@ def main():
             "shard_of": args.shard_of,
             "cluster_totals": ("kacc_allreduce_exports (interval exports; partial sums + RCCL on the comm stream)"
                                if args.totals == "exports" else
+                               f"kacc_run_interval_sums: step k's launch = interval k + step k-1's partial sums "
+                               f"(namespace-ordered exports, pod_export_pos); the region's last sums by "
+                               f"kacc_run_export_sums; one kacc_allreduce_sums per {max(1, args.allreduce_every)} "
+                               f"steps (comm stream)" if w.fused_sums else
                                f"kacc_cluster_partials every step (from the tables, compute stream) + one "
                                f"kacc_allreduce_sums per {max(1, args.allreduce_every)} steps (comm stream)"),
             "allreduce_every": None if args.totals == "exports" else max(1, args.allreduce_every),
@@ -909,7 +1134,8 @@ def main():
         "kernel_ms": k_avg_ms,
         "kernel_ms_steps": [round(x, 5) for x in kernel_ms],
         "step_minus_kernel_ms": wall_max * 1e3 / args.steps - k_avg_ms * K,
-        "totals_compute_ms": float(np.mean(totals_ms)),  # the partial-sum kernel (launch) / interval end -> its end
+        # the partial-sum kernel (launch) / interval end -> its end; fused: inside kernel_ms
+        "totals_compute_ms": float(np.mean(totals_ms)) if totals_ms else None,
         "kernel_timing": {
             "step_events": args.step_events,
             "ms_per_step_timing_pass": wall_ev * 1e3 / args.steps,
@@ -930,7 +1156,8 @@ def main():
             "bytes_per_interval": bytes_per_launch,
             "bytes_per_interval_unfused": accel.interval_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"],
                                                                sizes["n_vms"], sizes["n_pods"], w.flags),
-            "kernel": kernel_name(w.flags, K, fused, Z),
+            "kernel": kernel_name(w.flags, K, fused, Z, w.fused_sums),
+            "export_sums_bytes": sums_bytes,
             "same_box_copy_GBps": copy_gbps,
             "frac_of_copy": achieved / copy_gbps,
         },
@@ -1020,6 +1247,10 @@ def main():
             result["host_path"] = host_path_line(args)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["host_path"] = {"error": repr(e)}
+        try:
+            result["host_path_ticks"] = host_path_ticks_line(args)
+        except Exception as e:  # a secondary line: report, never lose the headline
+            result["host_path_ticks"] = {"error": repr(e)}
 
     if rank == 0:
         line = json.dumps(result)
@@ -1031,9 +1262,22 @@ def main():
         dist.destroy_process_group()
 
 
-def kernel_name(flags, K, fused, Z):
+def export_sums_bytes(Z, n_nodes, n_pods, n_ns):
+    """Algorithmic bytes --totals fused adds to a launch: the interval's exports
+    written (pod records 16Z B in namespace order, node rows 40Z B) and the previous
+    interval's read by the sums blocks (the same records, the namespace offsets), plus the
+    partial-sum outputs (16Z B per namespace, 40Z B of node totals)."""
+    exports = n_pods * 16 * Z + n_nodes * 40 * Z
+    return 2 * exports + 4 * (n_ns + 1) + n_ns * 16 * Z + 40 * Z
+
+
+def kernel_name(flags, K, fused, Z, sums=False):
     from kepler_amd import accel
 
+    if sums and not flags & accel.KACC_F_SMALL_NODES:
+        return (f"kacc::interval_sums_kernel<{Z},0> (one launch per step: the interval, its exports in namespace "
+                f"order, and the previous interval's cluster partial sums in the tail blocks; achieved counts "
+                f"export_sums_bytes too)")
     if fused:
         return (f"kacc::intervals_carry_kernel<{Z},0,{256 if flags & accel.KACC_F_MEDIUM_NODES else 512}>"
                 f" ({K} intervals in one launch, state carried on chip; "
@@ -1056,13 +1300,13 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_traffic(args, sizes, K, fused):
+def pmc_traffic(args, sizes, K, fused, sums=False):
     """roofline.traffic: HBM bytes per interval from profiles/pmc_traffic.json (rocprofv3 --pmc
     FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_summary.py) ONLY when that entry was measured on this
     very build (sha256 of libkepler_accel.so) and these sizes; otherwise null, with the reason."""
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     key = (f"config{args.config}" + (f"_frag{args.fragment:g}" if args.fragment else "")
-           + (f"_k{K}" if fused else ""))
+           + (f"_k{K}" if fused else "") + ("_sums" if sums else ""))
     if not os.path.exists(pmc_path):
         return None, "no profiles/pmc_traffic.json"
     with open(pmc_path) as f:

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define KACC_ABI_VERSION 4u
+#define KACC_ABI_VERSION 5u
 #define KACC_MAX_ZONES 8u
 
 /* Status codes. */
@@ -220,6 +220,16 @@ typedef struct kacc_interval {
    * through as device pointers.                                             */
   uint64_t *pod_export;
   uint64_t *node_export;
+  /* Optional INPUT (ABI 5, NULL = identity; a device pointer in every path,
+   * passed through by kacc_batch_submit like the exports): [n_pods] the
+   * pod_export row of batch pod q, each < n_pods and no row given twice (a row
+   * given twice is not detected: two pods would write one record).  With the rows of a namespace CSR (pod q of namespace k at its place in
+   * ns_pod_off[k] .. ns_pod_off[k+1]) the export is in NAMESPACE order and its
+   * partial sums stream contiguous records (kacc_export_sums.ns_ordered)
+   * instead of gathering one record per pod (Pod.Namespace,
+   * resource/types.go:109).  A row >= n_pods raises KACC_ERANGE and is not
+   * written.                                                                 */
+  const uint32_t *pod_export_pos;
 } kacc_interval;
 
 /* Device-resident state / result tables.  [n*Z+z] tables are node-major or
@@ -483,6 +493,46 @@ int kacc_allreduce_exports(kacc_cluster *c, uint32_t n_ns, const uint32_t *const
                            const uint64_t *const *node_export, uint64_t *const *out_energy,
                            double *const *out_power, uint64_t *const *out_node_energy,
                            double *const *out_node_power, void *const *streams, void *const *comm_streams);
+/* ---- cluster partial sums of an earlier interval, in the next one's launch --
+ * The per-shard partial sums of kacc_cluster_partials (namespace sums and the
+ * cluster node totals) computed from an interval's EXPORTS, so that they can run
+ * inside the NEXT interval's kernel launch: its sums workgroups are dispatched
+ * behind the node workgroups and fill the launch's tail, and a collection step is
+ * ONE launch instead of two (each kernel boundary on a stream costs several us:
+ * DESIGN §7).  Results are bit-identical to kacc_cluster_partials over the tables
+ * that interval left (the same per-lane order; namespace-ordered exports give
+ * the same sums as the slot CSR they were ordered by).  No reference call is
+ * replaced: the cluster sums are PromQL's in the reference
+ * (internal/resource/types.go:106-110).                                     */
+typedef struct kacc_export_sums {
+  uint32_t n_ns;               /* namespaces (0: no namespace sums)                  */
+  uint32_t n_pods;             /* rows of pod_export (the exporting batch's n_pods)  */
+  uint32_t n_nodes;            /* rows of node_export (its n_nodes)                  */
+  uint32_t ns_ordered;         /* 1: pod_export is in namespace order (written through
+                                  kacc_interval.pod_export_pos): namespace k owns rows
+                                  [ns_pod_off[k], ns_pod_off[k+1]) and ns_pod_row is
+                                  not read; 0: it owns rows ns_pod_row[ns_pod_off[k] ..] */
+  const uint32_t *ns_pod_off;  /* [n_ns + 1] (device)                                */
+  const uint32_t *ns_pod_row;  /* [ns_pod_off[n_ns]] batch pod rows (device)         */
+  const uint64_t *pod_export;  /* [n_pods][2Z] (device)                              */
+  const uint64_t *node_export; /* [n_nodes][5Z] (device); NULL: no node totals       */
+  uint64_t *out_energy;        /* [n_ns * Z] u64 namespace energy (device)           */
+  double *out_power;           /* [n_ns * Z] f64 namespace power                     */
+  uint64_t *out_node_energy;   /* [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal       */
+  double *out_node_power;      /* [3Z]: Σ Power, Σ ActivePower, Σ IdlePower          */
+} kacc_export_sums;
+/* One interval (as kacc_run_interval) plus, in the same launch, the partial sums
+ * `prev` of an earlier interval's exports (NULL: none).  The exports `prev` reads
+ * must not be the ones dev_batch writes (double-buffer them: KACC_EINVAL on
+ * overlap); they were complete when this call's work starts on `stream` (the
+ * interval that wrote them was queued there before).  The outputs are complete
+ * when this call's work is.  Batches of KACC_F_SMALL_NODES, and node totals over
+ * more than 16384 nodes, run the sums as a launch of their own (same results).  */
+int kacc_run_interval_sums(kacc_ctx *ctx, const kacc_interval *dev_batch, const kacc_export_sums *prev,
+                           void *stream);
+/* The same partial sums alone, as one launch on `stream` (the last interval's). */
+int kacc_run_export_sums(kacc_ctx *ctx, const kacc_export_sums *sums, void *stream);
+
 /* Cluster pod gather: shard s contributes n_pods[s] (HOST) pods, its slots
  * pod_slot[s] (device), in that order; every local shard receives all pods of
  * the cluster in (rank, shard) order — energy u64 / power f64 [total*Z] into
@@ -567,6 +617,60 @@ int kacc_slotmap_set_policy(kacc_slotmap *m, uint32_t policy);
 int kacc_slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, const void *keys,
                    const uint32_t *node_status, uint32_t *out_slot, uint64_t *term_key,
                    uint32_t *term_slot, uint32_t *term_count, uint32_t *out_span, void *stream);
+
+/* ---- CPU-tick input format: CPUTimeDelta on the device (ABI 5) -------------
+ * A leaner PCIe format for the host path.  The reference computes every
+ * process's CPUTimeDelta on the host (populateProcessFields,
+ * internal/resource/informer.go:512-524) from its cumulative CPU ticks
+ * (procWrapper.CPUTime, procfs_reader.go:75-82: float64(STime+UTime) / 100):
+ *     cpuTotalTime = float64(ticks) / 100;  CPUTimeDelta = cpuTotalTime - p.CPUTotalTime
+ * where p.CPUTotalTime is the same expression of the ticks the informer saw at the
+ * PID's previous reading (0 for a new process).  A tick map keeps, per process
+ * slot, the ticks of its last reading (u64, on the device), so the caller sends
+ * only each row's tick INCREMENT — 2 bytes for almost every row instead of the
+ * 8-byte float64 Δ — and kacc_ticks_delta writes Go's float64 CPUTimeDelta into
+ * the interval batch's proc_cpu_delta, bit-exact (float64(uint64) correctly
+ * rounded, one IEEE division by 100, one subtraction).  With the slot words from
+ * kacc_slot_join on the device as well, a process row crosses PCIe as its PID
+ * (4 B) plus its increment (2 B): 6 bytes instead of 12.
+ *
+ * Per row r of node n (rows of a KACC_NODE_READ_ERROR node are skipped: the
+ * reference skips Refresh for that node, monitor.go:399-410, so neither its
+ * informer cache nor the tick map moves):
+ *   prev  = proc_slot[r] has KACC_SLOT_NEW ? 0 : map[slot]      (new process)
+ *   inc   = dticks[r] != KACC_TICKS_ESCAPED ? dticks[r] : the escape of row r
+ *   now   = prev + inc (mod 2^64: a negative increment — a reused PID whose
+ *           new process has fewer ticks, informer.go:518 — is an escape)
+ *   proc_cpu_delta[r] = float64(now)/100 - float64(prev)/100;  map[slot] = now
+ * Escapes: increments outside 0 .. 0xfffe (big first readings of new
+ * processes, negative ones), per node n at [esc_off[n], esc_off[n+1]) of
+ * esc_row (absolute row numbers inside the node's rows) / esc_ticks (int64).
+ * The map starts at 0 (every process's first reading must be a NEW row, as
+ * the slot join makes it).  Errors (a slot past the capacity, an escape row
+ * outside its node, an escaped row without an escape) raise KACC_ERANGE at
+ * kacc_sync; such rows get Δ 0.                                              */
+#define KACC_TICKS_ESCAPED 0xffffu
+#define KACC_USER_HZ 100u /* procfs_reader.go:73 userHZ */
+typedef struct kacc_tickmap kacc_tickmap;
+typedef struct kacc_ticks {
+  uint32_t n_nodes, n_procs, n_escapes, reserved0;
+  const uint32_t *proc_off;   /* [n_nodes + 1] the batch's (device)                  */
+  const uint32_t *node_status;/* [n_nodes] or NULL                                   */
+  const uint32_t *proc_slot;  /* [n_procs] slot words (kacc_slot_join's out_slot)    */
+  const uint16_t *dticks;     /* [n_procs] tick increments, KACC_TICKS_ESCAPED = escape */
+  const uint32_t *esc_off;    /* [n_nodes + 1] (may be NULL when n_escapes == 0)     */
+  const uint32_t *esc_row;    /* [n_escapes]                                         */
+  const int64_t *esc_ticks;   /* [n_escapes]                                         */
+  double *proc_cpu_delta;     /* [n_procs] OUT: CPUTimeDelta (the batch's array)     */
+} kacc_ticks;
+/* A tick map over the context's process slots (all zero). */
+int kacc_tickmap_create(kacc_ctx *ctx, kacc_tickmap **out);
+void kacc_tickmap_destroy(kacc_tickmap *m);
+int kacc_tickmap_reset(kacc_tickmap *m);
+/* Device pointers, asynchronous on `stream` (NULL = the context's stream). */
+int kacc_ticks_delta(kacc_tickmap *m, const kacc_ticks *t, void *stream);
+/* Synchronous copy of count ticks from slot `first` (tests, checkpoints). */
+int kacc_tickmap_download(kacc_tickmap *m, uint64_t first, uint64_t count, uint64_t *host_dst);
 
 /* ---- host packer: informer records -> interval CSR -----
  * The step before the path: what resource.Informer.Refresh

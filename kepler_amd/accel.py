@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KACC_LIB", os.path.join(_HERE, "lib", "libkepler_accel.so"))  # KACC_LIB: A/B builds
 
-KACC_ABI_VERSION = 4
+KACC_ABI_VERSION = 5
 KACC_MAX_ZONES = 8
 KACC_OK = 0
 KACC_EINVAL = -1
@@ -117,6 +117,11 @@ EXPORTS = [
     "kacc_slotmap_reset",
     "kacc_slotmap_set_policy",
     "kacc_slot_join",
+    "kacc_tickmap_create",
+    "kacc_tickmap_destroy",
+    "kacc_tickmap_reset",
+    "kacc_ticks_delta",
+    "kacc_tickmap_download",
     "kacc_abi_version",
     "kacc_create",
     "kacc_destroy",
@@ -148,6 +153,8 @@ EXPORTS = [
     "kacc_cluster_partials",
     "kacc_allreduce_sums",
     "kacc_allreduce_exports",
+    "kacc_run_interval_sums",
+    "kacc_run_export_sums",
     "kacc_gather_pods",
     "kacc_last_error_copy",
     "kacc_intervals_bytes",
@@ -236,8 +243,9 @@ class KaccShape(ctypes.Structure):
     _fields_ = [(n, c_uint32) for n in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods", "intervals")]
 
 
-# optional per-interval OUTPUT arrays (device): the cluster-total exports
-INTERVAL_OUTPUTS = ["pod_export", "node_export"]
+# optional per-interval OUTPUT arrays (device): the cluster-total exports, and (ABI 5) the
+# export row of each batch pod (an input: namespace order)
+INTERVAL_OUTPUTS = ["pod_export", "node_export", "pod_export_pos"]
 
 
 class KaccInterval(ctypes.Structure):
@@ -249,6 +257,38 @@ class KaccInterval(ctypes.Structure):
         ("n_pods", c_uint32),
         ("flags", c_uint32),
     ] + [(name, c_void_p) for name in INTERVAL_ARRAYS + INTERVAL_OUTPUTS]
+
+
+class KaccExportSums(ctypes.Structure):
+    """kacc_export_sums: partial sums of an earlier interval's exports (kacc_run_interval_sums)."""
+    _fields_ = [(n, c_uint32) for n in ("n_ns", "n_pods", "n_nodes", "ns_ordered")] + [
+        (n, c_void_p) for n in ("ns_pod_off", "ns_pod_row", "pod_export", "node_export", "out_energy", "out_power",
+                                "out_node_energy", "out_node_power")]
+
+
+KACC_TICKS_ESCAPED = 0xFFFF
+KACC_USER_HZ = 100
+
+
+class KaccTicks(ctypes.Structure):
+    """kacc_ticks: one interval's CPU-tick increments (kacc_ticks_delta)."""
+    _fields_ = [(n, c_uint32) for n in ("n_nodes", "n_procs", "n_escapes", "reserved0")] + [
+        (n, c_void_p) for n in ("proc_off", "node_status", "proc_slot", "dticks", "esc_off", "esc_row", "esc_ticks",
+                                "proc_cpu_delta")]
+
+
+def encode_ticks(proc_off, ticks_now, ticks_prev):
+    """Host side of the tick format: per row the increment ticks_now - ticks_prev (u64 modular;
+    ticks_prev = 0 for a NEW row) as u16, or KACC_TICKS_ESCAPED with an int64 escape when it is
+    outside 0 .. 0xfffe.  Returns dticks [P] u16, esc_off [N+1] u32, esc_row [E] u32 (ascending
+    within each node), esc_ticks [E] i64."""
+    proc_off = np.asarray(proc_off, dtype=np.int64)
+    inc = (np.asarray(ticks_now, dtype=np.uint64) - np.asarray(ticks_prev, dtype=np.uint64)).view(np.int64)
+    esc = (inc < 0) | (inc >= KACC_TICKS_ESCAPED)
+    dticks = np.where(esc, KACC_TICKS_ESCAPED, inc).astype(np.uint16)
+    esc_row = np.flatnonzero(esc).astype(np.uint32)
+    esc_off = np.searchsorted(esc_row, proc_off).astype(np.uint32)
+    return dticks, esc_off, esc_row, inc[esc_row.astype(np.int64)].astype(np.int64)
 
 
 class AccelError(RuntimeError):
@@ -307,6 +347,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
                                         POINTER(c_void_p), POINTER(c_void_p)]
     lib.kacc_allreduce_exports.argtypes = [c_void_p, c_uint32, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_uint32),
                                            POINTER(c_void_p), POINTER(c_uint32)] + [POINTER(c_void_p)] * 7
+    lib.kacc_tickmap_create.argtypes = [c_void_p, POINTER(c_void_p)]
+    lib.kacc_tickmap_destroy.argtypes = [c_void_p]
+    lib.kacc_tickmap_destroy.restype = None
+    lib.kacc_tickmap_reset.argtypes = [c_void_p]
+    lib.kacc_ticks_delta.argtypes = [c_void_p, POINTER(KaccTicks), c_void_p]
+    lib.kacc_tickmap_download.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p]
+    lib.kacc_run_interval_sums.argtypes = [c_void_p, POINTER(KaccInterval), POINTER(KaccExportSums), c_void_p]
+    lib.kacc_run_export_sums.argtypes = [c_void_p, POINTER(KaccExportSums), c_void_p]
     lib.kacc_gather_pods.argtypes = [c_void_p, POINTER(c_uint32), POINTER(c_void_p), c_uint64, POINTER(c_void_p),
                                      POINTER(c_void_p), POINTER(c_uint64), POINTER(c_uint64), POINTER(c_void_p)]
     lib.kacc_batch_submit.argtypes = [c_void_p, c_void_p]
@@ -516,6 +564,16 @@ class Accel:
     def run_interval(self, dev_interval: KaccInterval, stream: int = 0) -> None:
         self._check(self.lib.kacc_run_interval(self.ctx, ctypes.byref(dev_interval), c_void_p(stream or None)))
 
+    def run_interval_sums(self, dev_interval: KaccInterval, sums: Optional[KaccExportSums], stream: int = 0) -> None:
+        """kacc_run_interval_sums: the interval and, in its launch, the partial sums of an earlier
+        interval's exports (``sums``; None: a plain interval)."""
+        self._check(self.lib.kacc_run_interval_sums(self.ctx, ctypes.byref(dev_interval),
+                                                    ctypes.byref(sums) if sums is not None else None, stream))
+
+    def export_sums(self, sums: KaccExportSums, stream: int = 0) -> None:
+        """kacc_run_export_sums: the partial sums of an interval's exports as one launch."""
+        self._check(self.lib.kacc_run_export_sums(self.ctx, ctypes.byref(sums), stream))
+
     def run_intervals(self, dev_intervals, stream: int = 0) -> None:
         """kacc_run_intervals: consecutive intervals issued back to back from C."""
         arr = (KaccInterval * len(dev_intervals))(*dev_intervals)
@@ -657,6 +715,42 @@ class SlotMap:
         if self.handle:
             self.lib.kacc_slotmap_destroy(self.handle)
             self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TickMap:
+    """kacc_tickmap: per process slot, the ticks (STime+UTime) of its last reading; kacc_ticks_delta
+    turns a batch's tick increments into Go's CPUTimeDelta on the device."""
+
+    def __init__(self, accel: Accel):
+        self.accel = accel
+        self.lib = accel.lib
+        h = c_void_p()
+        accel._check(self.lib.kacc_tickmap_create(accel.ctx, ctypes.byref(h)))
+        self.h = h
+
+    def reset(self) -> None:
+        self.accel._check(self.lib.kacc_tickmap_reset(self.h))
+
+    def delta(self, t: KaccTicks, stream: int = 0) -> None:
+        self.accel._check(self.lib.kacc_ticks_delta(self.h, ctypes.byref(t), stream))
+
+    def download(self, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        if count is None:
+            count = self.accel.cfg.proc_slots - first
+        out = np.zeros(count, dtype=np.uint64)
+        self.accel._check(self.lib.kacc_tickmap_download(self.h, first, count, out.ctypes.data))
+        return out
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.kacc_tickmap_destroy(self.h)
+            self.h = None
 
     def __del__(self):  # pragma: no cover
         try:

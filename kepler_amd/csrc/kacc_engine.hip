@@ -448,16 +448,33 @@ __device__ __forceinline__ void store_proc(const DevState &st, uint64_t s, const
 // Plain stores: a lane's record leaves as Z/2 + Z/2 16-B pieces, so each wave
 // instruction writes every 2Z-th 16 B of the wave's span; L2 merges the pieces
 // into full lines (non-temporal, each piece would reach HBM as a partial line).
+// The export row of batch pod q (kacc_interval.pod_export_pos: namespace order),
+// or ~0u when it is out of range (raised; nothing is written).
+__device__ __forceinline__ uint32_t export_row(const kacc_interval &b, uint32_t q, uint32_t *err) {
+  if (!b.pod_export_pos) return q;
+  const uint32_t r = b.pod_export_pos[q];
+  if (r >= b.n_pods) {
+    atomicOr(err, 1u << 1);  // kErrOffsets
+    return ~0u;
+  }
+  return r;
+}
 template <int Z>
-__device__ __forceinline__ void export_pod(const kacc_interval &b, uint32_t q, const uint64_t (&E)[Z],
-                                           const double (&P)[Z]) {
-  if (!b.pod_export) return;
-  uint64_t *o = b.pod_export + static_cast<uint64_t>(q) * (2 * Z);
+__device__ __forceinline__ void export_pod_at(const kacc_interval &b, uint32_t row, const uint64_t (&E)[Z],
+                                              const double (&P)[Z]) {
+  if (!b.pod_export || row == ~0u) return;
+  uint64_t *o = b.pod_export + static_cast<uint64_t>(row) * (2 * Z);
   store_row<Z, false, uint64_t>(o, 0, E);
   store_row<Z, false, double>(reinterpret_cast<double *>(o), 1, P);
 }
 template <int Z>
-__device__ __forceinline__ void export_pod_zero(const kacc_interval &b, uint32_t q) {
+__device__ __forceinline__ void export_pod(const kacc_interval &b, uint32_t q, const uint64_t (&E)[Z],
+                                           const double (&P)[Z], uint32_t *err) {
+  if (!b.pod_export) return;
+  export_pod_at<Z>(b, export_row(b, q, err), E, P);
+}
+template <int Z>
+__device__ __forceinline__ void export_pod_zero(const kacc_interval &b, uint32_t q, uint32_t *err) {
   uint64_t E[Z];
   double P[Z];
 #pragma unroll
@@ -465,7 +482,7 @@ __device__ __forceinline__ void export_pod_zero(const kacc_interval &b, uint32_t
     E[z] = 0;
     P[z] = 0.0;
   }
-  export_pod<Z>(b, q, E, P);
+  export_pod<Z>(b, q, E, P, err);
 }
 // Node n, zone z: ActiveEnergyTotal, IdleEnergyTotal, Power, ActivePower, IdlePower.
 template <int Z>
@@ -717,14 +734,14 @@ __device__ __forceinline__ void export_skipped(const kacc_interval &b, const Dev
     for (uint32_t q = r.q0 + lane; q < r.q1; q += nlanes) {
       const uint64_t sl = b.pod_slot[q] & KACC_SLOT_MASK;
       if (sl >= st.pod_slots) {
-        export_pod_zero<Z>(b, q);
+        export_pod_zero<Z>(b, q, st.err);
         continue;
       }
       uint64_t E[Z];
       double P[Z];
       load_row<Z>(st.pod_energy, pod_row(sl), E);
       load_row_f64<Z>(st.pod_power, pod_row(sl), P);
-      export_pod<Z>(b, q, E, P);
+      export_pod<Z>(b, q, E, P, st.err);
     }
   }
 }
@@ -794,7 +811,9 @@ __device__ __forceinline__ bool fits_fast(const NodeRanges &r) {
 // kW: 8-byte words between consecutive rows — 2Z both for the state tables
 // (rows = pod slots: one [energy Z | power Z] record per slot, pod_row) and for
 // an interval's pod export (rows = batch pod rows, the same record).
-template <int Z, int kW = 2 * Z, int kThreads = kBlock>
+// kIdentity: the rows are the CSR positions themselves (an export written in namespace
+// order, kacc_interval.pod_export_pos): each namespace is a run of contiguous records.
+template <int Z, int kW = 2 * Z, int kThreads = kBlock, bool kIdentity = false>
 __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, const uint32_t *__restrict__ off,
                                                 const uint32_t *__restrict__ slots, const uint64_t *__restrict__ pe,
                                                 const double *__restrict__ pp, uint64_t pod_slots, uint64_t *out_e,
@@ -809,13 +828,21 @@ __device__ __forceinline__ void namespace_block(uint32_t blk, uint32_t n_ns, con
     e[z] = 0;
     p[z] = 0.0;
   }
-  const uint32_t beg = active ? off[k] : 0u, end = active ? off[k + 1] : 0u;
+  const uint32_t beg = active ? off[k] : 0u;
+  uint32_t end = active ? off[k + 1] : 0u;
+  if (pod_slots == 0 && end > beg) {  // no rows to gather from (an empty export): nothing is read
+    raise_err(err, kErrNs);
+    end = beg;
+  }
   // loads unconditional from clamped indices (a predicated load makes the
   // compiler branch around it and wait per element); the adds are masked
   for (uint32_t j0 = beg + lane; j0 < end; j0 += kNsLanes * kNsUnroll) {
     uint32_t sl[kNsUnroll];
 #pragma unroll
-    for (int u = 0; u < kNsUnroll; ++u) sl[u] = slots[min(j0 + u * kNsLanes, end - 1)] & KACC_SLOT_MASK;
+    for (int u = 0; u < kNsUnroll; ++u) {
+      const uint32_t j = min(j0 + u * kNsLanes, end - 1);
+      sl[u] = kIdentity ? j : slots[j] & KACC_SLOT_MASK;
+    }
     uint64_t er[kNsUnroll][Z];
     double pr[kNsUnroll][Z];
 #pragma unroll
@@ -922,6 +949,42 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
       na.out_p[(t - 2) * Z + z] = r;
     }
   }
+}
+
+// Partial sums of an earlier interval's exports inside an interval launch
+// (kacc_run_interval_sums): after the n_nodes node workgroups come node_blocks
+// node-total columns and ns_blocks namespace-sum blocks of kTpb threads — the
+// same per-lane orders as cluster_partials_kernel (node_column_block sums with
+// its first kBlock lanes whatever the block size; a namespace is kNsLanes lanes
+// wherever its block starts), so the same bits.  Dispatched behind the node
+// workgroups, they run in the launch's tail, when the last residency round leaves
+// compute units free, and read only the earlier interval's exports (never a
+// table this launch writes): no wait, no second launch.
+struct SumsArgs {
+  uint32_t node_blocks, ns_blocks, n_ns, ordered;
+  const uint32_t *off, *rows;
+  const uint64_t *pe;
+  const double *pp;
+  uint64_t n_pods;
+  uint64_t *out_e;
+  double *out_p;
+  NodeTotalsArgs na;
+};
+
+template <int Z, int kThreads>
+__device__ __forceinline__ void sums_block(const SumsArgs &sa, uint32_t sb, uint32_t *err) {
+  if (sb < sa.node_blocks) {
+    __shared__ uint64_t s_w[kBlock / 64];
+    node_column_block<Z>(sa.na, sb, s_w);
+    return;
+  }
+  sb -= sa.node_blocks;
+  if (sa.ordered)
+    namespace_block<Z, 2 * Z, kThreads, true>(sb, sa.n_ns, sa.off, sa.rows, sa.pe, sa.pp, sa.n_pods, sa.out_e,
+                                              sa.out_p, err);
+  else
+    namespace_block<Z, 2 * Z, kThreads, false>(sb, sa.n_ns, sa.off, sa.rows, sa.pe, sa.pp, sa.n_pods, sa.out_e,
+                                               sa.out_p, err);
 }
 
 // One node snapshot of one interval on workgroup `blk` (interval_kernel).
@@ -1237,16 +1300,18 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   }
   auto aggregate_out = [&]() {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
     if (!a_ok) {
-      if (role == 3) export_pod_zero<Z>(b, q0 + j);
+      if (role == 3) export_pod_zero<Z>(b, q0 + j, st.err);
       return;
     }
     if constexpr (kLateAgg<V>) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
+    // a pod's export row (namespace order) loads beside its previous totals: no extra round trip
+    const uint32_t xrow = role == 3 && b.pod_export ? export_row(b, q0 + j, st.err) : ~0u;
     uint64_t E[Z];
     double P[Z];
     const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta,
                                           (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
     store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
-    if (role == 3) export_pod<Z>(b, q0 + j, E, P);
+    if (role == 3) export_pod_at<Z>(b, xrow, E, P);
   };
   if constexpr (!kLateAgg<V>) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
@@ -1311,6 +1376,18 @@ template <int Z, int V>
 #endif
 __global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
 void interval_kernel(const kacc_interval b, const DevState st) {
+  interval_node<Z, V>(b, st, blockIdx.x);
+}
+
+// interval_kernel + the partial sums of an earlier interval's exports in its tail
+// blocks (kacc_run_interval_sums; SumsArgs below)
+template <int Z, int V>
+__global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
+void interval_sums_kernel(const kacc_interval b, const DevState st, const SumsArgs sa) {
+  if (blockIdx.x >= b.n_nodes) {
+    sums_block<Z, kTpb<V>>(sa, blockIdx.x - b.n_nodes, st.err);
+    return;
+  }
   interval_node<Z, V>(b, st, blockIdx.x);
 }
 
@@ -2269,7 +2346,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
       const uint32_t a_s = a_w[h] & KACC_SLOT_MASK;
       if (role == 0) continue;
       if (a_s >= cap_of(role)) {
-        if (role == 3) export_pod_zero<Z>(b, q0 + index_of(i));
+        if (role == 3) export_pod_zero<Z>(b, q0 + index_of(i), st.err);
         continue;
       }
       uint64_t E[Z];
@@ -2277,7 +2354,7 @@ __global__ __launch_bounds__(64 * kSmallWaves) __attribute__((amdgpu_waves_per_e
       const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta[h],
                                             (a_w[h] & KACC_SLOT_NEW) != 0, a_prev[h], E, P);
       store_agg<Z, kNT && kNtAggStores>(st, role, a_s, E, P, ratio, n);
-      if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P);
+      if (role == 3) export_pod<Z>(b, q0 + index_of(i), E, P, st.err);
     }
   };
   if constexpr (KACC_SMALL_LATE_AGG == 0) aggregate_out();
@@ -2824,9 +2901,9 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       const double ratio =
           attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
       store_agg<Z, kNT>(st, a_role, s, E, P, ratio, n);
-      if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P);
+      if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P, st.err);
     } else if (a_role == 3 && !a_ok) {
-      export_pod_zero<Z>(b, qb + (utid - ncv));
+      export_pod_zero<Z>(b, qb + (utid - ncv), st.err);
     }
     if (defer && a_ok) {
       const uint32_t i = atomicAdd(st.defer_ctr, 1u);
@@ -2869,7 +2946,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       const bool ok = s < cap_of(role);
       if (!ok) {
         raise_err(st.err, kErrSlot);
-        if (role == 3) export_pod_zero<Z>(b, qb + (j - ncv));
+        if (role == 3) export_pod_zero<Z>(b, qb + (j - ncv), st.err);
         continue;
       }
       if (role == 3) {
@@ -2953,11 +3030,11 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     attribute_row<Z>(a, a.live_pod, delta, (w & KACC_SLOT_NEW) != 0, prev, E, P);
     store_row<Z, kNT, uint64_t>(st.pod_energy, pod_row(sl), E);
     store_row<Z, kNT, double>(st.pod_power, pod_row(sl), P);
-    export_pod<Z>(b, q, E, P);
+    export_pod<Z>(b, q, E, P, st.err);
   }
 }
 
-template <int Z, int kW = 2 * Z, bool kWideCols = false>
+template <int Z, int kW = 2 * Z, bool kWideCols = false, bool kIdentity = false>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
                                                                   const uint32_t *__restrict__ slots,
@@ -2973,12 +3050,14 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
   // The block count and the 5Z column blocks are the only coupling between blocks.
   const uint32_t nb = gridDim.x - ns_blocks;
   if (blockIdx.x >= nb) {
-    namespace_block<Z, kW>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p, err);
+    namespace_block<Z, kW, kBlock, kIdentity>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p,
+                                               err);
     return;
   }
   __shared__ uint64_t s_w[kBlock / 64];
   node_column_block<Z, kWideCols>(na, blockIdx.x, s_w);  // block b owns output value b: column b / Z, zone b % Z
 }
+
 
 // Elements [first, first + count) of the derived process power table
 // ([slot*Z + z], kacc_derive.hpp), grid-stride.
@@ -3230,7 +3309,8 @@ kacc::NodeTotalsArgs node_totals_args(const kacc_ctx *ctx, uint64_t live, const 
 template <int Z>
 void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t *slots, kacc_ctx *ctx,
                              uint64_t *out_e, double *out_p, const kacc::NodeTotalsArgs &na, uint32_t node_blocks,
-                             hipStream_t st, const uint64_t *pod_export = nullptr, uint64_t n_pods = 0) {
+                             hipStream_t st, const uint64_t *pod_export = nullptr, uint64_t n_pods = 0,
+                             bool ordered = false) {
   const uint32_t per_block = kacc::kBlock / kacc::kNsLanes;
   const uint32_t ns_blocks = (n_ns + per_block - 1) / per_block;
   // pod_export NULL: the pod tables, one [energy | power] record per slot like an export row
@@ -3238,12 +3318,85 @@ void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t 
   const double *pp = pod_export ? reinterpret_cast<const double *>(pod_export + Z)
                                 : (const double *)ctx->tables[KACC_T_POD_POWER];
   const uint64_t rows = pod_export ? n_pods : ctx->cfg.pod_slots;
-  if (na.n_nodes > kacc::kColWideNodes && node_blocks)
+  const bool wide = na.n_nodes > kacc::kColWideNodes && node_blocks;
+  if (wide && ordered)
+    KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, true, true>), dim3(ns_blocks + node_blocks),
+                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+  else if (wide)
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, true>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock),
                 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+  else if (ordered)
+    KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, false, true>), dim3(ns_blocks + node_blocks),
+                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
   else
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
                 ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+}
+
+// An interval and the partial sums of an earlier interval's exports in ONE launch
+// (kacc_run_interval_sums): interval_sums_kernel, then the big-node launches as
+// launch_zv does.
+template <int Z>
+void launch_fused(const kacc_interval &b, const kacc::DevState &s, const kacc::SumsArgs &sa, hipStream_t st) {
+  KACC_LAUNCH((kacc::interval_sums_kernel<Z, 0>), dim3(b.n_nodes + sa.node_blocks + sa.ns_blocks),
+              dim3(kacc::kTpb<0>), KACC_FAST_EXTRA_LDS, st, b, s, sa);
+  if (b.flags & (KACC_F_FAST_NODES | KACC_F_SMALL_NODES)) return;
+  const uint32_t chunk_grid = std::min<uint32_t>(s.item_cap, kacc::kChunkGrid);
+  KACC_LAUNCH((kacc::chunk_kernel<Z, 0>), dim3(chunk_grid), dim3(kacc::kChunkThreads), 0, st, b, s);
+  KACC_LAUNCH((kacc::pod_kernel<Z, 0>), dim3(kacc::kPodGrid), dim3(kacc::kBlock), 0, st, b, s);
+}
+
+void launch_fused_z(uint32_t Z, const kacc_interval &b, const kacc::DevState &s, const kacc::SumsArgs &sa,
+                    hipStream_t st) {
+  switch (Z) {
+    case 1: launch_fused<1>(b, s, sa, st); break;
+    case 2: launch_fused<2>(b, s, sa, st); break;
+    case 3: launch_fused<3>(b, s, sa, st); break;
+    case 4: launch_fused<4>(b, s, sa, st); break;
+    case 5: launch_fused<5>(b, s, sa, st); break;
+    case 6: launch_fused<6>(b, s, sa, st); break;
+    case 7: launch_fused<7>(b, s, sa, st); break;
+    default: launch_fused<8>(b, s, sa, st); break;
+  }
+}
+
+// [p, p + bytes) and [q, q + bytes2) share a byte
+bool overlaps(const void *p, uint64_t bytes, const void *q, uint64_t bytes2) {
+  if (!p || !q || !bytes || !bytes2) return false;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p), c = reinterpret_cast<uintptr_t>(q);
+  return a < c + bytes2 && c < a + bytes;
+}
+
+// The checked device arguments of a kacc_export_sums, for namespace blocks of
+// `threads` threads.
+int sums_args(kacc_ctx *ctx, const kacc_export_sums *x, uint32_t threads, kacc::SumsArgs &sa) {
+  if (!x) return fail(ctx, KACC_EINVAL, "export sums: NULL descriptor");
+  const uint64_t Z = ctx->cfg.zones;
+  const bool nodes = x->out_node_energy || x->out_node_power;
+  if (nodes && (!x->out_node_energy || !x->out_node_power))
+    return fail(ctx, KACC_EINVAL, "export sums: node totals need both output arrays");
+  if (nodes && x->n_nodes && !x->node_export) return fail(ctx, KACC_EINVAL, "export sums: node_export is NULL");
+  if (x->n_nodes > ctx->cfg.nodes)
+    return fail(ctx, KACC_EINVAL, "export sums: n_nodes %u exceeds node capacity", x->n_nodes);
+  if (x->n_ns && (!x->ns_pod_off || !x->out_energy || !x->out_power || (!x->ns_ordered && !x->ns_pod_row) ||
+                  (x->n_pods && !x->pod_export)))
+    return fail(ctx, KACC_EINVAL, "export sums: NULL namespace / pod export array");
+  if (x->ns_ordered > 1) return fail(ctx, KACC_EINVAL, "export sums: ns_ordered must be 0 or 1");
+  sa = kacc::SumsArgs{};
+  sa.node_blocks = nodes ? static_cast<uint32_t>(5 * Z) : 0u;
+  const uint32_t per_block = threads / kacc::kNsLanes;
+  sa.ns_blocks = (x->n_ns + per_block - 1) / per_block;
+  sa.n_ns = x->n_ns;
+  sa.ordered = x->ns_ordered;
+  sa.off = x->ns_pod_off;
+  sa.rows = x->ns_pod_row;
+  sa.pe = x->pod_export;
+  sa.pp = x->pod_export ? reinterpret_cast<const double *>(x->pod_export + Z) : nullptr;
+  sa.n_pods = x->pod_export ? x->n_pods : 0;  // no export: no row to read (a non-empty namespace raises)
+  sa.out_e = x->out_energy;
+  sa.out_p = x->out_power;
+  sa.na = node_totals_args(ctx, nodes ? x->n_nodes : 0, x->node_export, x->out_node_energy, x->out_node_power);
+  return KACC_OK;
 }
 
 // Chunk-item list sized for the worst case of a batch (every node oversized,
@@ -3911,6 +4064,7 @@ int kacc_batch_submit(kacc_ctx *ctx, kacc_batch *bt) {
     dv[k].flags = (h.flags & ~KACC_F_TRUSTED_LAYOUT) | (h.n_nodes ? node_size_flags(h) : 0u);
     dv[k].pod_export = h.pod_export;  // device outputs the caller owns, passed through
     dv[k].node_export = h.node_export;
+    dv[k].pod_export_pos = h.pod_export_pos;  // a device input, like the exports
     for (const BatchField &f : kBatchFields)  // honour optional arrays the caller switched off
       if (!field_ptr(h, f)) field_ptr(dv[k], f) = nullptr;
     max_nodes = std::max<uint64_t>(max_nodes, h.n_nodes);
@@ -4113,6 +4267,68 @@ int kacc_internal_export_partials(kacc_ctx *ctx, uint32_t n_ns, const uint32_t *
   }
 #undef KACC_PARTIALS
   KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_run_export_sums(kacc_ctx *ctx, const kacc_export_sums *x, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  const kacc::TimingScope timing(ctx);
+  kacc::SumsArgs sa;
+  int rc = sums_args(ctx, x, kacc::kBlock, sa);
+  if (rc != KACC_OK) return rc;
+  if (!sa.n_ns && !sa.node_blocks) return KACC_OK;
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  (void)hipGetLastError();
+#define KACC_XSUMS(Z_)                                                                                        \
+  launch_cluster_partials<Z_>(sa.n_ns, sa.off, sa.ordered ? nullptr : sa.rows, ctx, sa.out_e, sa.out_p, sa.na, \
+                              sa.node_blocks, st, sa.pe, sa.n_pods, sa.ordered != 0)
+  switch (ctx->cfg.zones) {
+    case 1: KACC_XSUMS(1); break;
+    case 2: KACC_XSUMS(2); break;
+    case 3: KACC_XSUMS(3); break;
+    case 4: KACC_XSUMS(4); break;
+    case 5: KACC_XSUMS(5); break;
+    case 6: KACC_XSUMS(6); break;
+    case 7: KACC_XSUMS(7); break;
+    default: KACC_XSUMS(8); break;
+  }
+#undef KACC_XSUMS
+  KACC_HIP(ctx, hipGetLastError());
+  return KACC_OK;
+}
+
+int kacc_run_interval_sums(kacc_ctx *ctx, const kacc_interval *b, const kacc_export_sums *prev, void *stream) {
+  if (!ctx) return KACC_EINVAL;
+  if (!prev) return kacc_run_interval(ctx, b, stream);
+  const kacc::TimingScope timing(ctx);
+  KACC_HIP(ctx, hipSetDevice(ctx->device));
+  int rc = check_shape(ctx, b);
+  if (rc != KACC_OK) return rc;
+  kacc::SumsArgs sa;
+  if ((rc = sums_args(ctx, prev, kacc::kTpb<0>, sa)) != KACC_OK) return rc;
+  const uint64_t Z = ctx->cfg.zones;
+  // the sums read an EARLIER interval's exports while this one writes its own
+  if (overlaps(prev->pod_export, 16 * Z * prev->n_pods, b->pod_export, 16 * Z * b->n_pods) ||
+      overlaps(prev->node_export, 40 * Z * prev->n_nodes, b->node_export, 40 * Z * b->n_nodes) ||
+      overlaps(prev->pod_export, 16 * Z * prev->n_pods, b->node_export, 40 * Z * b->n_nodes) ||
+      overlaps(prev->node_export, 40 * Z * prev->n_nodes, b->pod_export, 16 * Z * b->n_pods))
+    return fail(ctx, KACC_EINVAL, "export sums: the exports read overlap the exports this interval writes "
+                                  "(double-buffer them)");
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const bool fuse = b->n_nodes > 0 && !(b->flags & KACC_F_SMALL_NODES) &&
+                    !(sa.node_blocks && sa.na.n_nodes > kacc::kColWideNodes) &&
+                    (sa.n_ns || sa.node_blocks) &&
+                    static_cast<uint64_t>(b->n_nodes) + sa.node_blocks + sa.ns_blocks <= 0x7fffffffull;
+  if (!fuse) {  // the interval, then the sums as a launch of their own (the same results)
+    if ((rc = run_one(ctx, b, st)) != KACC_OK) return rc;
+    return kacc_run_export_sums(ctx, prev, st);  // inside this call's timing scope
+  }
+  if ((rc = ensure_items(ctx, b->n_nodes, b->n_procs, b->n_pods)) != KACC_OK) return rc;
+  (void)hipGetLastError();  // clear a stale error of an earlier call
+  launch_fused_z(ctx->cfg.zones, *b, dev_state(ctx), sa, st);
+  KACC_HIP(ctx, hipGetLastError());
+  ctx->live_nodes = b->n_nodes;
   return KACC_OK;
 }
 

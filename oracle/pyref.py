@@ -74,6 +74,33 @@ def energy_delta(cur: int, prev: int, max_e: int) -> int:
     return 0
 
 
+USER_HZ = 100  # procfs_reader.go:73 userHZ
+
+
+def go_cpu_time(ticks: int) -> float:
+    """procWrapper.CPUTime (procfs_reader.go:75-82): float64(st.STime+st.UTime) / userHZ — the uint
+    sum wraps mod 2^64, float64(uint64) rounds once (Python's float(int) rounds half to even), one
+    IEEE division."""
+    return float(ticks & U64) / USER_HZ
+
+
+class Informer:
+    """The informer's per-process CPU-time fields (populateProcessFields, informer.go:512-524) keyed
+    by an ID: p.CPUTotalTime of the PID's previous reading, 0 for a process the cache does not hold.
+    The tick format's oracle: feed it the same readings as the device tick map."""
+
+    def __init__(self):
+        self.total = {}  # ID -> p.CPUTotalTime (float64)
+
+    def read(self, pid, ticks: int, new: bool) -> float:
+        """One reading: returns p.CPUTimeDelta and updates p.CPUTotalTime.  ``new``: the cache has no
+        entry for this process (a new Process, p.CPUTotalTime = 0)."""
+        now = go_cpu_time(ticks)
+        prev = 0.0 if new else self.total.get(pid, 0.0)
+        self.total[pid] = now
+        return now - prev
+
+
 class PyRef:
     """Go-shaped state of a fleet of PowerMonitors (one per node)."""
 

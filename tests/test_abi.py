@@ -75,6 +75,28 @@ int main(void) {{
         assert getattr(accel.KaccInterval, f).offset == off, f
 
 
+def test_export_sums_layout_matches_header(tmp_path):
+    """kacc_export_sums (ABI 5): the ctypes twin's size and every field offset."""
+    c = tmp_path / "xs.c"
+    fields = [f for f, _ in accel.KaccExportSums._fields_]
+    body = "\n".join(f'printf("%zu\\n", offsetof(kacc_export_sums, {f}));' for f in fields)
+    c.write_text(f"""
+#include <stddef.h>
+#include <stdio.h>
+#include "kepler_accel.h"
+int main(void) {{
+  printf("%zu\\n", sizeof(kacc_export_sums));
+  {body}
+  return 0;
+}}""")
+    exe = tmp_path / "xs"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(accel.KaccExportSums)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(accel.KaccExportSums, f).offset == off, f
+
+
 def test_interval_bytes_formula(lib):
     # DESIGN.md §Roofline: node 76+96Z, proc 24+16Z (Δ 8 + slot 4 + prev 8Z in; totals 8Z + ratio 8 +
     # node 4 out: the power is derived, ABI 3), ctr 44+16Z, vm 28+16Z (ratio + node stored
