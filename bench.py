@@ -44,6 +44,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+# --totals auto: the partial sums ride in the next interval's launch up to this many nodes per GPU
+# (the launch's tail is then short of work and a second launch per step is a tenth of the step);
+# past it the export stores cost more than the launch they save
+FUSED_MAX_NODES = 2048
 METRIC = "process attributions/sec + achieved HBM GB/s, 10k-node fleet, 1/2/4/8 MI355X"
 
 
@@ -82,8 +86,11 @@ def parse():
                          "step of a W-GPU strong-scaling run, without the cross-GPU all-reduce)")
     ap.add_argument("--no-weak-line", dest="weak_line", action="store_false",
                     help="N > 1, strong scaling: skip the extra weak-scaling measurement (`weak_scaling`)")
-    ap.add_argument("--totals", choices=["fused", "tables", "exports", "tables+writes"], default="tables",
-                    help="cluster totals from the state tables, partial sums on the compute stream and the RCCL "
+    ap.add_argument("--totals", choices=["auto", "fused", "tables", "exports", "tables+writes"], default="auto",
+                    help="auto (default): fused when this GPU's shard has <= FUSED_MAX_NODES nodes (one interval per "
+                         "step), else tables — the measured crossover (profiles/r05/sums_ab: 1/8 shard fused 54.1 vs "
+                         "56.3 us per step, 1/4 shard equal, config 3 fused 391 vs 375 us).  "
+                         "tables: cluster totals from the state tables, partial sums on the compute stream and the RCCL "
                          "all-reduce on the comm stream (kacc_allreduce_namespaces, the default: measured fastest), "
                          "or from the interval's exports with everything on the comm stream (kacc_allreduce_exports: "
                          "the export stores cost 26 us and the concurrent partial sums slow the next interval more "
@@ -92,6 +99,9 @@ def parse():
                          "(pod_export_pos) and its launch also computes the previous interval's partial sums "
                          "(kacc_run_interval_sums: one launch per step; the region's last step's sums by "
                          "kacc_run_export_sums inside the timed region)")
+    ap.add_argument("--sums-order", choices=["ns", "rows"], default="ns",
+                    help="--totals fused: pod exports written in namespace order (pod_export_pos; the sums read "
+                         "contiguous records) or in batch order (the sums gather them through ns_pod_row)")
     ap.add_argument("--allreduce-every", type=int, default=8,
                     help="tables mode: the cluster totals of this many consecutive steps are all-reduced by ONE "
                          "kacc_allreduce_sums (each step's partial sums have their own rows; SURVEY 5: one "
@@ -753,7 +763,7 @@ class Workload:
             for st in range(n_steps):
                 t = self.iv_tensors[st * K + K - 1]
                 t["pod_export"], t["node_export"] = self.pex[st % 2], self.nex[st % 2]
-                if self.fused_sums:  # namespace-ordered exports: the partial sums stream contiguous records
+                if self.fused_sums and args.sums_order == "ns":  # the partial sums stream contiguous records
                     t["pod_export_pos"] = self.ns_t["pos"]
         # node-private slots (each node owns its slot range for the whole run): kacc_run_intervals
         # runs K > 1 fast-node intervals as one launch
@@ -842,8 +852,10 @@ def measure(args, w, rank, world, stream, comm_stream):
         for k in range(w.n_bufs):
             x = accel.KaccExportSums()
             x.n_ns = 0 if args.totals_probe == "nodes" else w.n_ns
-            x.n_pods, x.n_nodes, x.ns_ordered = w.sizes["n_pods"], w.sizes["n_nodes"], 1
+            x.n_pods, x.n_nodes = w.sizes["n_pods"], w.sizes["n_nodes"]
+            x.ns_ordered = 1 if args.sums_order == "ns" else 0
             x.ns_pod_off = w.ns_t["off"].data_ptr()
+            x.ns_pod_row = None if x.ns_ordered else w.ns_t["row"].data_ptr()
             x.pod_export, x.node_export = w.pex[k % 2].data_ptr(), None if no_nodes else w.nex[k % 2].data_ptr()
             x.out_energy, x.out_power = w.ns_e[k].data_ptr(), w.ns_p[k].data_ptr()
             x.out_node_energy = None if no_nodes else w.nd_e[k].data_ptr()
@@ -1042,6 +1054,13 @@ def main():
     total_nodes = bench_nodes(args.config, world, args.nodes, scaling)
     split = world * args.shard_of
     K = max(1, args.intervals)
+    totals_arg = args.totals
+
+    def pick_totals(nodes_per_gpu):  # the shard's node count (plan_node_ranges balances processes)
+        if totals_arg == "auto":
+            args.totals = "fused" if K == 1 and nodes_per_gpu <= FUSED_MAX_NODES else "tables"
+
+    pick_totals(-(-total_nodes // split))
     w = Workload(args, total_nodes, split, rank, rank, world, local, K, accel.Cluster.unique_id)
     stream = current_stream_handle()
     assert stream != 0
@@ -1204,6 +1223,7 @@ def main():
 
     if world > 1 and scaling == "strong" and args.weak_line and args.config in (1, 2, 3, 5):
         # extra key: every rank a full shard of its own (weak scaling), the same timed loop
+        pick_totals(bench_nodes(args.config, world, args.nodes, "weak") // world)
         wk = Workload(args, bench_nodes(args.config, world, args.nodes, "weak"), world, rank, rank, world, local, K,
                       accel.Cluster.unique_id)
         prime_t = to_device(wk.prime)
@@ -1214,6 +1234,7 @@ def main():
         wp = torch.tensor([wk.sizes["n_procs"]], dtype=torch.float64)
         dist.all_reduce(wp)
         result["weak_scaling"] = {"value": float(wp.item()) * K * args.steps / wwall, "unit": "proc-attr/s",
+                                  "totals": args.totals,
                                   "ms_per_step": wwall * 1e3 / args.steps, "kernel_ms": float(np.mean(wkms)),
                                   "nodes_per_gpu": wk.sizes["n_nodes"],
                                   "fleet_nodes": bench_nodes(args.config, world, args.nodes, "weak")}

@@ -952,14 +952,14 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
 }
 
 // Partial sums of an earlier interval's exports inside an interval launch
-// (kacc_run_interval_sums): after the n_nodes node workgroups come node_blocks
-// node-total columns and ns_blocks namespace-sum blocks of kTpb threads — the
+// (kacc_run_interval_sums): node_blocks node-total columns before the n_nodes node
+// workgroups and ns_blocks namespace-sum blocks of kTpb threads after them — the
 // same per-lane orders as cluster_partials_kernel (node_column_block sums with
 // its first kBlock lanes whatever the block size; a namespace is kNsLanes lanes
-// wherever its block starts), so the same bits.  Dispatched behind the node
-// workgroups, they run in the launch's tail, when the last residency round leaves
-// compute units free, and read only the earlier interval's exports (never a
-// table this launch writes): no wait, no second launch.
+// wherever its block starts), so the same bits.  The namespace blocks run in the
+// launch's tail, when the last residency round leaves compute units free; every sums
+// block reads only the earlier interval's exports (never a table this launch writes):
+// no wait, no second launch.
 struct SumsArgs {
   uint32_t node_blocks, ns_blocks, n_ns, ordered;
   const uint32_t *off, *rows;
@@ -1298,20 +1298,45 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
     st.node_cpu_delta[n] = a.nd;
     st.node_status[n] = a.first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
+  // A batch-order pod export (no pod_export_pos) leaves through LDS: the node's pods are
+  // export rows [q0, q1), so after the process pass (s_d free) each pod lane puts its
+  // record in s_d and the workgroup writes the node's records as one contiguous run of
+  // non-temporal 16-B stores — 1 KiB per wave instruction instead of 16-B pieces at a
+  // 16Z-B stride per lane (block-uniform; the late-aggregate order only)
+  constexpr uint32_t kStageWords = kRowsLds;  // s_d as u64 words
+  const bool stage = kLateAgg<V> && b.pod_export && !b.pod_export_pos && nq * 2u * Z <= kStageWords;
+  uint64_t *s_stage = reinterpret_cast<uint64_t *>(s_d);
   auto aggregate_out = [&]() {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
     if (!a_ok) {
-      if (role == 3) export_pod_zero<Z>(b, q0 + j, st.err);
+      if (role == 3) {
+        if (stage) {
+#pragma unroll
+          for (int z = 0; z < 2 * Z; ++z) s_stage[j * 2 * Z + z] = 0;
+        } else {
+          export_pod_zero<Z>(b, q0 + j, st.err);
+        }
+      }
       return;
     }
     if constexpr (kLateAgg<V>) load_row<Z>(a_energy(), agg_row(role, a_s), a_prev);
     // a pod's export row (namespace order) loads beside its previous totals: no extra round trip
-    const uint32_t xrow = role == 3 && b.pod_export ? export_row(b, q0 + j, st.err) : ~0u;
+    const uint32_t xrow = role == 3 && b.pod_export && !stage ? export_row(b, q0 + j, st.err) : ~0u;
     uint64_t E[Z];
     double P[Z];
     const double ratio = attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, a_delta,
                                           (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
     store_agg<Z, kNtAgg>(st, role, a_s, E, P, ratio, n);
-    if (role == 3) export_pod_at<Z>(b, xrow, E, P);
+    if (role == 3) {
+      if (stage) {
+#pragma unroll
+        for (int z = 0; z < Z; ++z) {
+          s_stage[j * 2 * Z + z] = E[z];
+          s_stage[j * 2 * Z + Z + z] = static_cast<uint64_t>(__double_as_longlong(P[z]));
+        }
+      } else {
+        export_pod_at<Z>(b, xrow, E, P);
+      }
+    }
   };
   if constexpr (!kLateAgg<V>) aggregate_out();
   if (swept) {  // process.go:118-148 in slot order: slot smin + pos0 + i holds row s_inv[pos0 + i]
@@ -1363,7 +1388,15 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
       store_proc<Z, kNtScat>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
     }
   }
+  if (stage) __syncthreads();  // every wave is past the process pass: s_d is free
   if constexpr (kLateAgg<V>) aggregate_out();
+  if (stage) {  // the node's pod records, rows [q0, q1) of the export: one contiguous run
+    __syncthreads();
+    using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
+    const u64x2 *src = reinterpret_cast<const u64x2 *>(s_stage);
+    u64x2 *dst = reinterpret_cast<u64x2 *>(b.pod_export + static_cast<uint64_t>(q0) * (2 * Z));
+    for (uint32_t i = utid; i < nq * Z; i += kThreads) nt_store(src[i], dst + i);
+  }
   if constexpr (kStamp) {
     __syncthreads();
     if (tid == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
@@ -1384,11 +1417,18 @@ void interval_kernel(const kacc_interval b, const DevState st) {
 template <int Z, int V>
 __global__ __launch_bounds__(kTpb<V>, Z > 4 ? 2 : KACC_FAST_WAVES)
 void interval_sums_kernel(const kacc_interval b, const DevState st, const SumsArgs sa) {
-  if (blockIdx.x >= b.n_nodes) {
-    sums_block<Z, kTpb<V>>(sa, blockIdx.x - b.n_nodes, st.err);
+  // the node-total columns FIRST (latency chains of 8-B loads: dispatched last they
+  // lengthened the launch's tail), then the nodes, then the namespace blocks in the tail
+  if (blockIdx.x < sa.node_blocks) {
+    sums_block<Z, kTpb<V>>(sa, blockIdx.x, st.err);
     return;
   }
-  interval_node<Z, V>(b, st, blockIdx.x);
+  const uint32_t x = blockIdx.x - sa.node_blocks;
+  if (x >= b.n_nodes) {
+    sums_block<Z, kTpb<V>>(sa, sa.node_blocks + (x - b.n_nodes), st.err);
+    return;
+  }
+  interval_node<Z, V>(b, st, x);
 }
 
 // ============ K intervals in one launch, state carried on chip ====================

@@ -22,3 +22,7 @@ tools/gpu_steps.sh "${args[@]}" || exit $?
 for f in gpurun_out/$O/*_r*.json; do
   python -c "import json;d=json.load(open('$f'));r=d['roofline'];t=d['totals_compute_ms'];print('$f', 'value %.2fG step %.2f us kern %.2f us tot %s frac %.3f' % (d['value']/1e9, d['ms_per_step']*1e3, d['kernel_ms']*1e3, ('%.2f us' % (t*1e3)) if t else '-', r['frac']))"
 done
+# the end-to-end lines: float64 batches (host_path) and the CPU-tick format (host_path_ticks)
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --frag-line 0 --no-pipeline-line --totals fused \
+  --json-out gpurun_out/$O/c3_host.json > gpurun_out/$O/c3_host.log 2>&1 || { echo "host lines rc=$?"; tail -20 gpurun_out/$O/c3_host.log; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/$O/c3_host.json'));print({k: {x: d[k].get(x) for x in ('proc_attr_per_s','ms_per_interval','h2d_bytes_per_interval','frac_of_pcie_copy','error')} for k in ('host_path','host_path_ticks')})"
