@@ -530,6 +530,36 @@ def host_path_line(args, steps=10):
                     "pcie_copy: torch pinned -> device copy of the same bytes (the ceiling)"}
 
 
+def scrape_line(acc, n_procs, Z, reps=10):
+    """What a per-interval scrape of every process's Usage.Power costs on the device: the
+    P x Z derived powers (kacc_table_read of KACC_T_PROC_POWER: the slot's ratio x its node's
+    ActivePower behind the process.go:124 guard) written to a dense device array, after the
+    timed region, on the snapshot it left.  Bytes: ratio 8 + node 4 per slot in, 8 per power
+    out (the node tables, N x Z, stay in cache)."""
+    import torch
+
+    from kepler_amd.torch_batch import current_stream_handle
+
+    n = n_procs * Z
+    out = torch.empty(max(n, 1), dtype=torch.float64, device="cuda")
+    s = current_stream_handle()
+    acc.read("proc_power", out.data_ptr(), 0, n, s)  # warm-up
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        acc.read("proc_power", out.data_ptr(), 0, n, s)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = n_procs * 12 + n * 8
+    gbps = nbytes / ms / 1e6
+    return {"powers": n, "processes": n_procs, "zones": Z, "ms": ms, "bytes": nbytes, "GBps": gbps,
+            "frac_of_spec": gbps / 8000.0, "reps": reps,
+            "note": "kacc_table_read(KACC_T_PROC_POWER) into a dense device array after the timed region "
+                    "(HIP events around reps back-to-back reads); not part of value"}
+
+
 def _pack(arrays):
     """One contiguous byte image of named arrays (16-B aligned segments): {name: (offset, dtype, n)}."""
     off, layout = 0, {}
@@ -1218,6 +1248,11 @@ def main():
                                          "affinity mask, shared with the other GPUs' jobs"},
         }
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / gf["value"]
+    if world == 1:
+        try:
+            result["scrape_powers"] = scrape_line(w.acc, w.sizes["n_procs"], Z)
+        except Exception as e:  # a secondary line: report, never lose the headline
+            result["scrape_powers"] = {"error": repr(e)}
     w.close()
     del w
 

@@ -378,6 +378,13 @@ int kacc_table_row_stride(const kacc_ctx *ctx, kacc_table t, uint64_t *stride);
 /* Synchronous copies of `count` elements starting at element `first`. */
 int kacc_table_download(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *host_dst);
 int kacc_table_upload(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const void *host_src);
+/* Asynchronous device-side read of the same logical range into dev_dst
+ * (device, count elements, dense): the scrape of a snapshot without the PCIe
+ * hop — a derived table (KACC_T_PROC_POWER, ...) is derived into it
+ * (ratio x its node's ActivePower, the guard of process.go:124-142), a pod
+ * table is gathered out of its records, any other table is copied.  Ordered
+ * on `stream` (NULL: the context's) after the intervals launched before it. */
+int kacc_table_read(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, void *dev_dst, void *stream);
 
 /* ---- cluster namespace totals (north star: only these cross GPUs) -------- */
 /* Per-namespace sums over pods of this context: ns k owns pod slots

@@ -142,6 +142,7 @@ EXPORTS = [
     "kacc_table_row_stride",
     "kacc_table_download",
     "kacc_table_upload",
+    "kacc_table_read",
     "kacc_namespace_totals",
     "kacc_create_multi",
     "kacc_cluster_unique_id",
@@ -366,6 +367,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.kacc_table_row_stride.argtypes = [c_void_p, c_int, POINTER(c_uint64)]
     lib.kacc_table_download.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
     lib.kacc_table_upload.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p]
+    if hasattr(lib, "kacc_table_read"):  # KACC_LIB A/B builds of earlier sources lack it
+        lib.kacc_table_read.argtypes = [c_void_p, c_int, c_uint64, c_uint64, c_void_p, c_void_p]
     lib.kacc_namespace_totals.argtypes = [
         c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
     ]
@@ -629,6 +632,14 @@ class Accel:
     def upload(self, name: str, values: np.ndarray, first: int = 0) -> None:
         v = np.ascontiguousarray(values, dtype=TABLES[TABLE_INDEX[name]][1])
         self._check(self.lib.kacc_table_upload(self.ctx, TABLE_INDEX[name], first, v.size, v.ctypes.data))
+
+    def read(self, name: str, dev_dst: int, first: int = 0, count: Optional[int] = None, stream=None) -> None:
+        """kacc_table_read: the logical range into device memory at dev_dst, on `stream` (derived
+        tables derived, pod tables gathered out of their records)."""
+        _, total = self.table_info(name)
+        if count is None:
+            count = total - first
+        self._check(self.lib.kacc_table_read(self.ctx, TABLE_INDEX[name], first, count, dev_dst, stream))
 
     def row_stride(self, name: str) -> int:
         """kacc_table_row_stride: elements between two slots' rows (2Z for the pod tables' records)."""
