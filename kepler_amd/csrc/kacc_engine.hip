@@ -124,17 +124,13 @@ constexpr bool kNtAggStores = KACC_NT_AGG != 0;
 #endif
 constexpr bool kNtScatterStores = KACC_NT_SCATTER != 0;
 constexpr uint32_t kPodGrid = 256;     // deferred-pod kernel workgroups (kBlock threads)
+constexpr int kTotLoads = 16;          // Δ loads in flight per lane (big-node CPU total)
 // KACC_CHUNK_THREADS: chunk kernel workgroup (4 rows per lane: 512 -> 2048-row
 // chunks); KACC_CHUNK_WAVES: waves per SIMD it is compiled for at Z <= 4
 // (512 threads: 4 = two workgroups per CU, 119 VGPRs; 6 = three, 80 VGPRs with
 // spills; 256 threads: a workgroup is one wave per SIMD)
 #ifndef KACC_CHUNK_THREADS
 #define KACC_CHUNK_THREADS 512
-#endif
-// KACC_CHUNK_EARLY_PREV: chunk_kernel issues the rows' previous totals with their Δ / slot
-// loads (one round trip) instead of after the chunk's LDS staging and tree
-#ifndef KACC_CHUNK_EARLY_PREV
-#define KACC_CHUNK_EARLY_PREV 1
 #endif
 #ifndef KACC_CHUNK_WAVES
 #define KACC_CHUNK_WAVES 4
@@ -165,22 +161,8 @@ static_assert(kRowsLds == KACC_FAST_MAX_PROCS && kTpb<0> == KACC_FAST_MAX_AGGREG
 // the first container / VM / pod the chunk owns; it owns them up to the next
 // chunk's begin (or the node's end for the last chunk).
 struct ChunkItem {
-  uint32_t node, chunk, nchunks, ctr_begin, vm_begin, pod_begin, flags, pad;
+  uint32_t node, chunk, nchunks, ctr_begin, vm_begin, pod_begin, pad[2];
 };
-// ChunkItem.flags: the node's phase B (its CPU-time total) runs inside chunk_kernel: every
-// chunk sums its own rows (the fast path's 256-lane tree) and the node's chunks exchange
-// those sums through memory — Δ is read once per interval, not twice
-constexpr uint32_t kItemFused = 1u;
-// a node of at most this many chunks takes the fused path: the hand-off waits for the
-// node's other chunks, which the dynamic dequeue hands to running workgroups in order,
-// so it completes whenever the resident workgroups outnumber one node's chunks
-#ifndef KACC_FUSED_MAX_CHUNKS
-#define KACC_FUSED_MAX_CHUNKS 0
-#endif
-constexpr uint32_t kFusedMaxChunks = KACC_FUSED_MAX_CHUNKS;
-// polls of a node's arrival count before a chunk sums the node's rows itself (each poll
-// an sc1 load round trip + a short sleep: a few ms in all)
-constexpr uint32_t kPollLimit = 4096;
 
 // Cluster node totals (kacc_allreduce_namespaces, kacc_cluster_partials): one
 // block per output value — block c sums column c (node table c / Z of the five,
@@ -240,15 +222,6 @@ struct DevState {
   uint32_t items_given, keep_items;
   uint64_t *stamps;  // kVarStamps only
 };
-// Fused big nodes (kItemFused): per chunk item its tree of Δ (the [item_cap] doubles after
-// the items, one allocation) and per node the arrival count of its chunks (the [nodes]
-// words after item_ctr's four, zeroed again by pod_kernel).  Derived, not DevState
-// members: a larger DevState kernarg is copied to scratch by interval_kernel (its
-// role-selected table pointers defeat the promotion past 328 bytes)
-__device__ __forceinline__ uint64_t *part_of(const DevState &st) {
-  return reinterpret_cast<uint64_t *>(st.items + st.item_cap);
-}
-__device__ __forceinline__ uint32_t *nsync_of(const DevState &st) { return st.item_ctr + 4; }
 
 struct NodeShared {
   uint64_t active_energy[KACC_MAX_ZONES];
@@ -820,7 +793,7 @@ __device__ __forceinline__ NodeRanges clamp_ranges(const kacc_interval &b, const
 }
 
 template <int Z, int V>
-__device__ __forceinline__ void big_node_prepare(const kacc_interval &b, const DevState &st, uint32_t n,
+__device__ void big_node_prepare(const kacc_interval &b, const DevState &st, uint32_t n,
                                  const NodeRanges &rg, double *red, NodeShared &sh,
                                  uint32_t &s_base);
 
@@ -2596,49 +2569,14 @@ __device__ __forceinline__ void gen_items(const kacc_interval &b, const DevState
     items[k].node = n;
     items[k].chunk = k;
     items[k].nchunks = nch;
-    items[k].flags = nch <= kFusedMaxChunks ? kItemFused : 0u;
     if (static_cast<int>(k) > kl_ctr) items[k].ctr_begin = c1;
     if (static_cast<int>(k) > kl_vm) items[k].vm_begin = v1;
     if (static_cast<int>(k) > kl_pod) items[k].pod_begin = q1;
   }
 }
 
-// The canonical total of a node of `rows` rows at d (device memory): each kChunkRows-row
-// chunk's 256-lane tree — the fast path's code — added in chunk order.  Called by every
-// thread of a workgroup of >= kTree threads (block-uniform loop: all meet the barriers);
-// red: kTree doubles of LDS.  Lane 0 returns the total.
-__device__ __forceinline__ double chunked_total(const double *d, uint32_t rows, double *red) {
-  const uint32_t tid = threadIdx.x;
-  const uint32_t nch = rows ? (rows + kChunkRows - 1) / kChunkRows : 1u;
-  double t = 0.0;  // lane 0
-  for (uint32_t c = 0; c < nch; ++c) {
-    const uint32_t c0 = c * kChunkRows, cr = rows ? min(rows - c0, static_cast<uint32_t>(kChunkRows)) : 0u;
-    if (tid < static_cast<uint32_t>(kTree)) {
-      const double *__restrict__ dc = d + c0;
-      double x = 0.0;
-#pragma unroll
-      for (int u = 0; u < kRowsLds / kTree; ++u) {
-        const double v = cr ? dc[min(tid + kTree * u, cr - 1)] : 0.0;
-        x = x + (tid + kTree * u < cr ? v : 0.0);
-      }
-      red[tid] = x;
-    }
-    __syncthreads();
-    if (tid < 128) red[tid] = red[tid] + red[tid + 128];
-    __syncthreads();
-    if (tid < 64) {
-      double x = red[tid] + red[tid + 64];
-#pragma unroll
-      for (int k = 32; k >= 1; k >>= 1) x = x + __shfl_down(x, k, 64);
-      t = c == 0 ? x : t + x;
-    }
-    __syncthreads();  // red is rewritten by the next chunk
-  }
-  return t;
-}
-
 template <int Z, int V>
-__device__ __forceinline__ void big_node_prepare(const kacc_interval &b, const DevState &st, const uint32_t n,
+__device__ void big_node_prepare(const kacc_interval &b, const DevState &st, const uint32_t n,
                                  const NodeRanges &rg, double *red, NodeShared &sh,
                                  uint32_t &s_base) {
   constexpr int kThreads = kTpb<V>;
@@ -2646,11 +2584,6 @@ __device__ __forceinline__ void big_node_prepare(const kacc_interval &b, const D
   const int tid = threadIdx.x;
   const uint32_t p0 = rg.p0, p1 = rg.p1, rows = p1 - p0;
   const uint32_t nch = rows ? (rows + kChunkRows - 1) / kChunkRows : 1u;
-  // phase A here for every big node (chunk_kernel reads its results from the tables);
-  // phase B — the node total — in chunk_kernel when the items are kItemFused and the
-  // total is not given: each chunk sums its own rows (Δ read once per interval)
-  const bool given = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) != 0;
-  const bool fused = nch <= kFusedMaxChunks && !given;
   if (tid == 0 && !st.items_given)
     s_base = (V & kVarBigNoAtomic) ? n + p0 / kChunkRows : atomicAdd(st.item_ctr, nch);
   if (tid < Z) node_zone<Z>(b, st, n, tid, sh);
@@ -2658,25 +2591,59 @@ __device__ __forceinline__ void big_node_prepare(const kacc_interval &b, const D
   const uint32_t base = st.items_given ? 0u : s_base;
   const bool fits = st.items_given || (base + nch <= st.item_cap && base + nch >= base);  // host sizes the list
   if (!fits && tid == 0) raise_err(st.err, kErrCapacity);
-  if (tid >= kTree && fits && !st.items_given)
-    gen_items<V, kGen>(b, st, n, rg, base, nch, static_cast<uint32_t>(tid) - kTree);
-  // phase B here: the total given, or a node of more than kFusedMaxChunks chunks (huge:
-  // > 262k processes); fused, chunk 0 of the node writes node_cpu_delta
-  if (!fused) {
-    if (given || (V & kVarBigNoTotal) != 0) {
-      if (tid == 0) sh.node_delta = given ? b.node_cpu_delta[n] : 0.0;
-    } else {
-      const double t = chunked_total(b.proc_cpu_delta + p0, rows, red);
-      if (tid == 0) sh.node_delta = t;
+  const bool given = (b.flags & KACC_F_NODE_CPU_DELTA_GIVEN) != 0;
+  if (tid < kTree) {
+    // ---- B: ProcessTotalCPUTimeDelta; lane l sums rows l, l+256, ... ---------
+    // software-pipelined: the next kTotLoads rows are in flight while the
+    // current ones are added (latency, not bandwidth, bounds one node's sum)
+    if (!given && (V & kVarBigNoTotal) == 0) {
+      const double *__restrict__ dcpu = b.proc_cpu_delta + p0;
+      double s = 0.0;
+      double v[kTotLoads];
+#pragma unroll
+      for (int k = 0; k < kTotLoads; ++k) {
+        const uint32_t i = tid + k * kTree;
+        v[k] = i < rows ? dcpu[i] : 0.0;
+      }
+      for (uint32_t r0 = 0; r0 < rows; r0 += kTree * kTotLoads) {
+        double nx[kTotLoads];
+#pragma unroll
+        for (int k = 0; k < kTotLoads; ++k) {
+          const uint32_t i = r0 + kTree * kTotLoads + tid + k * kTree;
+          nx[k] = i < rows ? dcpu[i] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < kTotLoads; ++k)
+          if (r0 + tid + k * kTree < rows) s = s + v[k];
+#pragma unroll
+        for (int k = 0; k < kTotLoads; ++k) v[k] = nx[k];
+      }
+      red[tid] = s;
     }
-    __syncthreads();
+  } else if (fits && !st.items_given) {
+    // ---- chunk items, concurrently with the sum (the other kGen lanes) --------
+    gen_items<V, kGen>(b, st, n, rg, base, nch, static_cast<uint32_t>(tid) - kTree);
   }
+  __syncthreads();
+  if (given) {
+    if (tid == 0) sh.node_delta = b.node_cpu_delta[n];
+  } else {
+    if (tid < 128) red[tid] = red[tid] + red[tid + 128];
+    __syncthreads();
+    if (tid < 64) {
+      double x = red[tid] + red[tid + 64];
+#pragma unroll
+      for (int k = 32; k >= 1; k >>= 1) x = x + __shfl_down(x, k, 64);
+      if (tid == 0) sh.node_delta = x;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {  // node scalars of the new snapshot (as the fast path)
     const bool first = sh.first != 0;
     st.node_ts[n] = b.node_ts_ns[n];
     st.node_has_prev[n] = 1u;
     st.node_usage_ratio[n] = first ? 0.0 : b.node_usage_ratio[n];
-    if (!fused) st.node_cpu_delta[n] = sh.node_delta;
+    st.node_cpu_delta[n] = sh.node_delta;
     st.node_status[n] = first ? KACC_NODE_FIRST_READ : KACC_NODE_OK;
   }
 }
@@ -2743,23 +2710,17 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
   __shared__ double s_ct[kThreads];  // and running CPU totals
   __shared__ NodeShared sh;
   __shared__ uint32_t s_next[2];
-  __shared__ double s_red[kTree];  // fused big nodes: this chunk's tree
-  __shared__ uint32_t s_ok;        // and whether all the node's chunks arrived in time
   const int tid = threadIdx.x;
   const uint32_t utid = static_cast<uint32_t>(tid);
   const uint32_t count =
       min(__hip_atomic_load(st.item_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), st.item_cap);
-  // every item dequeued (none static): an item is only ever held by a RUNNING workgroup,
-  // so the fused hand-off below waits only for items running or still to be dequeued
-  if (tid == 0) s_next[1] = atomicAdd(st.item_ctr + 1, 1u);
-  __syncthreads();
-  uint32_t idx = uniform_u32(s_next[1]);
+  uint32_t idx = blockIdx.x;  // first item static, the rest dequeued
   for (uint32_t parity = 0; idx < count; parity ^= 1u) {
-    if (tid == 0) s_next[parity] = atomicAdd(st.item_ctr + 1, 1u);
+    if (tid == 0) s_next[parity] = atomicAdd(st.item_ctr + 1, 1u) + gridDim.x;
     // the item's words and its successor's begins as ONE batch of vector loads
     // (waited for once), then the node's ranges as another: as scalar loads
     // behind the `last` selects they took nine dependent round trips per chunk
-    uint32_t f[10];
+    uint32_t f[9];
     {
       uint32_t ii = idx;
       asm volatile("" : "+v"(ii));
@@ -2774,17 +2735,12 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       f[6] = w1[3];
       f[7] = w1[4];
       f[8] = w1[5];
-      f[9] = w0[6];
       asm volatile("" ::"v"(f[0]), "v"(f[1]), "v"(f[2]), "v"(f[3]), "v"(f[4]), "v"(f[5]), "v"(f[6]), "v"(f[7]),
-                   "v"(f[8]), "v"(f[9]));
+                   "v"(f[8]));
 #pragma unroll
-      for (int q = 0; q < 10; ++q) f[q] = uniform_u32(f[q]);
+      for (int q = 0; q < 9; ++q) f[q] = uniform_u32(f[q]);
     }
     const uint32_t n = f[0], k = f[1], nch = f[2];
-    // kItemFused: this node's phase B here — every chunk its tree, exchanged (phase A ran in
-    // interval_kernel; a given total needs no exchange)
-    const bool fused = (f[9] & kItemFused) != 0 && nch <= kFusedMaxChunks && k < nch &&
-                       !(b.flags & KACC_F_NODE_CPU_DELTA_GIVEN);
     if (n >= b.n_nodes) {  // corrupt item: cannot happen unless the list overflowed
       if (tid == 0) raise_err(st.err, kErrCapacity);
       __syncthreads();
@@ -2828,15 +2784,10 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     }
     uint64_t prev[kR][Z];
     uint32_t contig = 0;
-    // the rows' previous totals: issued right after the chunk's tree is published (not
-    // live across the tree and its barriers; their latency hides under phase C and the
-    // wait for the node total)
-    auto load_prev = [&](bool from_lds) {
-      if constexpr ((V & kVarSkipProcs) == 0) {
+    if constexpr ((V & kVarSkipProcs) == 0) {
 #pragma unroll
-        for (int u = 0; u < kR; ++u) {
-          const uint32_t wu = from_lds ? (utid + u * kThreads < rows ? s_w[utid + u * kThreads] : 0xffffffffu) : w[u];
-          const uint64_t sl = wu & KACC_SLOT_MASK;
+      for (int u = 0; u < kR; ++u) {
+        const uint64_t sl = w[u] & KACC_SLOT_MASK;
         if constexpr (kT) {
           const uint64_t s0 = uniform_u32(static_cast<uint32_t>(sl));
           const bool mine = (utid + u * kThreads) < rows && sl == s0 + (tid & 63) &&
@@ -2854,9 +2805,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
           for (int z = 0; z < Z; ++z) prev[u][z] = 0;
         }
       }
-      }
-    };
-    if (KACC_CHUNK_EARLY_PREV) load_prev(false);
+    }
     // aggregate j of this chunk: containers [cb, ce), VMs [vb, ve), pods [qb, qe)
     const uint32_t ctr_rows_end = rg.c1 > rg.c0 ? b.ctr_proc_end[rg.c1 - 1] : rg.p0;
     auto agg = [&](uint32_t j, uint32_t &beg, uint32_t &end, uint32_t &wd) -> uint32_t {
@@ -2890,13 +2839,18 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
     if (utid < nagg) a_role = agg(utid, a_beg, a_end, a_w);
     const uint32_t a_s = a_w & KACC_SLOT_MASK;
     const bool a_ok = a_role != 0 && a_s < cap_of(a_role);
-    // the aggregate's previous energies load after the node total (not live across the
-    // tree, phase C and the wait; their latency hides under the process rows' pass)
+    uint64_t a_prev[Z];
     double a_total = 0.0;
-    if (a_ok && a_role != 2 && !(a_w & KACC_SLOT_NEW))
-      a_total = (a_role == 1 ? st.ctr_cpu_total : st.pod_cpu_total)[a_s];
+    if (a_ok) {
+      load_row<Z>(energy_of(a_role), agg_row(a_role, a_s), a_prev);
+      if (a_role != 2 && !(a_w & KACC_SLOT_NEW))
+        a_total = (a_role == 1 ? st.ctr_cpu_total : st.pod_cpu_total)[a_s];
+    } else {
+#pragma unroll
+      for (int z = 0; z < Z; ++z) a_prev[z] = 0;
+    }
     if (a_role != 0 && !a_ok) raise_err(st.err, kErrSlot);
-    node_params_to_lds<Z>(st, n, tid, sh);  // phase A ran in interval_kernel
+    node_params_to_lds<Z>(st, n, tid, sh);
 #pragma unroll
     for (int u = 0; u < kR; ++u) {
       const uint32_t r = utid + u * kThreads;
@@ -2906,37 +2860,16 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
       }
     }
     __syncthreads();
-    // ---- fused node phase B: this chunk's tree, published: an sc1 (write-through) store
-    // of ONE lane, its vmcnt drained, then one agent-scope add to the node's arrival count
-    // (the measured valid hand-off: MI355X_MICROARCH.md, inter-workgroup visibility, first
-    // row of the sc1 table)
-    if (fused) {  // the fast path's tree over this chunk's staged rows (block-uniform)
-      if (tid < kTree) {
-        double x = 0.0;  // +0.0 past the chunk's end: an identity
-#pragma unroll
-        for (int u = 0; u < kChunkRows / kTree; ++u) {
-          const uint32_t r = utid + kTree * u;
-          const double v = s_d[min(r, rows > 0 ? rows - 1 : 0u)];
-          x = x + (r < rows ? v : 0.0);
-        }
-        s_red[tid] = x;
-      }
-      __syncthreads();
-      if (tid < 128) s_red[tid] = s_red[tid] + s_red[tid + 128];
-      __syncthreads();
-    }
-    if (fused && tid < 64) {
-      double tc = s_red[tid] + s_red[tid + 64];
-#pragma unroll
-      for (int kk = 32; kk >= 1; kk >>= 1) tc = tc + __shfl_down(tc, kk, 64);
-      if (tid == 0)
-        __hip_atomic_store(part_of(st) + idx, static_cast<uint64_t>(__double_as_longlong(tc)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (tid == 0) __hip_atomic_fetch_add(nsync_of(st) + n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!KACC_CHUNK_EARLY_PREV) load_prev(true);  // every item (one copy of the code: register pressure)
+    const Attr<Z> a = make_attr<Z>(sh, b.flags);
 
+    auto agg_out = [&](uint32_t role, uint32_t wd, double delta, const uint64_t (&pv)[Z]) {
+      const uint64_t s = wd & KACC_SLOT_MASK;
+      uint64_t E[Z];
+      double P[Z];
+      const double ratio =
+          attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, delta, (wd & KACC_SLOT_NEW) != 0, pv, E, P);
+      store_agg<Z, kNT>(st, role, s, E, P, ratio, n);
+    };
     // ---- C: owned containers / VMs (informer.go:223-273) ------------------------
     auto segment = [&](uint32_t role, uint32_t beg, uint32_t end, uint32_t wd, bool ok,
                        double &total) -> double {
@@ -2977,54 +2910,7 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         s_ct[utid] = a_ok ? a_total : 0.0;
       }
     }
-    // ---- fused: the node total = the chunks' trees added in chunk order.  Lane 0 polls
-    // the node's arrival count (sc1 loads), a bounded number of times: a workgroup never
-    // waits for long (a chunk may not run soon when other kernels or processes hold the
-    // compute units), it then sums the node's rows itself — the same trees, the same bits
-    if (fused && tid == 0) {
-      uint32_t ok = 0;
-      for (uint32_t it = 0; it < kPollLimit; ++it) {
-        if (__hip_atomic_load(nsync_of(st) + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= nch) {
-          ok = 1u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      s_ok = ok;
-    }
     __syncthreads();
-    if (fused) {  // block-uniform
-      double t = 0.0;  // lane 0
-      if (s_ok) {
-        if (tid < 64) {  // the node's trees: items [idx - k, idx - k + nch) (a node's items are consecutive)
-          const uint64_t *pt = part_of(st) + (idx - k);
-          const uint64_t x0 = tid < nch ? __hip_atomic_load(pt + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-          const uint64_t x1 =
-              tid + 64 < nch ? __hip_atomic_load(pt + tid + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-          for (uint32_t c = 0; c < nch; ++c) {  // chunk order, shuffled in from their lanes
-            const uint64_t v = c < 64 ? __shfl(x0, static_cast<int>(c), 64) : __shfl(x1, static_cast<int>(c - 64), 64);
-            const double tc = __longlong_as_double(static_cast<long long>(v));
-            t = c == 0 ? tc : t + tc;
-          }
-        }
-      } else {  // the same trees from the node's rows in memory (s_red is free again)
-        t = chunked_total(b.proc_cpu_delta + rg.p0, rg.p1 - rg.p0, s_red);
-      }
-      if (tid == 0) {
-        sh.node_delta = t;
-        if (k == 0) st.node_cpu_delta[n] = t;  // the node scalar interval_kernel left to the chunks
-      }
-      __syncthreads();
-    }
-    const Attr<Z> a = make_attr<Z>(sh, b.flags);
-    auto agg_out = [&](uint32_t role, uint32_t wd, double delta, const uint64_t (&pv)[Z]) {
-      const uint64_t s = wd & KACC_SLOT_MASK;
-      uint64_t E[Z];
-      double P[Z];
-      const double ratio =
-          attribute_row<Z>(a, role == 3 ? a.live_pod : a.live, delta, (wd & KACC_SLOT_NEW) != 0, pv, E, P);
-      store_agg<Z, kNT>(st, role, s, E, P, ratio, n);
-    };
     // ---- D: owned pods whose containers are all in s_cd / s_ct ---------------
     bool defer = false;
     if (a_role == 3) {
@@ -3047,13 +2933,17 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         defer = true;  // pod_kernel, after every chunk's containers are stored
       }
     }
-    // ---- E: process rows (process.go:118-148), then the aggregates ------------------
-    uint64_t a_prev[Z];
+    // ---- E: aggregates, then process rows (process.go:118-148) ------------------
     if (a_ok && !defer) {
-      load_row<Z>(energy_of(a_role), agg_row(a_role, a_s), a_prev);
-    } else {
-#pragma unroll
-      for (int z = 0; z < Z; ++z) a_prev[z] = 0;
+      const uint64_t s = a_w & KACC_SLOT_MASK;
+      uint64_t E[Z];
+      double P[Z];
+      const double ratio =
+          attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
+      store_agg<Z, kNT>(st, a_role, s, E, P, ratio, n);
+      if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P, st.err);
+    } else if (a_role == 3 && !a_ok) {
+      export_pod_zero<Z>(b, qb + (utid - ncv), st.err);
     }
     if (defer && a_ok) {
       const uint32_t i = atomicAdd(st.defer_ctr, 1u);
@@ -3086,16 +2976,6 @@ __global__ __launch_bounds__(kChunkThreads, (Z > 4 ? 2 : KACC_CHUNK_WAVES)) void
         const double ratio = attribute_proc<Z>(a, s_d[r], (wk & KACC_SLOT_NEW) != 0, prev[u], E);
         store_proc<Z, kNT && kNtScatterStores>(st, sl, E, ratio, n, !a.keep_node || (wk & KACC_SLOT_NEW));
       }
-    }
-    if (a_ok && !defer) {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
-      uint64_t E[Z];
-      double P[Z];
-      const double ratio =
-          attribute_row<Z>(a, a_role == 3 ? a.live_pod : a.live, a_delta, (a_w & KACC_SLOT_NEW) != 0, a_prev, E, P);
-      store_agg<Z, kNT>(st, a_role, a_s, E, P, ratio, n);
-      if (a_role == 3) export_pod<Z>(b, qb + (utid - ncv), E, P, st.err);
-    } else if (a_role == 3 && !a_ok) {
-      export_pod_zero<Z>(b, qb + (utid - ncv), st.err);
     }
     // aggregates beyond one per lane (chunks of mostly empty containers):
     // containers / VMs here, their pods always deferred
@@ -3141,8 +3021,6 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
     if (!st.keep_items) st.item_ctr[0] = 0u;  // the list stays for the next interval of one layout
     st.item_ctr[1] = 0u;
   }
-  // the fused big nodes' arrival counts, for the next interval (chunk_kernel has ended)
-  for (uint32_t i = blockIdx.x * kBlock + tid; i < b.n_nodes; i += gridDim.x * kBlock) nsync_of(st)[i] = 0u;
   const uint32_t count = min(st.defer_ctr[0], st.defer_cap);
   for (uint32_t i = blockIdx.x * kBlock + tid; i < count; i += gridDim.x * kBlock) {
     const uint2 e = st.defer[i];
@@ -3223,12 +3101,26 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
 
 // Elements [first, first + count) of the derived process power table
 // ([slot*Z + z], kacc_derive.hpp), grid-stride.
+// Derived powers of elements [first, first + count) ([slot*Z + z]) into out: one lane per
+// ELEMENT (a wave stores 512 contiguous bytes), slot = e / Z by a compile-time Z (a
+// multiply, not a 64-bit division); the Z lanes of a slot read its ratio and node from the
+// same line, the node's guards come from cache.  Per slot: ratio 8 + node 4 in, 8Z out
+// (bench.py scrape_powers).
+template <int Z>
 __global__ __launch_bounds__(kBlock) void proc_power_kernel(const ProcDerive d, uint64_t first, uint64_t count,
                                                             double *out) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < count;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    const uint64_t e = first + i;
-    out[i] = proc_power(d, e / d.zones, static_cast<uint32_t>(e % d.zones));
+    const uint64_t e = first + i, s = e / Z;
+    const uint32_t z = static_cast<uint32_t>(e - s * Z);
+    const uint32_t n = d.node[s];
+    double p = 0.0;
+    if (n < d.nodes) {
+      const uint64_t k = static_cast<uint64_t>(n) * Z + z;
+      const double aP = d.active_power[k];
+      if (d.active_energy[k] != 0 && d.cpu_delta[n] != 0 && aP != 0) p = d.ratio[s] * aP;  // process.go:124, 142
+    }
+    __builtin_nontemporal_store(p, out + i);
   }
 }
 
@@ -3325,9 +3217,6 @@ uint64_t table_count(const kacc_config &c, int t) {
   }
   return d.zoned ? base * c.zones : base;
 }
-
-// d_ctr: four work words, then the fused big nodes' arrival counts (nsync_of)
-uint64_t ctr_bytes(uint64_t nodes) { return 16 + 4 * std::max<uint64_t>(nodes, 1); }
 
 kacc::DevState dev_state(const kacc_ctx *ctx) {
   kacc::DevState s;
@@ -3578,8 +3467,7 @@ int ensure_items(kacc_ctx *ctx, uint64_t nodes, uint64_t procs, uint64_t pods) {
     if (ctx->d_items) KACC_HIP(ctx, hipFree(ctx->d_items));
     ctx->d_items = nullptr;
     ctx->item_cap = 0;
-    // the items, then each item's fused tree (part_of)
-    KACC_HIP(ctx, hipMalloc(&ctx->d_items, need * (sizeof(kacc::ChunkItem) + sizeof(double))));
+    KACC_HIP(ctx, hipMalloc(&ctx->d_items, need * sizeof(kacc::ChunkItem)));
     ctx->item_cap = static_cast<uint32_t>(need);
   }
   if (need_defer > ctx->defer_cap) {
@@ -3849,7 +3737,7 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
   }
   ctx->tables[KACC_T_POD_POWER] = static_cast<char *>(ctx->tables[KACC_T_POD_ENERGY]) + 8ull * ctx->cfg.zones;
   if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_ctr, ctr_bytes(cfg->nodes))) != hipSuccess) {
+      (e = hipMalloc(&ctx->d_ctr, 16)) != hipSuccess) {
     fail(ctx, KACC_ENOMEM, "hipMalloc work words: %s", hipGetErrorString(e));
     return bail(KACC_ENOMEM);
   }
@@ -3896,7 +3784,7 @@ int kacc_reset(kacc_ctx *ctx) {
     if (!kTables[t].derived && t != KACC_T_POD_POWER)
       KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0, table_alloc_bytes(ctx, t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
-  KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, ctr_bytes(ctx->cfg.nodes), ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->live_nodes = 0;
   return KACC_OK;
@@ -4520,10 +4408,20 @@ int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t c
   if (!out) return fail(ctx, KACC_EINVAL, "NULL argument");
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  const uint64_t blocks = (count + kacc::kBlock - 1) / kacc::kBlock;
+  const uint32_t Z = ctx->cfg.zones;
+  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + kacc::kBlock - 1) / kacc::kBlock, 65536)));
+  const kacc::ProcDerive d = kacc_derive(ctx, static_cast<kacc_kind>(kind));
   (void)hipGetLastError();
-  hipLaunchKernelGGL(kacc::proc_power_kernel, dim3(static_cast<uint32_t>(std::min<uint64_t>(blocks, 65536))),
-                     dim3(kacc::kBlock), 0, st, kacc_derive(ctx, static_cast<kacc_kind>(kind)), first, count, out);
+  switch (Z) {
+    case 1: hipLaunchKernelGGL(kacc::proc_power_kernel<1>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 2: hipLaunchKernelGGL(kacc::proc_power_kernel<2>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 3: hipLaunchKernelGGL(kacc::proc_power_kernel<3>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 4: hipLaunchKernelGGL(kacc::proc_power_kernel<4>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 5: hipLaunchKernelGGL(kacc::proc_power_kernel<5>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 6: hipLaunchKernelGGL(kacc::proc_power_kernel<6>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    case 7: hipLaunchKernelGGL(kacc::proc_power_kernel<7>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+    default: hipLaunchKernelGGL(kacc::proc_power_kernel<8>, grid, dim3(kacc::kBlock), 0, st, d, first, count, out); break;
+  }
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }

@@ -24,10 +24,8 @@ struct kacc_ctx {
   void *tables[KACC_T_COUNT] = {};
   uint64_t counts[KACC_T_COUNT] = {};
   uint32_t *d_err = nullptr;
-  // [0,1] chunk list length / head, [2] deferred pods, [4, 4 + nodes) fused big nodes
-  // arrival counts (zero between launches)
-  uint32_t *d_ctr = nullptr;
-  kacc::ChunkItem *d_items = nullptr;  // [item_cap] items, then [item_cap] doubles (fused trees)
+  uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
+  kacc::ChunkItem *d_items = nullptr;
   uint32_t item_cap = 0;
   uint2 *d_defer = nullptr;
   uint32_t defer_cap = 0;

@@ -70,33 +70,21 @@ inline uint32_t pod_begin(const kacc_interval *b, const Ranges &r, uint32_t q) {
   return q == r.q0 ? r.c0 : b->pod_ctr_end[q - 1];
 }
 
-// The engine's 256-lane tree over rows [p0, p1): lane l sums rows p0+l, p0+l+256,
-// ... in order, then the 256 lane sums are halved pairwise (l += l+s, s = 128..1).
-double tree256(const double *d, uint32_t p0, uint32_t p1) {
-  double lane[256];
-  for (int l = 0; l < 256; ++l) lane[l] = 0.0;
-  for (uint32_t i = p0; i < p1; ++i) lane[(i - p0) & 255u] += d[i];
-  for (int s = 128; s >= 1; s >>= 1)
-    for (int l = 0; l < s; ++l) lane[l] += lane[l + s];
-  return lane[0];
-}
-
-// resource/informer.go:328-345 refreshNode: procCPUDeltaTotal over Running.  Go sums
-// over a map (random order); the engine's canonical order (round 5): a node of at most
-// KOR_CHUNK_ROWS rows is one 256-lane tree; a bigger node is cut into KOR_CHUNK_ROWS-row
-// chunks, each chunk's tree, added in chunk order — the big-node chunks then sum
-// themselves (kacc_engine.hip chunk_kernel) and only one f64 per chunk is exchanged.
+// resource/informer.go:328-345 refreshNode: procCPUDeltaTotal over Running.
 double node_cpu_delta_sum(const double *d, uint32_t p0, uint32_t p1, int mode) {
   if (mode == KOR_SUM_LISTING) {
     double s = 0;
     for (uint32_t i = p0; i < p1; ++i) s += d[i];
     return s;
   }
-  if (p1 - p0 <= KOR_CHUNK_ROWS) return tree256(d, p0, p1);
-  double t = tree256(d, p0, p0 + KOR_CHUNK_ROWS);
-  for (uint32_t c = p0 + KOR_CHUNK_ROWS; c < p1; c += KOR_CHUNK_ROWS)
-    t = t + tree256(d, c, c + KOR_CHUNK_ROWS < p1 ? c + KOR_CHUNK_ROWS : p1);
-  return t;
+  // canonical engine order: lane l sums rows p0+l, p0+l+256, ... in order,
+  // then the 256 lane sums are halved pairwise (l += l+s for s=128..1).
+  double lane[256];
+  for (int l = 0; l < 256; ++l) lane[l] = 0.0;
+  for (uint32_t i = p0; i < p1; ++i) lane[(i - p0) & 255u] += d[i];
+  for (int s = 128; s >= 1; s >>= 1)
+    for (int l = 0; l < s; ++l) lane[l] += lane[l + s];
+  return lane[0];
 }
 
 // The per-zone workload formula shared by process.go:118-148,

@@ -26,13 +26,10 @@ extern "C" {
 
 /* Order used for the node total ProcessTotalCPUTimeDelta (informer.go:330-333).
  * Go sums over a map, so its order is random; the engine's canonical order is
- * KOR_SUM_TREE256 (256 strided lane sums, then a halving tree; a node of more than
- * KOR_CHUNK_ROWS rows: one such tree per KOR_CHUNK_ROWS-row chunk, added in chunk
- * order) and the oracle reproduces it bit for bit.  KOR_SUM_LISTING sums in row
- * (listing) order, which is one of the orders Go may take; tests compare it at
- * 1e-12 rel.                                                                  */
+ * KOR_SUM_TREE256 (256 strided lane sums, then a halving tree) and the oracle
+ * reproduces it bit for bit.  KOR_SUM_LISTING sums in row (listing) order,
+ * which is one of the orders Go may take; tests compare it at 1e-12 rel.   */
 #define KOR_SUM_TREE256 0
-#define KOR_CHUNK_ROWS 2048u /* big nodes: per-chunk trees added in chunk order */
 #define KOR_SUM_LISTING 1
 
 /* Host mirror of the device state tables (same layout, see kacc_table). */

@@ -16,10 +16,13 @@ for c in ${CONFIGS:-3 1}; do
     1) kern="small_kernel<2"; cmd=(python3 "$R/bench.py" --config 1 --steps 5 --warmup 1 --no-cpu-baseline --frag-line 0) ;;
     5) kern="interval_kernel<4, 0>|chunk_kernel<4, 0>|pod_kernel<4, 0>"
        cmd=(python3 "$R/bench.py" --config 5 --steps 3 --warmup 1 --no-cpu-baseline --frag-line 0 --no-pipeline-line --no-host-line) ;;
+    s8) kern="interval_sums_kernel<4, 0>"  # rank 0's 1/8 shard, partial sums in the launch
+       cmd=(python3 "$R/bench.py" --shard-of 8 --steps 20 --warmup 3 --no-cpu-baseline --frag-line 0 --no-pipeline-line --no-host-line) ;;
     *) echo "no PMC recipe for config $c"; exit 2 ;;
   esac
   step fetch_c$c 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/fetch_c$c" -o run -- "${cmd[@]}"
   step write_c$c 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/write_c$c" -o run -- "${cmd[@]}"
-  (cd "$R" && python3 tools/pmc_summary.py "$O/fetch_c$c" "$O/write_c$c" "profiles/${PMC_ROUND:-r04}/${OUT:-pmc} (tools/gpu_pmc_traffic.sh)" \
-     "$O/pmc_traffic.json" "$c" "$kern") || exit $?
+  cfg=$c; shard=1; sums=0; [ "$c" = s8 ] && { cfg=3; shard=8; sums=1; }
+  (cd "$R" && PMC_SHARD_OF=$shard PMC_SUMS=$sums python3 tools/pmc_summary.py "$O/fetch_c$c" "$O/write_c$c" \
+     "profiles/${PMC_ROUND:-r04}/${OUT:-pmc} (tools/gpu_pmc_traffic.sh)" "$O/pmc_traffic.json" "$cfg" "$kern") || exit $?
 done

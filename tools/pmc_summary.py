@@ -38,13 +38,25 @@ def main():
     K = int(sys.argv[7]) if len(sys.argv) > 7 else 1
     from kepler_amd import accel, fleet
 
-    layout = fleet.config_layout(cfg, nodes=40000 if cfg == 1 else None)  # bench.py --config 1 fleet
+    # PMC_SHARD_OF=W: rank 0's shard of the W-way split (bench.py --shard-of W); PMC_SUMS=1: the
+    # launch also carries the previous interval's partial sums (bench.py --totals fused: entry
+    # "config<C>_sums", algorithmic bytes + export_sums_bytes)
+    shard_of = int(os.environ.get("PMC_SHARD_OF", "1"))
+    sums = os.environ.get("PMC_SUMS", "0") == "1"
+    if shard_of > 1:
+        _, _, layout = fleet.config_shard(cfg, shard_of, 0, {1: 40000, 2: 1000, 3: 10000, 5: 1000}[cfg])
+    else:
+        layout = fleet.config_layout(cfg, nodes=40000 if cfg == 1 else None)  # bench.py --config 1 fleet
     s = layout.sizes()
     dims = [s[k] for k in ("n_nodes", "n_procs", "n_ctrs", "n_vms", "n_pods")]
     # the flags bench.py / tools/bench_variants.py run with
     flags = layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES | accel.KACC_F_STABLE_SLOT_NODES
     alg = (accel.interval_bytes(layout.zones, *dims, flags) if K == 1 else
            accel.intervals_bytes(layout.zones, *dims, K, True, flags))
+    if sums:
+        from bench import export_sums_bytes
+
+        alg += export_sums_bytes(layout.zones, s["n_nodes"], s["n_pods"], layout.n_namespaces)
     # KERNEL "a|b|c": the launches of one interval (config 5: interval_kernel + chunk_kernel +
     # pod_kernel), each kernel's median summed
     fm = wm = 0.0
@@ -61,10 +73,11 @@ def main():
     if os.path.exists(out):
         with open(out) as f:
             res = json.load(f)
-    key = f"config{cfg}" + (f"_k{K}" if K > 1 else "")
+    key = f"config{cfg}" + (f"_k{K}" if K > 1 else "") + ("_sums" if sums else "")
     res.update({
         key: {
             "n_procs": s["n_procs"],
+            "shard_of": shard_of,
             "kernel": " + ".join("kacc::" + kn.replace(" ", "") for kn in kernel.split("|")),
             "fetch_size_kib_median": fm,
             "write_size_kib_median": wm,
