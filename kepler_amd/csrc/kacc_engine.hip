@@ -4409,7 +4409,9 @@ int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t c
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint32_t Z = ctx->cfg.zones;
-  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + kacc::kBlock - 1) / kacc::kBlock, 65536)));
+  // one element per lane (the node-table gathers depend on the slot's node: many waves
+  // in flight hide that second round trip, a grid-stride loop would serialise it)
+  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + kacc::kBlock - 1) / kacc::kBlock, 1u << 24)));
   const kacc::ProcDerive d = kacc_derive(ctx, static_cast<kacc_kind>(kind));
   (void)hipGetLastError();
   switch (Z) {
