@@ -168,19 +168,21 @@ struct ChunkItem {
 // block per output value — block c sums column c (node table c / Z of the five,
 // zone c % Z) over every node: lane l < kBlock adds nodes l, l + kBlock, ... in
 // order (kColLoads loads in flight), then the wave tree and the four waves in
-// order — and writes it.  No cross-block combine: no partial exchange, block
-// count or last-block reload (rounds 2-3 summed node ranges per block and let the
-// last block to finish add the partials: four dependent round trips, 6.5 us at
-// the 1/8 shard of config 3 against one or two here; and no reliance on how
-// gfx950 performs agent-scope atomics).  Config 3: 40 loads per lane, hidden
-// under the namespace blocks of the same launch.  Past kColWideNodes the lanes keep kColLoadsWide loads in flight (config 1,
-// 40k nodes: 157 loads per lane in 5 round trips instead of 20: sums 36.8 ->
-// 27.8 us).  That is a kernel of its own (cluster_partials_kernel<Z, kW, true>):
-// its 166 VGPRs would hold the namespace blocks of every fleet at three waves per
-// SIMD instead of eight (config 3, 10k nodes: 17.5 against 16.6 us with 8 loads;
-// profiles/r04/colw).
-constexpr int kColLoads = 8, kColLoadsWide = 32;
-constexpr uint64_t kColWideNodes = 16384;
+// order — and writes it.  No cross-block combine up to kColSplitFrom nodes
+// (config 3: 40 loads per lane, hidden under the namespace blocks of the same
+// launch; the 1/8 shard: 5 per lane, one round trip).
+// Past kColSplitFrom nodes (config 1: 40k) ONE column is more than one CU
+// streams in time (a CU takes in ~11 B per clock: 40k x 16 B of strided column
+// ~ 24 us), so each column is split over ceil(N / kColSplitNodes) blocks: block
+// (c, k) sums nodes [k R, (k+1) R) in the per-lane order above, publishes its
+// partial (an agent-scope store, then an acq_rel agent-scope add to the column's
+// arrival count), and the block that arrives last adds the partials in k order
+// and re-arms the count for the next launch.  The per-column order is fixed by N
+// alone, so every launch (and the fused path, which never splits) gives the same
+// bits for the same inputs.  Round 4's wide instance (32 loads in flight per lane,
+// 166 VGPRs: 27.8 us at 40k nodes) is gone.
+constexpr int kColLoads = 8;
+constexpr uint64_t kColSplitFrom = 16384, kColSplitNodes = 4096;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
   const uint64_t *active_total, *idle_total;
@@ -188,6 +190,9 @@ struct NodeTotalsArgs {
   const uint64_t *node_export;  // else the five tables: an interval's node export [n_nodes][5Z]
   uint64_t *out_e;              // [2Z]: Σ ActiveEnergyTotal, Σ IdleEnergyTotal (u64, modular)
   double *out_p;                // [3Z]: Σ Power, Σ ActivePower, Σ IdlePower (f64)
+  uint32_t split;               // blocks per column (1: no combine)
+  uint64_t *part;               // [5Z][split] the column blocks' partials (split > 1)
+  uint32_t *arrived;            // [5Z] arrival counts, 0 between launches
 };
 
 struct DevState {
@@ -890,13 +895,17 @@ __global__ __launch_bounds__(kBlock) void namespace_kernel(uint32_t n_ns, const 
 // the first 5Z blocks are the node-total columns (NodeTotalsArgs), the last
 // ns_blocks blocks are namespace_kernel's.
 // Column mode of the cluster node totals (see NodeTotalsArgs): block b owns output
-// value b — column b / Z of the five node tables, zone b % Z — and lanes tid < kBlock
-// sum it (the same order whatever the caller's block size); s_w: kBlock / 64 words.
-template <int Z, bool kWideCols = false>
+// value b / split — column (b / split) / Z of the five node tables, zone (b / split) % Z —
+// and, split > 1, its node range b % split; lanes tid < kBlock sum it (the same order
+// whatever the caller's block size); s_w: kBlock / 64 words.  kSplit: the instance
+// that may split (cluster_partials_kernel past kColSplitFrom nodes).
+template <int Z, bool kSplit = false>
 __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint32_t b, uint64_t *s_w) {
   const uint32_t tid = threadIdx.x;
   if (tid >= static_cast<uint32_t>(kBlock)) return;  // no barrier below: the idle lanes leave
-  const uint32_t t = b / Z, z = b % Z;
+  const uint32_t split = kSplit ? na.split : 1u;
+  const uint32_t o = b / split, part = b % split;
+  const uint32_t t = o / Z, z = o % Z;
   const bool is_u64 = t < 2;
   const uint64_t *col = na.node_export ? na.node_export + t * Z + z
                         : t == 0 ? na.active_total + z
@@ -904,33 +913,27 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
                         : reinterpret_cast<const uint64_t *>(t == 2 ? na.power : t == 3 ? na.active_power
                                                                                         : na.idle_power) + z;
   const uint64_t stride = na.node_export ? 5ull * Z : static_cast<uint64_t>(Z);
+  const uint64_t lo = kSplit ? min(static_cast<uint64_t>(part) * kColSplitNodes, na.n_nodes) : 0ull;
+  const uint64_t hi = kSplit && split > 1 ? min(lo + kColSplitNodes, na.n_nodes) : na.n_nodes;
   unsigned long long e = 0;
   double p = 0.0;
-  // lane tid adds nodes tid, tid + kBlock, ... in that order whatever the loads per
-  // round: the wide rounds of big fleets give the same bits with fewer round trips
-  auto rounds = [&](auto loads) {
-    constexpr int kL = decltype(loads)::value;
-    for (uint64_t n0 = tid; n0 < na.n_nodes; n0 += static_cast<uint64_t>(kBlock) * kL) {
-      uint64_t v[kL];
+  // lane tid adds nodes lo + tid, lo + tid + kBlock, ... in that order
+  for (uint64_t n0 = lo + tid; n0 < hi; n0 += static_cast<uint64_t>(kBlock) * kColLoads) {
+    uint64_t v[kColLoads];
 #pragma unroll
-      for (int u = 0; u < kL; ++u) {  // unconditional from clamped nodes: all in flight
-        const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, na.n_nodes - 1);
-        v[u] = col[n * stride];
-      }
-#pragma unroll
-      for (int u = 0; u < kL; ++u) {
-        if (n0 + static_cast<uint64_t>(u) * kBlock >= na.n_nodes) continue;
-        if (is_u64)
-          e += v[u];
-        else
-          p = p + __longlong_as_double(static_cast<long long>(v[u]));
-      }
+    for (int u = 0; u < kColLoads; ++u) {  // unconditional from clamped nodes: all in flight
+      const uint64_t n = min(n0 + static_cast<uint64_t>(u) * kBlock, hi - 1);
+      v[u] = col[n * stride];
     }
-  };
-  if constexpr (kWideCols)
-    rounds(std::integral_constant<int, kColLoadsWide>{});
-  else
-    rounds(std::integral_constant<int, kColLoads>{});
+#pragma unroll
+    for (int u = 0; u < kColLoads; ++u) {
+      if (n0 + static_cast<uint64_t>(u) * kBlock >= hi) continue;
+      if (is_u64)
+        e += v[u];
+      else
+        p = p + __longlong_as_double(static_cast<long long>(v[u]));
+    }
+  }
 #pragma unroll
   for (int sft = 32; sft >= 1; sft >>= 1) {
     e += __shfl_down(e, sft, 64);
@@ -938,17 +941,30 @@ __device__ __forceinline__ void node_column_block(const NodeTotalsArgs na, uint3
   }
   if ((tid & 63u) == 0) s_w[tid >> 6] = is_u64 ? e : static_cast<uint64_t>(__double_as_longlong(p));
   __syncthreads();
-  if (tid == 0) {
-    if (is_u64) {
-      unsigned long long r = s_w[0];
-      for (int w = 1; w < kBlock / 64; ++w) r += s_w[w];
-      na.out_e[t * Z + z] = r;
-    } else {
-      double r = __longlong_as_double(static_cast<long long>(s_w[0]));
-      for (int w = 1; w < kBlock / 64; ++w) r = r + __longlong_as_double(static_cast<long long>(s_w[w]));
-      na.out_p[(t - 2) * Z + z] = r;
+  if (tid != 0) return;
+  auto add = [&](uint64_t a, uint64_t x) -> uint64_t {  // u64 (modular) or f64 bits
+    if (is_u64) return a + x;
+    const double f = __longlong_as_double(static_cast<long long>(a)) + __longlong_as_double(static_cast<long long>(x));
+    return static_cast<uint64_t>(__double_as_longlong(f));
+  };
+  uint64_t r = s_w[0];  // the block's value
+  for (int w = 1; w < kBlock / 64; ++w) r = add(r, s_w[w]);
+  if (kSplit && split > 1) {  // publish; the last block of the column adds the partials in order
+    __hip_atomic_store(na.part + static_cast<uint64_t>(o) * split + part, r, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (__hip_atomic_fetch_add(na.arrived + o, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != split - 1) return;
+    r = __hip_atomic_load(na.part + static_cast<uint64_t>(o) * split, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t k = 1; k < split; ++k) {
+      const uint64_t x =
+          __hip_atomic_load(na.part + static_cast<uint64_t>(o) * split + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r = add(r, x);
     }
+    __hip_atomic_store(na.arrived + o, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
   }
+  if (is_u64)
+    na.out_e[t * Z + z] = r;
+  else
+    na.out_p[(t - 2) * Z + z] = __longlong_as_double(static_cast<long long>(r));
 }
 
 // Partial sums of an earlier interval's exports inside an interval launch
@@ -3074,7 +3090,7 @@ __global__ __launch_bounds__(kBlock) void pod_kernel(const kacc_interval b, cons
   }
 }
 
-template <int Z, int kW = 2 * Z, bool kWideCols = false, bool kIdentity = false>
+template <int Z, int kW = 2 * Z, bool kSplit = false, bool kIdentity = false>
 __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_blocks, uint32_t n_ns,
                                                                   const uint32_t *__restrict__ off,
                                                                   const uint32_t *__restrict__ slots,
@@ -3095,7 +3111,7 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
     return;
   }
   __shared__ uint64_t s_w[kBlock / 64];
-  node_column_block<Z, kWideCols>(na, blockIdx.x, s_w);  // block b owns output value b: column b / Z, zone b % Z
+  node_column_block<Z, kSplit>(na, blockIdx.x, s_w);  // column (b / split) / Z, zone (b / split) % Z
 }
 
 
@@ -3216,6 +3232,13 @@ uint64_t table_count(const kacc_config &c, int t) {
     default: base = c.pod_slots; break;
   }
   return d.zoned ? base * c.zones : base;
+}
+
+// the split cluster node totals' scratch (NodeTotalsArgs.part / arrived)
+constexpr size_t kColArrivedBytes = 5 * KACC_MAX_ZONES * sizeof(uint32_t);
+size_t col_part_bytes(uint64_t nodes) {
+  const uint64_t split = std::max<uint64_t>((nodes + kacc::kColSplitNodes - 1) / kacc::kColSplitNodes, 1);
+  return 5 * KACC_MAX_ZONES * split * sizeof(uint64_t);
 }
 
 kacc::DevState dev_state(const kacc_ctx *ctx) {
@@ -3355,6 +3378,7 @@ kacc::NodeTotalsArgs node_totals_args(const kacc_ctx *ctx, uint64_t live, const 
   na.out_e = node_energy;
   na.out_p = node_power;
   na.node_export = node_export;
+  na.split = 1;
   return na;
 }
 
@@ -3372,19 +3396,26 @@ void launch_cluster_partials(uint32_t n_ns, const uint32_t *off, const uint32_t 
   const double *pp = pod_export ? reinterpret_cast<const double *>(pod_export + Z)
                                 : (const double *)ctx->tables[KACC_T_POD_POWER];
   const uint64_t rows = pod_export ? n_pods : ctx->cfg.pod_slots;
-  const bool wide = na.n_nodes > kacc::kColWideNodes && node_blocks;
+  const bool wide = na.n_nodes > kacc::kColSplitFrom && node_blocks;
+  kacc::NodeTotalsArgs nas = na;
+  if (wide) {  // each column over ceil(N / kColSplitNodes) blocks, combined by the last one
+    nas.split = static_cast<uint32_t>((na.n_nodes + kacc::kColSplitNodes - 1) / kacc::kColSplitNodes);
+    nas.part = ctx->d_colpart;
+    nas.arrived = ctx->d_colarrived;
+    node_blocks *= nas.split;
+  }
   if (wide && ordered)
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, true, true>), dim3(ns_blocks + node_blocks),
-                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, nas);
   else if (wide)
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, true>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock),
-                0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+                0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, nas);
   else if (ordered)
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z, 2 * Z, false, true>), dim3(ns_blocks + node_blocks),
-                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+                dim3(kacc::kBlock), 0, st, ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, nas);
   else
     KACC_LAUNCH((kacc::cluster_partials_kernel<Z>), dim3(ns_blocks + node_blocks), dim3(kacc::kBlock), 0, st,
-                ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, na);
+                ns_blocks, n_ns, off, slots, pe, pp, rows, out_e, out_p, ctx->d_err, nas);
 }
 
 // An interval and the partial sums of an earlier interval's exports in ONE launch
@@ -3737,7 +3768,9 @@ int kacc_create(int device, const kacc_config *cfg, kacc_ctx **out) {
   }
   ctx->tables[KACC_T_POD_POWER] = static_cast<char *>(ctx->tables[KACC_T_POD_ENERGY]) + 8ull * ctx->cfg.zones;
   if ((e = hipMalloc(&ctx->d_err, sizeof(uint32_t))) != hipSuccess ||
-      (e = hipMalloc(&ctx->d_ctr, 16)) != hipSuccess) {
+      (e = hipMalloc(&ctx->d_ctr, 16)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_colpart, col_part_bytes(cfg->nodes))) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_colarrived, kColArrivedBytes)) != hipSuccess) {
     fail(ctx, KACC_ENOMEM, "hipMalloc work words: %s", hipGetErrorString(e));
     return bail(KACC_ENOMEM);
   }
@@ -3755,6 +3788,8 @@ void kacc_destroy(kacc_ctx *ctx) {
     if (ctx->tables[t] && t != KACC_T_POD_POWER) (void)hipFree(ctx->tables[t]);  // pod power: inside the records
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
+  if (ctx->d_colpart) (void)hipFree(ctx->d_colpart);
+  if (ctx->d_colarrived) (void)hipFree(ctx->d_colarrived);
   if (ctx->d_items) (void)hipFree(ctx->d_items);
   if (ctx->d_defer) (void)hipFree(ctx->d_defer);
   if (ctx->batch_copied) {
@@ -3785,6 +3820,7 @@ int kacc_reset(kacc_ctx *ctx) {
       KACC_HIP(ctx, hipMemsetAsync(ctx->tables[t], 0, table_alloc_bytes(ctx, t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
   KACC_HIP(ctx, hipMemsetAsync(ctx->d_ctr, 0, 16, ctx->stream));
+  KACC_HIP(ctx, hipMemsetAsync(ctx->d_colarrived, 0, kColArrivedBytes, ctx->stream));
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   ctx->live_nodes = 0;
   return KACC_OK;
@@ -4385,7 +4421,7 @@ int kacc_run_interval_sums(kacc_ctx *ctx, const kacc_interval *b, const kacc_exp
                                   "(double-buffer them)");
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const bool fuse = b->n_nodes > 0 && !(b->flags & KACC_F_SMALL_NODES) &&
-                    !(sa.node_blocks && sa.na.n_nodes > kacc::kColWideNodes) &&
+                    !(sa.node_blocks && sa.na.n_nodes > kacc::kColSplitFrom) &&
                     (sa.n_ns || sa.node_blocks) &&
                     static_cast<uint64_t>(b->n_nodes) + sa.node_blocks + sa.ns_blocks <= 0x7fffffffull;
   if (!fuse) {  // the interval, then the sums as a launch of their own (the same results)

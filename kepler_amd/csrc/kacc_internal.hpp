@@ -26,6 +26,10 @@ struct kacc_ctx {
   uint32_t *d_err = nullptr;
   uint32_t *d_ctr = nullptr;  // [0,1] chunk list length / head, [2] deferred pods
   kacc::ChunkItem *d_items = nullptr;
+  // cluster node totals past kColSplitFrom nodes: [5 * KACC_MAX_ZONES][col_split_cap] column
+  // partials and [5 * KACC_MAX_ZONES] arrival counts (zero between launches)
+  uint64_t *d_colpart = nullptr;
+  uint32_t *d_colarrived = nullptr;
   uint32_t item_cap = 0;
   uint2 *d_defer = nullptr;
   uint32_t defer_cap = 0;

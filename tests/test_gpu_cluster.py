@@ -389,9 +389,9 @@ def test_cluster_node_totals_follow_the_live_nodes():
 def test_cluster_node_totals_back_to_back_launches():
     """The cluster node totals under back-to-back launches with no host sync: 24 intervals of
     changing node data, each followed by its partial sums into its own row.  20k nodes: past
-    kColWideNodes, so the wide column-mode instance (cluster_partials_kernel<Z, kW, true>,
-    32 loads in flight per lane) runs; a stale or mixed-up total would show against the oracle
-    (the round-3 last-block handoff this pinned is gone)."""
+    kColSplitFrom, so every column is split over 5 blocks whose partials the last-arriving
+    block adds (and re-arms the arrival count for the next launch); a stale partial, a
+    count left armed or a mixed-up total would show against the oracle."""
     from oracle.oracle import Oracle
 
     n, Z, K = 20000, 2, 24
