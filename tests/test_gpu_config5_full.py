@@ -12,7 +12,7 @@ import torch
 
 from kepler_amd import accel, fleet
 from kepler_amd.torch_batch import current_stream_handle, interval_from_tensors, to_device
-from table_check import assert_table_equal
+from table_check import assert_tables_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -50,6 +50,5 @@ def test_config5_full_size_bit_exact():
     acc.sync(s)
     for a in ivs:
         ora.interval(a, sizes)
-    for tname, _ in accel.TABLES:
-        assert_table_equal(acc.download(tname), ora.state[tname], tname)
+    assert_tables_equal(acc.download, ora.state, "config 5")
     acc.close()
