@@ -182,7 +182,13 @@ struct ChunkItem {
 // bits for the same inputs.  Round 4's wide instance (32 loads in flight per lane,
 // 166 VGPRs: 27.8 us at 40k nodes) is gone.
 constexpr int kColLoads = 8;
-constexpr uint64_t kColSplitFrom = 16384, kColSplitNodes = 4096;
+#ifndef KACC_COL_SPLIT_FROM
+#define KACC_COL_SPLIT_FROM 16384  // from 4096 with 2048-node blocks: config 3 16.6 -> 19.2 us,
+#endif                             // config 1 23.1 -> 28.5 us (profiles/r05/r05l)
+#ifndef KACC_COL_SPLIT_NODES
+#define KACC_COL_SPLIT_NODES 4096
+#endif
+constexpr uint64_t kColSplitFrom = KACC_COL_SPLIT_FROM, kColSplitNodes = KACC_COL_SPLIT_NODES;
 struct NodeTotalsArgs {
   uint64_t n_nodes;
   const uint64_t *active_total, *idle_total;
@@ -3098,12 +3104,13 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
                                                                   const double *__restrict__ pp, uint64_t pod_slots,
                                                                   uint64_t *out_e, double *out_p, uint32_t *err,
                                                                   const NodeTotalsArgs na) {
-  // the first 5Z blocks are the cluster node totals in column mode: block c owns
-  // output value c (column c / Z of the five node tables, zone c % Z) and writes it,
-  // with no cross-block combine; they come first because their per-lane chain of
-  // loads is the longer one (node blocks dispatched last finished last:
-  // profiles/r03/tprobe2).  The remaining ns_blocks blocks are the namespace sums.
-  // The block count and the 5Z column blocks are the only coupling between blocks.
+  // the first 5Z x split blocks are the cluster node totals in column mode: block b
+  // owns output value b / split (column (b / split) / Z of the five node tables, zone
+  // (b / split) % Z) and, split > 1 (kSplit instance), node range b % split, whose
+  // partial the column's last-arriving block adds (node_column_block); they come first
+  // because their per-lane chain of loads is the longer one (node blocks dispatched
+  // last finished last: profiles/r03/tprobe2).  The remaining ns_blocks blocks are the
+  // namespace sums.
   const uint32_t nb = gridDim.x - ns_blocks;
   if (blockIdx.x >= nb) {
     namespace_block<Z, kW, kBlock, kIdentity>(blockIdx.x - nb, n_ns, off, slots, pe, pp, pod_slots, out_e, out_p,
