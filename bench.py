@@ -574,14 +574,17 @@ def _pack(arrays):
     return img, layout
 
 
-def host_path_ticks_line(args, steps=10):
+def host_path_ticks_line(args, steps=10, nbuf=3, mode="full"):
     """End-to-end with the CPU-tick input format (kepler_accel.h "CPU-tick input format"): per
     interval ONE pinned host image crosses PCIe — node readings and CSR, per process row its PID
     (4 B, for the device slot join) and its tick increment (2 B; 1 % escapes as int64), the
     aggregates' CSR ends and slot words — then, on the device, kacc_slot_join (PIDs -> slot words,
     KACC_JOIN_REUSE_TERMINATED) -> kacc_ticks_delta (Go's CPUTimeDelta from the tick map) ->
-    kacc_run_interval.  Two staging buffers: interval i + 1's copy (copy stream) overlaps interval
-    i's kernels (compute stream).  Reported beside the headline, never as `value`."""
+    kacc_run_interval.  Three staging buffers: the copies (copy stream) run back to back while
+    the kernels (compute stream) follow them — with two, a copy waited for the interval two back
+    and the path ran at 3.39 ms against a 2.62 ms copy; with three (or four) 2.71 ms
+    (profiles/r05/r05m, tools/bench_host_ticks.py).  Reported beside the headline, never as
+    `value`."""
     import ctypes
 
     import torch
@@ -605,7 +608,7 @@ def host_path_ticks_line(args, steps=10):
     rng = np.random.default_rng(5)
     statics = layout.static_arrays()
     imgs = []
-    for k in range(2):
+    for k in range(nbuf):
         node = sim.next_node_inputs()
         keys = churn.next_keys()
         dt = rng.integers(0, 3000, size=P).astype(np.uint16)
@@ -623,7 +626,7 @@ def host_path_ticks_line(args, steps=10):
         imgs.append(_pack(arrays))
     nbytes = max(im.nbytes for im, _ in imgs)
     host = [torch.from_numpy(im).pin_memory() for im, _ in imgs]
-    dev = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    dev = [torch.empty(nbytes, dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
     d_slot = torch.zeros(P, dtype=torch.int32, device="cuda")
     d_delta = torch.zeros(P, dtype=torch.float64, device="cuda")
     cap = int(slot_off[-1])
@@ -638,7 +641,7 @@ def host_path_ticks_line(args, steps=10):
         return {n: dev[b][o:o + cnt_ * dt_.itemsize].view(tdt[dt_]) for n, (o, dt_, cnt_) in lay.items()}
 
     descs = []
-    for b in range(2):
+    for b in range(nbuf):
         v = views(b, imgs[b][1])
         t = {n: v[n] for n in ("node_ts_ns", "node_usage_ratio", "node_status", "zone_energy", "zone_max",
                                "proc_off", "ctr_off", "vm_off", "pod_off", "ctr_proc_end", "ctr_slot",
@@ -654,18 +657,23 @@ def host_path_ticks_line(args, steps=10):
     compute = torch.cuda.current_stream()
     copy = torch.cuda.Stream()
     cs = compute.cuda_stream
-    copied = [torch.cuda.Event() for _ in range(2)]
-    done = [torch.cuda.Event() for _ in range(2)]
-    used = [False, False]
+    copied = [torch.cuda.Event() for _ in range(nbuf)]
+    done = [torch.cuda.Event() for _ in range(nbuf)]
+    used = [False] * nbuf
 
     def one(i):
-        b = i % 2
-        if used[b]:
-            copy.wait_event(done[b])  # staging b is free once interval i - 2 has run
-        with torch.cuda.stream(copy):
-            dev[b][:imgs[b][0].nbytes].copy_(host[b], non_blocking=True)
-        copied[b].record(copy)
-        compute.wait_event(copied[b])
+        b = i % nbuf
+        if mode != "compute":  # mode: "copy" / "compute" time one side alone (diagnostics)
+            if used[b]:
+                copy.wait_event(done[b])  # staging b is free once interval i - nbuf has run
+            with torch.cuda.stream(copy):
+                dev[b][:imgs[b][0].nbytes].copy_(host[b], non_blocking=True)
+            copied[b].record(copy)
+            if mode == "copy":
+                done[b].record(copy)
+                used[b] = True
+                return
+            compute.wait_event(copied[b])
         iv, tks, v, _ = descs[b]
         sm.join(P, v["proc_off"].data_ptr(), v["pid"].data_ptr(), v["node_status"].data_ptr(), d_slot.data_ptr(),
                 tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), cs, span.data_ptr())
@@ -675,6 +683,9 @@ def host_path_ticks_line(args, steps=10):
         used[b] = True
 
     try:
+        if mode == "compute":  # the images resident once
+            for b in range(nbuf):
+                dev[b][:imgs[b][0].nbytes].copy_(host[b])
         for i in range(4):  # first read + warm-up
             one(i)
         torch.cuda.synchronize()
@@ -710,10 +721,10 @@ def host_path_ticks_line(args, steps=10):
             "proc_attr_per_s": P / tp, "node_snapshots_per_s": N / tp, "ms_per_interval": tp * 1e3,
             "h2d_bytes_per_interval": nbytes, "bytes_per_process_row": nbytes / P, "escapes": n_esc,
             "pcie_copy_ms": t_copy * 1e3, "pcie_copy_GBps": nbytes / t_copy / 1e9,
-            "frac_of_pcie_copy": t_copy / tp, "buffers_in_flight": 2, "intervals": steps,
+            "frac_of_pcie_copy": t_copy / tp, "buffers_in_flight": nbuf, "mode": mode, "intervals": steps,
             "note": "one pinned image per interval (node readings + CSR, PID u32 + tick increment u16 per "
-                    "process, 1 % int64 escapes, aggregate CSR ends + slot words); copy stream / compute stream "
-                    "overlap, two staging buffers; the join's churn is fleet.ProcChurn (2 %)"}
+                    f"process, 1 % int64 escapes, aggregate CSR ends + slot words); copy stream / compute stream "
+                    f"overlap, {nbuf} staging buffers; the join's churn is fleet.ProcChurn (2 %)"}
 
 
 def bench_nodes(config, world, nodes=None, scaling="strong"):
