@@ -3122,26 +3122,37 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
 }
 
 
-// Elements [first, first + count) of the derived process power table
-// ([slot*Z + z], kacc_derive.hpp), grid-stride.
 // Derived powers of elements [first, first + count) ([slot*Z + z]) into out: one lane per
-// ELEMENT (a wave stores 512 contiguous bytes), slot = e / Z by a compile-time Z (a
-// multiply, not a 64-bit division); the Z lanes of a slot read its ratio and node from the
-// same line, the node's guards come from cache.  Per slot: ratio 8 + node 4 in, 8Z out
+// element, kPowPerLane elements per lane a block-width apart (every wave store 512
+// contiguous bytes), slot = e / Z by a compile-time Z (a multiply, not a 64-bit
+// division).  Each element's slot ratio and node load together, all of the lane's at
+// once, then the node's guard values (cache hits): two round trips per lane, four
+// elements' bytes in flight behind each.  Per slot: ratio 8 + node 4 in, 8Z out
 // (bench.py scrape_powers).
+constexpr int kPowPerLane = 4;
 template <int Z>
 __global__ __launch_bounds__(kBlock) void proc_power_kernel(const ProcDerive d, uint64_t first, uint64_t count,
                                                             double *out) {
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < count;
-       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kBlock * kPowPerLane + threadIdx.x;
+  uint32_t n[kPowPerLane];
+  double r[kPowPerLane];
+#pragma unroll
+  for (int u = 0; u < kPowPerLane; ++u) {  // unconditional from a clamped element
+    const uint64_t s = (first + min(i0 + static_cast<uint64_t>(u) * kBlock, count - 1)) / Z;
+    n[u] = d.node[s];
+    r[u] = d.ratio[s];
+  }
+#pragma unroll
+  for (int u = 0; u < kPowPerLane; ++u) {
+    const uint64_t i = i0 + static_cast<uint64_t>(u) * kBlock;
+    if (i >= count) break;
     const uint64_t e = first + i, s = e / Z;
     const uint32_t z = static_cast<uint32_t>(e - s * Z);
-    const uint32_t n = d.node[s];
     double p = 0.0;
-    if (n < d.nodes) {
-      const uint64_t k = static_cast<uint64_t>(n) * Z + z;
+    if (n[u] < d.nodes) {
+      const uint64_t k = static_cast<uint64_t>(n[u]) * Z + z;
       const double aP = d.active_power[k];
-      if (d.active_energy[k] != 0 && d.cpu_delta[n] != 0 && aP != 0) p = d.ratio[s] * aP;  // process.go:124, 142
+      if (d.active_energy[k] != 0 && d.cpu_delta[n[u]] != 0 && aP != 0) p = r[u] * aP;  // process.go:124, 142
     }
     __builtin_nontemporal_store(p, out + i);
   }
@@ -4452,9 +4463,10 @@ int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t c
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint32_t Z = ctx->cfg.zones;
-  // one element per lane (the node-table gathers depend on the slot's node: many waves
-  // in flight hide that second round trip, a grid-stride loop would serialise it)
-  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + kacc::kBlock - 1) / kacc::kBlock, 1u << 24)));
+  // kPowPerLane elements per lane, no grid-stride loop (a loop would serialise the lanes'
+  // round trips); count <= 2^31 * 1024 elements for any table the context can hold
+  const uint64_t per_block = static_cast<uint64_t>(kacc::kBlock) * kacc::kPowPerLane;
+  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + per_block - 1) / per_block, 0x7fffffffull)));
   const kacc::ProcDerive d = kacc_derive(ctx, static_cast<kacc_kind>(kind));
   (void)hipGetLastError();
   switch (Z) {
