@@ -1138,7 +1138,9 @@ def main():
     bytes_per_launch = accel.intervals_bytes(Z, sizes["n_nodes"], sizes["n_procs"], sizes["n_ctrs"], sizes["n_vms"],
                                              sizes["n_pods"], K, fused, w.flags) / K
     sums_bytes = export_sums_bytes(Z, sizes["n_nodes"], sizes["n_pods"], w.n_ns) if w.fused_sums else 0
-    bytes_per_launch += sums_bytes
+    # the timed region's first launch carries no earlier step's sums (its last step's sums run
+    # as a launch of their own, untimed): steps - 1 of the `steps` timed launches move them
+    bytes_per_launch += sums_bytes * (args.steps - 1) / args.steps
     k_avg_ms = float(np.mean(kernel_ms))
     achieved = bytes_per_launch / (k_avg_ms * 1e-3) / 1e9
 
@@ -1264,6 +1266,17 @@ def main():
             result["scrape_powers"] = scrape_line(w.acc, w.sizes["n_procs"], Z)
         except Exception as e:  # a secondary line: report, never lose the headline
             result["scrape_powers"] = {"error": repr(e)}
+        sp = result["scrape_powers"]
+        if "ms" in sp:  # beside `value`: the same steps with every interval's process powers scraped
+            step_ms = result["ms_per_step"] + K * sp["ms"]
+            extra = {"value_with_scrape": total_procs * K / (step_ms * 1e-3),
+                     "value_note": "value: intervals attributed, process Usage.Power derived on read (not "
+                                   "materialised); value_with_scrape: the same steps plus one kacc_table_read of "
+                                   "every process power per interval (scrape_powers.ms each)"}
+            items = list(result.items())
+            at = [k for k, _ in items].index("value") + 1
+            result.clear()
+            result.update(items[:at] + list(extra.items()) + items[at:])
     w.close()
     del w
 

@@ -227,8 +227,11 @@ typedef struct kacc_interval {
    * ns_pod_off[k] .. ns_pod_off[k+1]) the export is in NAMESPACE order and its
    * partial sums stream contiguous records (kacc_export_sums.ns_ordered)
    * instead of gathering one record per pod (Pod.Namespace,
-   * resource/types.go:109).  A row >= n_pods raises KACC_ERANGE and is not
-   * written.                                                                 */
+   * resource/types.go:109).  Exports written through pod_export_pos are in
+   * namespace order: only kacc_run_export_sums / kacc_run_interval_sums with
+   * kacc_export_sums.ns_ordered = 1 may sum them (kacc_allreduce_exports and
+   * the cluster export partials read pod exports in batch order).  A row
+   * >= n_pods raises KACC_ERANGE and is not written.                         */
   const uint32_t *pod_export_pos;
 } kacc_interval;
 
@@ -534,7 +537,13 @@ typedef struct kacc_export_sums {
  * overlap); they were complete when this call's work starts on `stream` (the
  * interval that wrote them was queued there before).  The outputs are complete
  * when this call's work is.  Batches of KACC_F_SMALL_NODES, and node totals over
- * more than 16384 nodes, run the sums as a launch of their own (same results).  */
+ * more than 16384 nodes, run the sums as a launch of their own (same results).
+ * Past 16384 nodes the node-total columns are split over node blocks whose
+ * partials meet in per-CONTEXT arrival counters: the launches of one context
+ * that compute node totals (this call, kacc_run_export_sums,
+ * kacc_cluster_partials) must be serialized — one stream, or ordered by events.
+ * The outputs may not alias any export read or written by the launch
+ * (KACC_EINVAL).                                                              */
 int kacc_run_interval_sums(kacc_ctx *ctx, const kacc_interval *dev_batch, const kacc_export_sums *prev,
                            void *stream);
 /* The same partial sums alone, as one launch on `stream` (the last interval's). */
@@ -821,7 +830,9 @@ int kacc_zone_agg_read(kacc_zone_agg *z, const uint64_t *readings, const uint32_
  * +Inf/-Inf spelled out, else Go strconv.AppendFloat(f, 'g', -1, 64)).
  * out: device [count * KACC_FMT_WIDTH] bytes, element i's text left-aligned in
  * its field (zero-padded); len: device [count] text lengths.  Labels are the
- * Go side's strings; it joins them with these fields into sample lines.       */
+ * Go side's strings; it joins them with these fields into sample lines.
+ * KACC_T_NODE_USAGE_RATIO is written as the float64 it is
+ * (kepler_node_cpu_usage_ratio, power_collector.go:250-255).                 */
 #define KACC_FMT_WIDTH 24
 int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, char *out,
                        uint8_t *len, void *stream);
@@ -843,6 +854,10 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
  *   line_off: DEVICE [count * n_zones + 1] byte offset of every line (+ total)
  *   out: DEVICE buffer of out_cap bytes, or NULL to size only
  *   *total: HOST, bytes of the whole text.
+ * t is a workload energy / power table (rows = slots) or one of the node x
+ * zone energy / power tables (rows = nodes; the node families carry a
+ * per-zone `path` label that sorts before zone, so a caller writes them one
+ * zone per call, power_collector.go:257-298).
  * Synchronous (the total is read back).  KACC_ERANGE when out_cap < *total.   */
 int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t count, const char *name,
                       const char *const *zone_names, const uint32_t *zone_order, uint32_t n_zones,

@@ -1326,7 +1326,8 @@ __device__ __forceinline__ void interval_node(const kacc_interval &b, const DevS
   // non-temporal 16-B stores — 1 KiB per wave instruction instead of 16-B pieces at a
   // 16Z-B stride per lane (block-uniform; the late-aggregate order only)
   constexpr uint32_t kStageWords = kRowsLds;  // s_d as u64 words
-  const bool stage = kLateAgg<V> && b.pod_export && !b.pod_export_pos && nq * 2u * Z <= kStageWords;
+  const bool stage = kLateAgg<V> && (V & kVarSkipAggregates) == 0 && b.pod_export && !b.pod_export_pos &&
+                     nq * 2u * Z <= kStageWords;
   uint64_t *s_stage = reinterpret_cast<uint64_t *>(s_d);
   auto aggregate_out = [&]() {  // container.go:106-140 / vm.go:78-109 / pod.go:87-118
     if (!a_ok) {
@@ -3957,7 +3958,14 @@ int kacc_sync(kacc_ctx *ctx, void *stream) {
   KACC_HIP(ctx, hipMemcpy(&err, ctx->d_err, sizeof(err), hipMemcpyDeviceToHost));
   if (err) {
     KACC_HIP(ctx, hipMemset(ctx->d_err, 0, sizeof(uint32_t)));
-    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list 32=oversized node under KACC_F_FAST_NODES 64=join key 128=join range 256=format lines)", err);
+    // every bit a library kernel raises (kacc_engine / join / format / tracker / ticks /
+    // packer / cluster); any other bit has no writer in the library — a stray device
+    // store into this word — and is named as such
+    constexpr uint32_t kKnown = 0x1ffu | (1u << 10);
+    if (err & ~kKnown)
+      return fail(ctx, KACC_ERANGE, "device error word 0x%x holds bits no library kernel raises (0x%x): a stray "
+                  "device store into the context's error word; known bits 0x%x", err, err & ~kKnown, err & kKnown);
+    return fail(ctx, KACC_ERANGE, "device range check failed (bits 0x%x: 1=node 2=offsets 4=slot 8=namespace 16=work list 32=oversized node under KACC_F_FAST_NODES 64=join key 128=join range 256=format lines 1024=tracker capacity)", err);
   }
   return KACC_OK;
 }
@@ -4430,13 +4438,27 @@ int kacc_run_interval_sums(kacc_ctx *ctx, const kacc_interval *b, const kacc_exp
   kacc::SumsArgs sa;
   if ((rc = sums_args(ctx, prev, kacc::kTpb<0>, sa)) != KACC_OK) return rc;
   const uint64_t Z = ctx->cfg.zones;
-  // the sums read an EARLIER interval's exports while this one writes its own
+  // the sums read an EARLIER interval's exports while this one writes its own, and the
+  // sums' outputs are written in the same launch: no output may alias an export of
+  // either interval (a silent race inside one launch otherwise)
   if (overlaps(prev->pod_export, 16 * Z * prev->n_pods, b->pod_export, 16 * Z * b->n_pods) ||
       overlaps(prev->node_export, 40 * Z * prev->n_nodes, b->node_export, 40 * Z * b->n_nodes) ||
       overlaps(prev->pod_export, 16 * Z * prev->n_pods, b->node_export, 40 * Z * b->n_nodes) ||
       overlaps(prev->node_export, 40 * Z * prev->n_nodes, b->pod_export, 16 * Z * b->n_pods))
     return fail(ctx, KACC_EINVAL, "export sums: the exports read overlap the exports this interval writes "
                                   "(double-buffer them)");
+  {
+    const struct { const void *p; uint64_t bytes; } outs[4] = {
+        {prev->out_energy, 8 * Z * prev->n_ns}, {prev->out_power, 8 * Z * prev->n_ns},
+        {prev->out_node_energy, prev->node_export ? 16 * Z : 0}, {prev->out_node_power, prev->node_export ? 24 * Z : 0}};
+    const struct { const void *p; uint64_t bytes; } ins[4] = {
+        {prev->pod_export, 16 * Z * prev->n_pods}, {prev->node_export, 40 * Z * prev->n_nodes},
+        {b->pod_export, 16 * Z * b->n_pods}, {b->node_export, 40 * Z * b->n_nodes}};
+    for (const auto &o : outs)
+      for (const auto &e : ins)
+        if (overlaps(o.p, o.bytes, e.p, e.bytes))
+          return fail(ctx, KACC_EINVAL, "export sums: an output of the sums overlaps an export of this launch");
+  }
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const bool fuse = b->n_nodes > 0 && !(b->flags & KACC_F_SMALL_NODES) &&
                     !(sa.node_blocks && sa.na.n_nodes > kacc::kColSplitFrom) &&

@@ -378,7 +378,8 @@ __device__ void write_joules(uint64_t e, Text &t) {
 struct Args {
   const void *src;
   uint64_t count;
-  uint32_t is_energy;  // u64 µJ -> Joules(); else f64 µW -> Watts()
+  uint32_t is_energy;  // u64 µJ -> Joules(); else f64 / div
+  double div;          // 1e6: µW -> Watts(); 1: a plain float64 (Node.UsageRatio)
   char *out;
   uint8_t *len;
 };
@@ -390,7 +391,7 @@ __global__ __launch_bounds__(kThreads) void format_kernel(const Args a) {
   if (a.is_energy)
     write_joules(static_cast<const uint64_t *>(a.src)[i], o);  // energy.go:30-32
   else
-    write_float(static_cast<const double *>(a.src)[i] / 1e6, o);  // energy.go:57-59
+    write_float(static_cast<const double *>(a.src)[i] / a.div, o);  // energy.go:57-59 (x / 1 == x)
   uint64_t *dst = reinterpret_cast<uint64_t *>(a.out + i * KACC_FMT_WIDTH);
   dst[0] = o.w[0];
   dst[1] = o.w[1];
@@ -772,7 +773,10 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
   const bool power = t == KACC_T_NODE_POWER || t == KACC_T_NODE_ACTIVE_POWER || t == KACC_T_NODE_IDLE_POWER ||
                      t == KACC_T_PROC_POWER || t == KACC_T_CTR_POWER || t == KACC_T_VM_POWER ||
                      t == KACC_T_POD_POWER;
-  if (!energy && !power) return kacc_fail(ctx, KACC_EINVAL, "table %d is not an energy or power table", (int)t);
+  // kepler_node_cpu_usage_ratio (power_collector.go:280-285): Node.UsageRatio as is
+  const bool plain = t == KACC_T_NODE_USAGE_RATIO;
+  if (!energy && !power && !plain)
+    return kacc_fail(ctx, KACC_EINVAL, "table %d is not an energy, power or usage-ratio table", (int)t);
   if (first > ctx->counts[t] || count > ctx->counts[t] - first)
     return kacc_fail(ctx, KACC_EINVAL, "format range outside table %d", (int)t);
   if (!count) return KACC_OK;
@@ -795,6 +799,7 @@ int kacc_format_values(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t cou
   }
   a.count = count;
   a.is_energy = energy ? 1u : 0u;
+  a.div = plain ? 1.0 : 1e6;
   a.out = out;
   a.len = len;
   (void)hipGetLastError();  // clear a stale error of an earlier call
@@ -817,11 +822,16 @@ int kacc_format_lines(kacc_ctx *ctx, kacc_table t, uint64_t first, uint64_t coun
   if (!ctx || t < 0 || t >= KACC_T_COUNT || !total) return KACC_EINVAL;
   *total = 0;
   const uint32_t Z = ctx->cfg.zones;
+  // workload tables (rows = slots) and the node x zone tables (rows = nodes: the node
+  // families of power_collector.go:246-278, one call per zone for their path label)
   const bool energy = t == KACC_T_PROC_ENERGY || t == KACC_T_CTR_ENERGY || t == KACC_T_VM_ENERGY ||
-                      t == KACC_T_POD_ENERGY;
+                      t == KACC_T_POD_ENERGY || t == KACC_T_NODE_ENERGY_TOTAL || t == KACC_T_NODE_ACTIVE_TOTAL ||
+                      t == KACC_T_NODE_IDLE_TOTAL;
   const bool power = t == KACC_T_PROC_POWER || t == KACC_T_CTR_POWER || t == KACC_T_VM_POWER ||
-                     t == KACC_T_POD_POWER;
-  if (!energy && !power) return kacc_fail(ctx, KACC_EINVAL, "table %d is not a workload energy or power table", (int)t);
+                     t == KACC_T_POD_POWER || t == KACC_T_NODE_POWER || t == KACC_T_NODE_ACTIVE_POWER ||
+                     t == KACC_T_NODE_IDLE_POWER;
+  if (!energy && !power)
+    return kacc_fail(ctx, KACC_EINVAL, "table %d is not a workload or node energy / power table", (int)t);
   const uint64_t slots = ctx->counts[t] / Z;
   if (first > slots || count > slots - first)
     return kacc_fail(ctx, KACC_EINVAL, "format_lines: rows outside table %d", (int)t);

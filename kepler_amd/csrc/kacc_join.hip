@@ -297,10 +297,30 @@ constexpr int kJSeenNR = 64;   // seen marks without return; duplicates found by
 constexpr int kJVec = 128;     // a lane's keys loaded / slot words stored as vectors
 constexpr int kJGroup = 256;   // kJ6B lookups read four buckets per LDS read
 constexpr int kJDpp = 1024;    // block scans by DPP moves instead of LDS permutes
+// Steady-state nodes finish in ONE wave (round 6): after the lookups' barrier a node whose
+// churn fits (new rows <= kNewCap and the free slots, no rebuild due) has its found rows'
+// slot words stored by their own lanes, and waves 1-7 end; wave 0 alone lists the
+// terminated IDs, hands out the free slots, inserts the new IDs and writes the changed
+// buckets back — no block scan, no further barrier.  Any other node (first interval,
+// mass churn, a rebuild, a range error) takes the block-wide steps 3-7 unchanged.  The
+// held-slot marks carry each slot's bucket (s_bkt), so the terminated IDs are found from
+// the bitmaps without a pass over the table; an ID found twice is caught by the seen
+// mark's return value (not by counting), so the decision needs no step-3 scan.
+constexpr int kJEasy = 2048;
+constexpr uint32_t kPendWords = (kSmallRows + 31) / 32;  // rows-not-found bitmap (kJEasy)
 
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// LDS ordering among the lanes of ONE wave (kJEasy's wave-0 tail): a wave's LDS
+// instructions execute in order; the fences keep the compiler from moving an access
+// across the point and wait for the wave's own LDS operations.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -394,6 +414,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   constexpr bool kLock = (V & kJLock) != 0, kErrReg = (V & kJErrReg) != 0, kInsDup = (V & kJInsDup) != 0;
   constexpr bool kScan2 = (V & kJScan2) != 0, kSeenNR = (V & kJSeenNR) != 0, kVec = (V & kJVec) != 0;
   constexpr bool kGroup = k6 && (V & kJGroup) != 0;
+  constexpr bool kEasy = (V & kJEasy) != 0;
+  static_assert(!kEasy || (!kSeenNR && kLock && kErrReg && kInsDup && kScan2),
+                "kJEasy builds on the lock-step lookups with returned seen marks");
   using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
   using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
   using SlotT = std::conditional_t<k6, uint16_t, uint32_t>;
@@ -410,6 +433,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   __shared__ uint32_t s_dirty[kLdsBuckets / 32];
   __shared__ uint32_t s_wave[2 * kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
   __shared__ uint32_t s_occ;
+  // kJEasy: slot -> bucket of its live ID (valid where s_used is set), rows not found,
+  // block totals {live | occupied buckets at load, found | not-found rows}, found span
+  __shared__ uint16_t s_bkt[kEasy ? kSmallWords * 32 : 1];
+  __shared__ uint32_t s_pend[kEasy ? kPendWords : 1];
+  __shared__ uint32_t s_tot[2], s_flo, s_fhi;
 
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
   if (n >= a.n_nodes) return;
@@ -500,6 +528,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
     if (tid == 0) s_occ = 0u;
+    if constexpr (kEasy) {
+      if (tid < kPendWords) s_pend[tid] = 0u;
+      if (tid == 0) {
+        s_tot[0] = 0u;
+        s_tot[1] = 0u;
+        s_flo = 0xffffffffu;
+        s_fhi = 0u;
+      }
+    }
     if constexpr (k6) {
       if (tid * kPer < H) {
         __builtin_memcpy(s_ent + tid * kPer, ev, sizeof(ev));
@@ -521,7 +558,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // ---- 2: held slots and the occupancy, from this lane's buckets still in registers;
   //         lookups ---------------------------------------------------------------------
   {
-    uint32_t occ = 0;
+    uint32_t occ = 0, live = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (bucket_of(j) >= H) break;
@@ -533,13 +570,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         sl = sv[j];
       else
         sl = static_cast<uint32_t>(ev[j]);
-      if (sl < S) atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
+      if (sl < S) {
+        atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
+        if constexpr (kEasy) {
+          s_bkt[sl] = static_cast<uint16_t>(bucket_of(j));
+          ++live;
+        }
+      }
     }
-    occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
-    if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
+    if constexpr (kEasy) {  // both counts <= 4096: one packed sum
+      occ = wave_sum(occ | (live << 16));
+      if ((tid & 63) == 0 && occ) atomicAdd(&s_tot[0], occ);
+    } else {
+      occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
+      if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
+    }
   }
   uint32_t mine = 0;   // new rows of this lane
   uint32_t found = 0;  // kSeenNR: rows of this lane that found their ID
+  uint32_t pm = 0;     // kJEasy: bit j = row j of this lane not found
   if constexpr (kLock) {
     // every row of the lane probes in lock-step: unconditional LDS reads per depth
     uint32_t pb[kRpl];
@@ -607,6 +656,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       if (sj == 3u) {
         res[j] = kPending;
         ++mine;
+        pm |= 1u << j;
       } else if (sj == 2u) {
         const uint32_t sl = lslot(pb[j]);
         if (sl >= S) continue;
@@ -618,7 +668,38 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
           raise(kErrKey);
           continue;
         }
+        if constexpr (kEasy) ++found;
         res[j] = s0 + sl;
+      }
+    }
+    if constexpr (kEasy) {  // block totals and the found rows' span for the decision below
+      if (pm) {  // this lane's rows not found: <= 2 words of the row bitmap
+        uint32_t base = tid * kRpl;
+        asm volatile("" : "+v"(base));  // computed here, not hoisted above the probe loop
+        const uint32_t w0 = base >> 5, o = base & 31u;
+        atomicOr(&s_pend[w0], pm << o);
+        if (o + kRpl > 32u) atomicOr(&s_pend[w0 + 1], pm >> (32u - o));
+      }
+      uint32_t lo = 0xffffffffu, hi = 0u;
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        if (res[j] < kPending) {
+          lo = min(lo, res[j]);
+          hi = max(hi, res[j]);
+        }
+      }
+      const uint32_t fp = wave_sum(mine | (found << 16));  // each <= 3072
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
+        hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
+      }
+      if ((tid & 63) == 0) {
+        if (fp) atomicAdd(&s_tot[1], fp);
+        if (lo <= hi) {
+          atomicMin(&s_flo, lo);
+          atomicMax(&s_fhi, hi);
+        }
       }
     }
   } else {
@@ -653,6 +734,170 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   }
   jbar<V>();
   if (a.stop_after == 2u) return;  // timing ablation
+
+  uint32_t occ_load = 0;  // kJEasy: buckets not empty at load (the full path's rebuild test)
+  if constexpr (kEasy) {
+    const uint32_t t0 = s_tot[0], t1 = s_tot[1];
+    const uint32_t live = t0 >> 16, found_t = t1 >> 16, pend_t = t1 & 0xffffu;
+    occ_load = t0 & 0xffffu;
+    // block-uniform: the counts say the tail fits one wave; wave 0 re-derives every
+    // count from the bitmaps, and a range check still guards each slot it hands out
+    const uint32_t term_e = live >= found_t ? live - found_t : 0u, free_e = S >= live ? S - live : 0u;
+    const bool easy = a.stop_after == 0u && live >= found_t && pend_t <= kNewCap &&
+                      pend_t <= free_e + (a.reuse ? term_e : 0u) && (occ_load + pend_t) * 4 <= H * 3;
+    if (easy) {
+      uint32_t *__restrict__ out = a.out_slot + v.r0;
+      // the found rows' (and error rows') slot words, by their own lanes; wave 0 writes
+      // the new rows' below
+      if (kVec && mine == 0 && tid * kRpl + kRpl <= R) {
+        __builtin_memcpy(out + tid * kRpl, res, sizeof(res));
+      } else {
+#pragma unroll
+        for (int j = 0; j < kRpl; ++j)
+          if (tid * kRpl + j < R && res[j] != kPending) out[tid * kRpl + j] = res[j];
+      }
+      if (tid >= 64) {
+        if (errs) atomicOr(a.err, errs);
+        return;
+      }
+      // ---- wave 0: terminated list, free slots, new rows, inserts, write-back --------
+      const uint32_t lane = tid;
+      uint32_t tmw[2], fmw[2], tpre[2], fpre[2], pk[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = lane + 64u * i;
+        tmw[i] = 0u;
+        fmw[i] = 0u;
+        if (w < W) {
+          const uint32_t used = s_used[w], seen = s_seen[w];
+          const uint32_t valid = (w + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
+          fmw[i] = ~used & valid;
+          tmw[i] = used & ~seen & valid;
+        }
+        pk[i] = (static_cast<uint32_t>(__popc(fmw[i])) << 16) | static_cast<uint32_t>(__popc(tmw[i]));
+      }
+      uint32_t base = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {  // exclusive prefixes over the words in slot order
+        const uint32_t inc = wave_scan_dpp(pk[i], 0u, DppAdd{});
+        const uint32_t ex = base + inc - pk[i];
+        tpre[i] = ex & 0xffffu;
+        fpre[i] = ex >> 16;
+        base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+      }
+      const uint32_t n_term = base & 0xffffu, total_free = base >> 16;
+      if (lane == 0) a.term_count[n] = n_term;
+      const uint32_t t_first = a.reuse ? n_term : 0u, n_avail = total_free + t_first;
+      const uint32_t want = min(pend_t, n_avail);  // <= kNewCap
+      // terminated IDs, ascending by slot, and their tombstones; with the reuse policy
+      // their slots head the list of slots handed out
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = lane + 64u * i;
+        uint32_t rank = tpre[i];
+        for (uint32_t tm = tmw[i]; tm; tm &= tm - 1, ++rank) {
+          const uint32_t sl = w * 32 + static_cast<uint32_t>(__builtin_ctz(tm));
+          const uint32_t b = s_bkt[sl];
+          a.term_key[s0 + rank] = static_cast<uint64_t>(L.key(b));
+          a.term_slot[s0 + rank] = s0 + sl;
+          if (a.reuse && rank < want) s_free[rank] = static_cast<uint16_t>(sl);
+          L.tomb(b);
+          atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+        }
+        uint32_t p = t_first + fpre[i];
+        for (uint32_t fm = fmw[i]; fm && p < want; fm &= fm - 1, ++p)
+          s_free[p] = static_cast<uint16_t>(w * 32 + __builtin_ctz(fm));
+      }
+      // rows not found, in row order: the q-th takes s_free[q]
+      uint32_t pw[2], ppre[2];
+      base = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = lane + 64u * i;
+        pw[i] = w < kPendWords ? s_pend[w] : 0u;
+        const uint32_t c = static_cast<uint32_t>(__popc(pw[i]));
+        const uint32_t inc = wave_scan_dpp(c, 0u, DppAdd{});
+        ppre[i] = base + inc - c;
+        base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+      }
+      const uint32_t n_new = base;  // == pend_t
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = lane + 64u * i;
+        uint32_t q = ppre[i];
+        for (uint32_t m = pw[i]; m; m &= m - 1, ++q)
+          if (q < kNewCap) s_newkey[q] = static_cast<K>(w * 32 + __builtin_ctz(m));  // the row, for now
+      }
+      wave_lds_sync();
+      uint32_t lo = s_flo, hi = s_fhi;
+      for (uint32_t q = lane; q < n_new && q < kNewCap; q += 64) {
+        const uint32_t r = static_cast<uint32_t>(s_newkey[q]);
+        if (q >= n_avail) {  // more new IDs than free slots: the block-wide path's error
+          errs |= kErrRange;
+          out[r] = kInvalid;
+          continue;
+        }
+        const K k = keys[r];
+        const uint32_t sl = s_free[q];
+        // claim the first empty or tombstone bucket on k's path; meeting k itself
+        // there = a new ID given twice in the node (as the block-wide step 6)
+        uint32_t b = bucket(k, v.shift), got = ~0u;
+        for (uint32_t p = 0; p < H;) {
+          const auto raw = L.raw(b);
+          const K kk = static_cast<K>(T::key_of(raw));
+          if (kk == k) {
+            got = ~1u;
+            break;
+          }
+          if (kk == T::kEmpty || kk == T::kTomb) {
+            if (L.claim(b, raw, k, sl)) {
+              got = b;
+              break;
+            }
+            continue;  // another lane claimed it: look at it again
+          }
+          ++p;
+          b = (b + 1) & hmask;
+        }
+        if (got >= ~1u) {
+          errs |= kErrKey;
+          out[r] = kInvalid;
+          continue;
+        }
+        atomicOr(&s_dirty[got >> 5], 1u << (got & 31));
+        out[r] = (s0 + sl) | KACC_SLOT_NEW;
+        lo = min(lo, s0 + sl);
+        hi = max(hi, s0 + sl);
+      }
+      wave_lds_sync();
+      // the changed buckets back to the node's table
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = lane + 64u * i;
+        if (w >= H / 32) break;
+        for (uint32_t d = s_dirty[w]; d; d &= d - 1) {
+          const uint32_t b = w * 32 + __builtin_ctz(d);
+          if constexpr (kSplit) {
+            G.k[b] = s_ent[b];
+            G.s[b] = s_slot[b];
+          } else {
+            G.e[b] = s_ent[b];
+          }
+        }
+      }
+      if (a.out_span) {
+        lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
+        hi = wave_reduce_dpp(hi, 0u, DppMax{});
+        if (lane == 0) {
+          const bool none = lo > hi;
+          a.out_span[2 * n] = none ? 1u : lo;
+          a.out_span[2 * n + 1] = none ? 0u : hi;
+        }
+      }
+      if (errs) atomicOr(a.err, errs);
+      return;
+    }
+  }
 
   // ---- 3: per-word free / terminated bits and their prefixes -------------------------
   uint32_t packed = 0;
@@ -848,7 +1093,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // s_occ: the buckets not empty at load (step 2) + inserts into empty buckets (step 6;
   // tombstones of step 4 keep their buckets occupied) — every write of s_occ is
   // behind step 6's barriers
-  const bool rebuild = s_occ * 4 > H * 3;  // tombstones crowd the table
+  // kJEasy: the bound the one-wave test uses (load occupancy + inserts), so a node that
+  // missed it for a crowded table leaves here rebuilt and takes the one-wave tail again
+  const bool rebuild = kEasy ? (occ_load + n_ins) * 4 > H * 3 : s_occ * 4 > H * 3;  // tombstones crowd the table
   if (rebuild) {
     for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
     jbar<V>();
@@ -1152,7 +1399,8 @@ namespace {
 constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
                         kacc::join::kJInsDup | kacc::join::kJScan2;
 constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
-constexpr int kJoinDefault = kJoinGroup;
+constexpr int kJoinEasy = kJoinR2 | kacc::join::kJ6B | kacc::join::kJVec | kacc::join::kJGroup | kacc::join::kJEasy;
+constexpr int kJoinDefault = kJoinEasy;
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
 int launched_variant(int v) {
@@ -1162,7 +1410,9 @@ int launched_variant(int v) {
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR:
     case kJoinR2 | kacc::join::kJSeenNR | kacc::join::kJVec:
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
+    case kJoinGroup:
     case kJoinGroup | kacc::join::kJDpp:
+    case kJoinEasy:
       return v;
     default: return kJoinDefault;
   }
@@ -1350,6 +1600,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
         hipLaunchKernelGGL((join_small<K, kJoinR2 | kJ6B | kJSeenNR | kJVec>), grid, block, 0, st, a);
         break;
       case kJoinGroup | kJDpp: hipLaunchKernelGGL((join_small<K, kJoinGroup | kJDpp>), grid, block, 0, st, a); break;
+      case kJoinGroup: hipLaunchKernelGGL((join_small<K, kJoinGroup>), grid, block, 0, st, a); break;
       default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
     }
   };

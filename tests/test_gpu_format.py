@@ -278,3 +278,155 @@ def test_format_derived_process_power():
                    for r in range(rows) for j in range(2))
     assert text == want
     acc.close()
+
+
+def _parse_exposition(text):
+    """Sample lines of the text format -> [(name, {label: value}, float)] (label values
+    unescaped: \\\\, \\" and \\n, expfmt's escapes)."""
+    out = []
+    for line in text.splitlines():
+        name, rest = line.split("{", 1)
+        labels, i = {}, 0
+        while rest[i] != "}":
+            eq = rest.index("=", i)
+            key = rest[i:eq]
+            assert rest[eq + 1] == '"', line
+            j, val = eq + 2, []
+            while rest[j] != '"':
+                if rest[j] == "\\":
+                    val.append({"\\": "\\", '"': '"', "n": "\n"}[rest[j + 1]])
+                    j += 2
+                else:
+                    val.append(rest[j])
+                    j += 1
+            labels[key] = "".join(val)
+            i = j + 1
+            if rest[i] == ",":
+                i += 1
+        assert rest[i + 1] == " ", line
+        out.append((name, labels, float(rest[i + 2:])))
+    return out
+
+
+def test_format_collector_fixture_snapshot():
+    """The reference exporter test's snapshot (power_collector_test.go:184-272, transcribed in
+    tests/golden/collector_snapshot.json) held in the engine's tables and written by the
+    device: kacc_format_lines for the node families (one call per zone, whose path label sorts
+    before zone) and the four workload families, kacc_format_values for the usage ratio.  The
+    text is parsed back and checked as the reference test checks its registry: the 16 family
+    names (:307-328), the node joules / watts / active / idle values per zone path and the zone
+    names and paths (:342-418), and each workload family's labels and value (:437-483).
+    kepler_process_cpu_seconds_total is CPUTotalTime from the Go informer (not an engine
+    table): its line is the Go side's, written here with oracle/gofmt.  Every device line is
+    also byte-compared with oracle/gofmt.sample_line."""
+    import json
+    import os
+
+    from kepler_amd.torch_batch import current_stream_handle
+    from oracle.gofmt import joules, label_pairs, sample_line, watts
+
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "collector_snapshot.json")))
+    node_name, zones, nd = fx["node_name"], fx["zones"], fx["node"]
+    Z = len(zones)
+    acc = accel.Accel(Z, nodes=1, proc_slots=1, ctr_slots=1, vm_slots=1, pod_slots=1)
+    # the node x zone tables; activeEnergy and ProcessTotalCPUTimeDelta pass the derive guard
+    # (process.go:124) and ActivePower is the snapshot's, so ratio x ActivePower = the usage's power
+    acc.upload("node_energy_total", np.array(nd["energy_total"], dtype=np.uint64))
+    acc.upload("node_active_total", np.array(nd["active_energy_total"], dtype=np.uint64))
+    acc.upload("node_idle_total", np.array(nd["idle_energy_total"], dtype=np.uint64))
+    acc.upload("node_active_energy", np.array(nd["active_energy_total"], dtype=np.uint64))
+    acc.upload("node_power", np.array(nd["power"], dtype=np.float64))
+    acc.upload("node_active_power", np.array(nd["active_power"], dtype=np.float64))
+    acc.upload("node_idle_power", np.array(nd["idle_power"], dtype=np.float64))
+    acc.upload("node_usage_ratio", np.array([nd["usage_ratio"]], dtype=np.float64))
+    acc.upload("node_cpu_delta", np.array([1.0]))
+    zi = {z["name"]: i for i, z in enumerate(zones)}
+    wl = fx["workloads"]
+    for kind in ("proc", "ctr", "vm", "pod"):
+        u = wl[{"proc": "process", "ctr": "container", "vm": "vm", "pod": "pod"}[kind]]["usage"]
+        e = np.zeros(Z, dtype=np.uint64)
+        e[zi[u["zone"]]] = u["energy_total"]
+        acc.upload(f"{kind}_energy", e)
+        if kind == "pod":  # stored
+            p = np.zeros(Z)
+            p[zi[u["zone"]]] = u["power"]
+            acc.upload("pod_power", p)
+        else:  # derived: ratio x the node's ActivePower of the zone
+            acc.upload(f"{kind}_ratio", np.array([u["power"] / nd["active_power"][zi[u["zone"]]]]))
+            acc.upload(f"{kind}_node", np.array([0], dtype=np.uint32))
+    s = current_stream_handle()
+
+    def lines(table, metric, label_text, zone_names, zone_order):
+        d_labels = torch.from_numpy(np.frombuffer(label_text.encode(), np.uint8).copy()).cuda()
+        d_loff = torch.tensor([0, len(label_text.encode())], dtype=torch.int64, device="cuda")
+        d_line_off = torch.zeros(len(zone_names) + 1, dtype=torch.int64, device="cuda")
+        args = (table, metric, 0, 1, zone_names, d_labels.data_ptr(), d_loff.data_ptr(), d_line_off.data_ptr())
+        total = acc.format_lines(*args, zone_order=zone_order, stream=s)
+        out = torch.zeros(total, dtype=torch.uint8, device="cuda")
+        acc.format_lines(*args, out_ptr=out.data_ptr(), out_cap=total, zone_order=zone_order, stream=s)
+        acc.sync(s)
+        return bytes(out.cpu().numpy()).decode()
+
+    text, want = [], []
+    node_tables = [("kepler_node_cpu_joules_total", "node_energy_total"), ("kepler_node_cpu_watts", "node_power"),
+                   ("kepler_node_cpu_active_joules_total", "node_active_total"),
+                   ("kepler_node_cpu_idle_joules_total", "node_idle_total"),
+                   ("kepler_node_cpu_active_watts", "node_active_power"),
+                   ("kepler_node_cpu_idle_watts", "node_idle_power")]
+    for metric, table in node_tables:  # labels {zone, path} + node_name (power_collector.go:111-121)
+        for z, zone in enumerate(zones):
+            lab = label_pairs([("node_name", node_name), ("path", zone["path"])])
+            text.append(lines(table, metric, lab, [zone["name"]], [z]))
+            v = nd[table.replace("node_", "").replace("active_total", "active_energy_total")
+                   .replace("idle_total", "idle_energy_total")][z]
+            want.append(sample_line(metric, lab, zone["name"], joules(int(v)) if "joules" in metric else watts(v)))
+    # usage ratio: no zone label (power_collector.go:123-126); the value from the device
+    d_out = torch.zeros(W, dtype=torch.uint8, device="cuda")
+    d_len = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    acc.format_values("node_usage_ratio", 0, 1, d_out.data_ptr(), d_len.data_ptr(), s)
+    acc.sync(s)
+    ratio_text = bytes(d_out.cpu().numpy()[: int(d_len.item())]).decode()
+    assert ratio_text == write_float(nd["usage_ratio"])
+    text.append(f'kepler_node_cpu_usage_ratio{{node_name="{node_name}"}} {ratio_text}\n')
+    want.append(text[-1])
+    p, c, v, q = wl["process"], wl["container"], wl["vm"], wl["pod"]
+    fams = [  # label sets of power_collector.go:128-139 (state "running": :226-241), zone spliced last
+        ("proc", "kepler_process_cpu", [("pid", p["pid"]), ("comm", p["comm"]), ("exe", p["exe"]),
+                                        ("type", p["type"]), ("state", "running"), ("container_id", p["container_id"]),
+                                        ("vm_id", p["vm_id"]), ("node_name", node_name)], p["usage"]),
+        ("ctr", "kepler_container_cpu", [("container_id", c["id"]), ("container_name", c["name"]),
+                                         ("runtime", c["runtime"]), ("state", "running"), ("pod_id", c["pod_id"]),
+                                         ("node_name", node_name)], c["usage"]),
+        ("vm", "kepler_vm_cpu", [("vm_id", v["id"]), ("vm_name", v["name"]), ("hypervisor", v["hypervisor"]),
+                                 ("state", "running"), ("node_name", node_name)], v["usage"]),
+        ("pod", "kepler_pod_cpu", [("pod_id", q["id"]), ("pod_name", q["name"]), ("pod_namespace", q["namespace"]),
+                                   ("state", "running"), ("node_name", node_name)], q["usage"]),
+    ]
+    for kind, prefix, pairs, u in fams:
+        lab = label_pairs(pairs)
+        for suffix, table, conv in (("_joules_total", f"{kind}_energy", lambda x: joules(int(x))),
+                                    ("_watts", f"{kind}_power", watts)):
+            text.append(lines(table, prefix + suffix, lab, [u["zone"]], [zi[u["zone"]]]))
+            want.append(sample_line(prefix + suffix, lab, u["zone"],
+                                    conv(u["energy_total"] if suffix == "_joules_total" else u["power"])))
+    # the Go side's line (CPUTotalTime is the informer's, power_collector.go:315-321)
+    secs = label_pairs([("pid", p["pid"]), ("comm", p["comm"]), ("exe", p["exe"]), ("type", p["type"]),
+                        ("container_id", p["container_id"]), ("vm_id", p["vm_id"]), ("node_name", node_name)])
+    text.append(f"kepler_process_cpu_seconds_total{{{secs}}} {write_float(p['cpu_total_time'])}\n")
+    want.append(text[-1])
+    assert "".join(text) == "".join(want)  # byte-exact against the restated expfmt
+    samples = _parse_exposition("".join(text))
+    assert sorted({n for n, _, _ in samples}) == sorted(fx["expected_metric_names"])  # :307-328
+    node_js = [(lb, val) for n, lb, val in samples if n == "kepler_node_cpu_joules_total"]
+    assert sorted({lb["zone"] for lb, _ in node_js}) == sorted(fx["expected_zone_names"])  # :419-432
+    assert sorted({lb["path"] for lb, _ in node_js}) == sorted(fx["expected_zone_paths"])
+    for chk in fx["node_checks"]:  # :342-418
+        got = [val for n, lb, val in samples if n == chk["metric"] and lb.get("path") == chk["path"]]
+        assert got == [chk["value"]], chk
+        assert all(lb["node_name"] == node_name for n, lb, _ in samples if n == chk["metric"])
+    for chk in fx["label_checks"]:  # :437-483
+        for metric, value in zip(chk["metrics"], chk["values"]):
+            hits = [val for n, lb, val in samples
+                    if n == metric and all(lb.get(k) == x for k, x in chk["labels"].items())]
+            assert hits == [value], (metric, chk["labels"], hits)
+    acc.close()

@@ -117,6 +117,40 @@ def test_join_bit_exact(name, sizes, churn, kind, policy):
         assert term == want_term, f"interval {it}"
 
 
+@pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
+@pytest.mark.parametrize("churn", [0.02, 0.1, 0.3])
+def test_join_long_churn_bit_exact(churn, policy):
+    """30 intervals of churn, bit-exact every interval: at 2-10 % the small nodes take the
+    one-wave tail (kJEasy) until tombstones crowd their tables, then one block-wide
+    interval rebuilds them and the tail resumes; at 30 % the 2000-row nodes have more
+    than 512 new rows per interval (block-wide path) and the small ones stay on the tail.
+    Read errors skip nodes (their tables unchanged) every few intervals."""
+    sizes = [2000, 2000, 1500, 300, 40, 0, 2700, 5, 2400, 64]
+    row_off = np.r_[0, np.cumsum(sizes)].astype(np.uint32)
+    # room for the held policy: rows + this interval's terminated (+ a skipped interval's)
+    # slots; a 2000-row node stays on a 4096-bucket (LDS) table, 2400 / 2700 go global
+    slot_off = np.r_[0, np.cumsum([int(s * 1.35) + 8 for s in sizes])].astype(np.uint32)
+    acc = accel.Accel(1, **caps_for(slot_off))
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, slot_off, policy)
+    ora = OracleSlotMap(slot_off, policy)
+    sim = fleet.KeyedChurn(row_off, seed=11, churn=churn, kind="proc")
+    rng = np.random.default_rng(5)
+    for it in range(30):
+        keys = sim.next_keys()
+        status = None
+        if it % 4 == 3 and churn <= 0.1:
+            status = np.where(rng.random(len(sizes)) < 0.3, accel.KACC_NODE_READ_ERROR, 0).astype(np.uint32)
+        rc, want, tk, ts, cnt = ora.join(row_off, keys, status)
+        assert rc == 0
+        want_term = ora.terminated(tk, ts, cnt)
+        got, term = gpu.join(row_off, keys, status)
+        if status is not None:
+            keep = np.repeat(status == 0, np.diff(row_off.astype(np.int64)))
+            got, want = got[keep], want[keep]
+        np.testing.assert_array_equal(got, want, err_msg=f"interval {it}")
+        assert term == want_term, f"interval {it}"
+
+
 def test_join_errors_raise_erange():
     slot_off = np.array([0, 8, 10], dtype=np.uint32)
     acc = accel.Accel(1, **caps_for(slot_off))
