@@ -124,8 +124,9 @@ struct kacc_slotmap {
   uint64_t *d_hoff = nullptr;
   bool has_big = false;         // some node's table exceeds the LDS size
   uint32_t policy = 0;          // KACC_JOIN_* bits (kacc_slotmap_set_policy)
-  bool fmt6 = false;            // PID small tables in 6-B buckets, fixed at reset (the join
-                                // variant launched then); a join in the other format fails
+  int fmt = 0;                  // PID small-table format, fixed at reset (the join variant
+                                // launched then): 0 8-B buckets, 1 6-B buckets, 2 slot-keyed
+                                // (kJSK); a join in another format fails
   uint64_t *d_ent = nullptr;    // packed entries (PIDs) or keys (64-bit IDs)
   uint32_t *d_slots = nullptr;  // 64-bit IDs only
 };

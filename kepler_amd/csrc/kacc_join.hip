@@ -297,30 +297,40 @@ constexpr int kJSeenNR = 64;   // seen marks without return; duplicates found by
 constexpr int kJVec = 128;     // a lane's keys loaded / slot words stored as vectors
 constexpr int kJGroup = 256;   // kJ6B lookups read four buckets per LDS read
 constexpr int kJDpp = 1024;    // block scans by DPP moves instead of LDS permutes
-// Steady-state nodes finish in ONE wave (round 6): after the lookups' barrier a node whose
-// churn fits (new rows <= kNewCap and the free slots, no rebuild due) has its found rows'
-// slot words stored by their own lanes, and waves 1-7 end; wave 0 alone lists the
-// terminated IDs, hands out the free slots, inserts the new IDs and writes the changed
-// buckets back — no block scan, no further barrier.  Any other node (first interval,
-// mass churn, a rebuild, a range error) takes the block-wide steps 3-7 unchanged.  The
-// held-slot marks carry each slot's bucket (s_bkt), so the terminated IDs are found from
-// the bitmaps without a pass over the table; an ID found twice is caught by the seen
-// mark's return value (not by counting), so the decision needs no step-3 scan.
-constexpr int kJEasy = 2048;
-constexpr uint32_t kPendWords = (kSmallRows + 31) / 32;  // rows-not-found bitmap (kJEasy)
+constexpr uint32_t kPendWords = (kSmallRows + 31) / 32;  // rows-not-found bitmap (kJLean)
+// The block-wide tail without its table pass (round 6): step 3's word prefixes come from
+// wave 0 (two DPP scans over the slot bitmaps, two over the rows-not-found bitmap), a new
+// row's rank is its row's position in that bitmap, and step 4 lists the terminated IDs
+// from the terminated bits through the held slots' buckets (s_bkt) instead of every lane
+// walking the node's whole table; the other steps are join_small's.
+constexpr int kJLean = 8192;
+// Two-choice cuckoo placement of the 6-B PID table (round 6): a key lives in one of the
+// 4-bucket groups ck_g1(k) / ck_g2(k), so a lookup reads exactly those two 16-B groups —
+// no probe loop, whose lock-step depth is the deepest of a wave's 384 rows — and a
+// terminated key's bucket is simply emptied (no tombstones, no rebuild).  New keys claim
+// an empty bucket of their two groups (CAS); the rare key whose groups are both full is
+// placed by lane 0 alone, moving keys to their other group (cuckoo kicks).  At most
+// 2730 live keys in 4096 buckets (load <= 2/3), far below 4-way 2-choice cuckoo's limit.
+constexpr int kJCuckoo = 16384;
+constexpr int kCkMaxKicks = 512;
+__device__ __forceinline__ uint32_t ck_g1(uint32_t k, uint32_t gs) { return (k * 0x9E3779B1u) >> gs; }
+__device__ __forceinline__ uint32_t ck_g2(uint32_t k, uint32_t gs) {
+  uint32_t x = k ^ (k >> 15);
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 12;
+  x *= 0x297A2D39u;
+  x ^= x >> 15;
+  const uint32_t g = x >> gs;
+  return g == ck_g1(k, gs) ? g ^ 1u : g;
+}
+// bit e: key word e of a group equals k
+__device__ __forceinline__ uint32_t ck_match(const uint4 &g, uint32_t k) {
+  return (g.x == k ? 1u : 0u) | (g.y == k ? 2u : 0u) | (g.z == k ? 4u : 0u) | (g.w == k ? 8u : 0u);
+}
 
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
-// LDS ordering among the lanes of ONE wave (kJEasy's wave-0 tail): a wave's LDS
-// instructions execute in order; the fences keep the compiler from moving an access
-// across the point and wait for the wave's own LDS operations.
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
@@ -414,9 +424,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   constexpr bool kLock = (V & kJLock) != 0, kErrReg = (V & kJErrReg) != 0, kInsDup = (V & kJInsDup) != 0;
   constexpr bool kScan2 = (V & kJScan2) != 0, kSeenNR = (V & kJSeenNR) != 0, kVec = (V & kJVec) != 0;
   constexpr bool kGroup = k6 && (V & kJGroup) != 0;
-  constexpr bool kEasy = (V & kJEasy) != 0;
-  static_assert(!kEasy || (!kSeenNR && kLock && kErrReg && kInsDup && kScan2),
-                "kJEasy builds on the lock-step lookups with returned seen marks");
+  constexpr bool kLean = (V & kJLean) != 0;
+  static_assert(!kLean || (kSeenNR && kLock && kErrReg && kInsDup && kScan2),
+                "kJLean builds on the lock-step lookups with counted duplicates");
+  constexpr bool kBkt = kLean;  // held slots' buckets and the rows-not-found bitmap
+  constexpr bool kCuckoo = k6 && kGroup && (V & kJCuckoo) != 0;  // PID tables only
+  static_assert(!kCuckoo || kLean, "kJCuckoo empties terminated buckets through kJLean's step 4");
   using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
   using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
   using SlotT = std::conditional_t<k6, uint16_t, uint32_t>;
@@ -433,11 +446,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   __shared__ uint32_t s_dirty[kLdsBuckets / 32];
   __shared__ uint32_t s_wave[2 * kThreads / 64], s_lo[kThreads / 64], s_hi[kThreads / 64];
   __shared__ uint32_t s_occ;
-  // kJEasy: slot -> bucket of its live ID (valid where s_used is set), rows not found,
-  // block totals {live | occupied buckets at load, found | not-found rows}, found span
-  __shared__ uint16_t s_bkt[kEasy ? kSmallWords * 32 : 1];
-  __shared__ uint32_t s_pend[kEasy ? kPendWords : 1];
-  __shared__ uint32_t s_tot[2], s_flo, s_fhi;
+  // kJLean: slot -> bucket of its live ID (valid where s_used is set), rows not found;
+  // block totals (found rows), the rows' span (kJCuckoo)
+  __shared__ uint16_t s_bkt[kBkt ? kSmallWords * 32 : 1];
+  __shared__ uint32_t s_pend[kBkt ? kPendWords : 1];
+  __shared__ uint32_t s_ppre[kLean ? kPendWords : 1];  // kJLean: rows not found before word w
+  __shared__ uint32_t s_ckkey[kCuckoo ? kNewCap : 1];    // kJCuckoo: keys left to kick in
+  __shared__ uint16_t s_ckrel[kCuckoo ? kNewCap : 1];
+  __shared__ uint32_t s_ckn, s_ckfail;
+  __shared__ uint32_t s_tot[1], s_flo, s_fhi;
 
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
   if (n >= a.n_nodes) return;
@@ -527,12 +544,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       if constexpr (kSeenNR) s_dup[i] = 0u;
     }
     for (uint32_t w = tid; w < kLdsBuckets / 32; w += kThreads) s_dirty[w] = 0u;
-    if (tid == 0) s_occ = 0u;
-    if constexpr (kEasy) {
+    if (tid == 0) {
+      s_occ = 0u;
+      s_ckn = 0u;
+      s_ckfail = 0u;
+    }
+    if constexpr (kBkt) {
       if (tid < kPendWords) s_pend[tid] = 0u;
       if (tid == 0) {
         s_tot[0] = 0u;
-        s_tot[1] = 0u;
         s_flo = 0xffffffffu;
         s_fhi = 0u;
       }
@@ -558,7 +578,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // ---- 2: held slots and the occupancy, from this lane's buckets still in registers;
   //         lookups ---------------------------------------------------------------------
   {
-    uint32_t occ = 0, live = 0;
+    uint32_t occ = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
       if (bucket_of(j) >= H) break;
@@ -572,23 +592,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         sl = static_cast<uint32_t>(ev[j]);
       if (sl < S) {
         atomicOr(&s_used[sl >> 5], 1u << (sl & 31));
-        if constexpr (kEasy) {
-          s_bkt[sl] = static_cast<uint16_t>(bucket_of(j));
-          ++live;
-        }
+        if constexpr (kBkt) s_bkt[sl] = static_cast<uint16_t>(bucket_of(j));
       }
     }
-    if constexpr (kEasy) {  // both counts <= 4096: one packed sum
-      occ = wave_sum(occ | (live << 16));
-      if ((tid & 63) == 0 && occ) atomicAdd(&s_tot[0], occ);
-    } else {
-      occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
-      if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
-    }
+    occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
+    if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
   }
   uint32_t mine = 0;   // new rows of this lane
   uint32_t found = 0;  // kSeenNR: rows of this lane that found their ID
-  uint32_t pm = 0;     // kJEasy: bit j = row j of this lane not found
+  uint32_t pm = 0;     // kJLean: bit j = row j of this lane not found
   if constexpr (kLock) {
     // every row of the lane probes in lock-step: unconditional LDS reads per depth
     uint32_t pb[kRpl];
@@ -605,7 +617,33 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       }
       state |= 1u << (2 * j);
     }
-    if constexpr (kGroup) {
+    if constexpr (kCuckoo) {
+      // the key's two groups; found in either or absent (three rows at a time)
+      const uint32_t gs = 32u - static_cast<uint32_t>(__builtin_ctz(H / 4));
+#pragma unroll
+      for (int h2 = 0; h2 < kRpl; h2 += kRpl / 2) {
+        uint4 ga[kRpl / 2], gb[kRpl / 2];
+        uint32_t g1[kRpl / 2], g2[kRpl / 2];
+#pragma unroll
+        for (int j = 0; j < kRpl / 2; ++j) {
+          const uint32_t k = static_cast<uint32_t>(key[h2 + j]);
+          g1[j] = ck_g1(k, gs);
+          g2[j] = ck_g2(k, gs);
+          ga[j] = *reinterpret_cast<const uint4 *>(s_ent + g1[j] * 4);
+          gb[j] = *reinterpret_cast<const uint4 *>(s_ent + g2[j] * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < kRpl / 2; ++j) {
+          const uint32_t k = static_cast<uint32_t>(key[h2 + j]);
+          const uint32_t m1 = ck_match(ga[j], k), m2 = ck_match(gb[j], k);
+          const uint32_t b = m1 ? g1[j] * 4 + __builtin_ctz(m1) : g2[j] * 4 + __builtin_ctz(m2 | 16u);
+          const bool act = ((state >> (2 * (h2 + j))) & 3u) == 1u;
+          const uint32_t nv = (m1 | m2) ? 2u : 3u;
+          state = act ? (state & ~(3u << (2 * (h2 + j)))) | (nv << (2 * (h2 + j))) : state;
+          pb[h2 + j] = b;
+        }
+      }
+    } else if constexpr (kGroup) {
       // four consecutive buckets per LDS read (16 B, aligned): the probe ends at the
       // first bucket at or after pb holding the key or empty (where linear probing
       // stops; tombstones are skipped); <= H / 4 + 1 groups cover the whole table
@@ -668,11 +706,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
           raise(kErrKey);
           continue;
         }
-        if constexpr (kEasy) ++found;
         res[j] = s0 + sl;
       }
     }
-    if constexpr (kEasy) {  // block totals and the found rows' span for the decision below
+    if constexpr (kBkt) {  // the rows not found (row bitmap) and the found rows' count
       if (pm) {  // this lane's rows not found: <= 2 words of the row bitmap
         uint32_t base = tid * kRpl;
         asm volatile("" : "+v"(base));  // computed here, not hoisted above the probe loop
@@ -680,27 +717,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         atomicOr(&s_pend[w0], pm << o);
         if (o + kRpl > 32u) atomicOr(&s_pend[w0 + 1], pm >> (32u - o));
       }
-      uint32_t lo = 0xffffffffu, hi = 0u;
-#pragma unroll
-      for (int j = 0; j < kRpl; ++j) {
-        if (res[j] < kPending) {
-          lo = min(lo, res[j]);
-          hi = max(hi, res[j]);
-        }
-      }
-      const uint32_t fp = wave_sum(mine | (found << 16));  // each <= 3072
-#pragma unroll
-      for (int d = 32; d >= 1; d >>= 1) {
-        lo = min(lo, static_cast<uint32_t>(__shfl_xor(static_cast<int>(lo), d, 64)));
-        hi = max(hi, static_cast<uint32_t>(__shfl_xor(static_cast<int>(hi), d, 64)));
-      }
-      if ((tid & 63) == 0) {
-        if (fp) atomicAdd(&s_tot[1], fp);
-        if (lo <= hi) {
-          atomicMin(&s_flo, lo);
-          atomicMax(&s_fhi, hi);
-        }
-      }
+      // the found rows (duplicates included) for step 3's counting check
+      const uint32_t f = wave_reduce_dpp(found, 0u, DppAdd{});
+      if ((tid & 63) == 0 && f) atomicAdd(&s_tot[0], f);
     }
   } else {
 #pragma unroll
@@ -735,173 +754,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   jbar<V>();
   if (a.stop_after == 2u) return;  // timing ablation
 
-  uint32_t occ_load = 0;  // kJEasy: buckets not empty at load (the full path's rebuild test)
-  if constexpr (kEasy) {
-    const uint32_t t0 = s_tot[0], t1 = s_tot[1];
-    const uint32_t live = t0 >> 16, found_t = t1 >> 16, pend_t = t1 & 0xffffu;
-    occ_load = t0 & 0xffffu;
-    // block-uniform: the counts say the tail fits one wave; wave 0 re-derives every
-    // count from the bitmaps, and a range check still guards each slot it hands out
-    const uint32_t term_e = live >= found_t ? live - found_t : 0u, free_e = S >= live ? S - live : 0u;
-    const bool easy = a.stop_after == 0u && live >= found_t && pend_t <= kNewCap &&
-                      pend_t <= free_e + (a.reuse ? term_e : 0u) && (occ_load + pend_t) * 4 <= H * 3;
-    if (easy) {
-      uint32_t *__restrict__ out = a.out_slot + v.r0;
-      // the found rows' (and error rows') slot words, by their own lanes; wave 0 writes
-      // the new rows' below
-      if (kVec && mine == 0 && tid * kRpl + kRpl <= R) {
-        __builtin_memcpy(out + tid * kRpl, res, sizeof(res));
-      } else {
-#pragma unroll
-        for (int j = 0; j < kRpl; ++j)
-          if (tid * kRpl + j < R && res[j] != kPending) out[tid * kRpl + j] = res[j];
-      }
-      if (tid >= 64) {
-        if (errs) atomicOr(a.err, errs);
-        return;
-      }
-      // ---- wave 0: terminated list, free slots, new rows, inserts, write-back --------
-      const uint32_t lane = tid;
-      uint32_t tmw[2], fmw[2], tpre[2], fpre[2], pk[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t w = lane + 64u * i;
-        tmw[i] = 0u;
-        fmw[i] = 0u;
-        if (w < W) {
-          const uint32_t used = s_used[w], seen = s_seen[w];
-          const uint32_t valid = (w + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
-          fmw[i] = ~used & valid;
-          tmw[i] = used & ~seen & valid;
-        }
-        pk[i] = (static_cast<uint32_t>(__popc(fmw[i])) << 16) | static_cast<uint32_t>(__popc(tmw[i]));
-      }
-      uint32_t base = 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {  // exclusive prefixes over the words in slot order
-        const uint32_t inc = wave_scan_dpp(pk[i], 0u, DppAdd{});
-        const uint32_t ex = base + inc - pk[i];
-        tpre[i] = ex & 0xffffu;
-        fpre[i] = ex >> 16;
-        base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
-      }
-      const uint32_t n_term = base & 0xffffu, total_free = base >> 16;
-      if (lane == 0) a.term_count[n] = n_term;
-      const uint32_t t_first = a.reuse ? n_term : 0u, n_avail = total_free + t_first;
-      const uint32_t want = min(pend_t, n_avail);  // <= kNewCap
-      // terminated IDs, ascending by slot, and their tombstones; with the reuse policy
-      // their slots head the list of slots handed out
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t w = lane + 64u * i;
-        uint32_t rank = tpre[i];
-        for (uint32_t tm = tmw[i]; tm; tm &= tm - 1, ++rank) {
-          const uint32_t sl = w * 32 + static_cast<uint32_t>(__builtin_ctz(tm));
-          const uint32_t b = s_bkt[sl];
-          a.term_key[s0 + rank] = static_cast<uint64_t>(L.key(b));
-          a.term_slot[s0 + rank] = s0 + sl;
-          if (a.reuse && rank < want) s_free[rank] = static_cast<uint16_t>(sl);
-          L.tomb(b);
-          atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
-        }
-        uint32_t p = t_first + fpre[i];
-        for (uint32_t fm = fmw[i]; fm && p < want; fm &= fm - 1, ++p)
-          s_free[p] = static_cast<uint16_t>(w * 32 + __builtin_ctz(fm));
-      }
-      // rows not found, in row order: the q-th takes s_free[q]
-      uint32_t pw[2], ppre[2];
-      base = 0;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t w = lane + 64u * i;
-        pw[i] = w < kPendWords ? s_pend[w] : 0u;
-        const uint32_t c = static_cast<uint32_t>(__popc(pw[i]));
-        const uint32_t inc = wave_scan_dpp(c, 0u, DppAdd{});
-        ppre[i] = base + inc - c;
-        base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
-      }
-      const uint32_t n_new = base;  // == pend_t
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t w = lane + 64u * i;
-        uint32_t q = ppre[i];
-        for (uint32_t m = pw[i]; m; m &= m - 1, ++q)
-          if (q < kNewCap) s_newkey[q] = static_cast<K>(w * 32 + __builtin_ctz(m));  // the row, for now
-      }
-      wave_lds_sync();
-      uint32_t lo = s_flo, hi = s_fhi;
-      for (uint32_t q = lane; q < n_new && q < kNewCap; q += 64) {
-        const uint32_t r = static_cast<uint32_t>(s_newkey[q]);
-        if (q >= n_avail) {  // more new IDs than free slots: the block-wide path's error
-          errs |= kErrRange;
-          out[r] = kInvalid;
-          continue;
-        }
-        const K k = keys[r];
-        const uint32_t sl = s_free[q];
-        // claim the first empty or tombstone bucket on k's path; meeting k itself
-        // there = a new ID given twice in the node (as the block-wide step 6)
-        uint32_t b = bucket(k, v.shift), got = ~0u;
-        for (uint32_t p = 0; p < H;) {
-          const auto raw = L.raw(b);
-          const K kk = static_cast<K>(T::key_of(raw));
-          if (kk == k) {
-            got = ~1u;
-            break;
-          }
-          if (kk == T::kEmpty || kk == T::kTomb) {
-            if (L.claim(b, raw, k, sl)) {
-              got = b;
-              break;
-            }
-            continue;  // another lane claimed it: look at it again
-          }
-          ++p;
-          b = (b + 1) & hmask;
-        }
-        if (got >= ~1u) {
-          errs |= kErrKey;
-          out[r] = kInvalid;
-          continue;
-        }
-        atomicOr(&s_dirty[got >> 5], 1u << (got & 31));
-        out[r] = (s0 + sl) | KACC_SLOT_NEW;
-        lo = min(lo, s0 + sl);
-        hi = max(hi, s0 + sl);
-      }
-      wave_lds_sync();
-      // the changed buckets back to the node's table
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t w = lane + 64u * i;
-        if (w >= H / 32) break;
-        for (uint32_t d = s_dirty[w]; d; d &= d - 1) {
-          const uint32_t b = w * 32 + __builtin_ctz(d);
-          if constexpr (kSplit) {
-            G.k[b] = s_ent[b];
-            G.s[b] = s_slot[b];
-          } else {
-            G.e[b] = s_ent[b];
-          }
-        }
-      }
-      if (a.out_span) {
-        lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
-        hi = wave_reduce_dpp(hi, 0u, DppMax{});
-        if (lane == 0) {
-          const bool none = lo > hi;
-          a.out_span[2 * n] = none ? 1u : lo;
-          a.out_span[2 * n + 1] = none ? 0u : hi;
-        }
-      }
-      if (errs) atomicOr(a.err, errs);
-      return;
-    }
-  }
-
   // ---- 3: per-word free / terminated bits and their prefixes -------------------------
   uint32_t packed = 0;
-  if (tid < W) {
+  if (!kLean && tid < W) {
     const uint32_t used = s_used[tid], seen = s_seen[tid];
     const uint32_t valid = (tid + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
     const uint32_t fm = ~used & valid, tm = used & ~seen & valid;
@@ -909,16 +764,57 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     s_tmask[tid] = tm;
     packed = (static_cast<uint32_t>(__popc(fm)) << 16) | static_cast<uint32_t>(__popc(tm));
   }
-  uint32_t ptot, ntot, pex, rank0;  // rank0: this lane's first new-row rank
+  uint32_t ptot, ntot, pex = 0, rank0;  // rank0: this lane's first new-row rank
   // kSeenNR: the found rows ride in the new-row channel's high half (<= 3072 each)
   const uint32_t chan = kSeenNR ? mine | (found << 16) : mine;
-  if constexpr (kScan2) {
+  if constexpr (kLean) {
+    // wave 0: the slot-bitmap words (lane, lane + 64) and their prefixes, the prefixes of
+    // the rows-not-found bitmap; everyone reads them after the barrier
+    if (tid < 64) {
+      uint32_t base = 0, pbase = 0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t w = tid + 64u * i;
+        uint32_t fm = 0, tm = 0;
+        if (w < W) {
+          const uint32_t used = s_used[w], seen = s_seen[w];
+          const uint32_t valid = (w + 1) * 32 <= S ? 0xffffffffu : ((1u << (S & 31)) - 1u);
+          fm = ~used & valid;
+          tm = used & ~seen & valid;
+          s_fmask[w] = fm;
+          s_tmask[w] = tm;
+        }
+        const uint32_t pk = (static_cast<uint32_t>(__popc(fm)) << 16) | static_cast<uint32_t>(__popc(tm));
+        const uint32_t inc = wave_scan_dpp(pk, 0u, DppAdd{});
+        if (w < W) s_wpre[w] = base + inc - pk;
+        base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+        const uint32_t c = w < kPendWords ? static_cast<uint32_t>(__popc(s_pend[w])) : 0u;
+        const uint32_t pinc = wave_scan_dpp(c, 0u, DppAdd{});
+        if (w < kPendWords) s_ppre[w] = pbase + pinc - c;
+        pbase += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pinc), 63));
+      }
+      if (tid == 0) {
+        s_wave[0] = base;
+        s_wave[1] = pbase;
+      }
+    }
+    jbar<V>();
+    ptot = s_wave[0];
+    ntot = s_wave[1] | (s_tot[0] << 16);
+    rank0 = 0;
+    if (pm) {  // rows not found before this lane's first row
+      uint32_t r = tid * kRpl;
+      asm volatile("" : "+v"(r));
+      const uint32_t w = r >> 5, below = (1u << (r & 31)) - 1u;
+      rank0 = s_ppre[w] + static_cast<uint32_t>(__popc(s_pend[w] & below));
+    }
+  } else if constexpr (kScan2) {
     block_scan2<V>(packed, chan, s_wave, pex, rank0, ptot, ntot);
   } else {
     pex = block_scan(packed, s_wave, ptot);
     rank0 = block_scan(chan, s_wave, ntot);
   }
-  if (tid < W) s_wpre[tid] = pex;
+  if (!kLean && tid < W) s_wpre[tid] = pex;
   const uint32_t total_free = ptot >> 16, n_term = ptot & 0xffffu, n_new = ntot & 0xffffu;
   if constexpr (kSeenNR) {
     rank0 &= 0xffffu;
@@ -940,11 +836,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // (slot order), then the free ones; otherwise terminated slots are held
   const uint32_t t_first = a.reuse ? n_term : 0u, n_avail = total_free + t_first;
   if (tid == 0) a.term_count[n] = n_term;
-  jbar<V>();
+  if constexpr (!kLean) jbar<V>();  // (kJLean: step 4's inputs were written before its barrier)
   if (a.stop_after == 3u) return;  // timing ablation
 
   // ---- 4: terminated list (slot order) + tombstones; the first free slots ------------
-  if (n_term) {
+  if (kLean && n_term && tid < W) {  // the word's terminated slots, their buckets from s_bkt
+    uint32_t rank = s_wpre[tid] & 0xffffu;
+    for (uint32_t tm = s_tmask[tid]; tm; tm &= tm - 1, ++rank) {
+      const uint32_t sl = tid * 32 + static_cast<uint32_t>(__builtin_ctz(tm));
+      const uint32_t b = s_bkt[sl], pos = s0 + rank;
+      a.term_key[pos] = static_cast<uint64_t>(L.key(b));
+      a.term_slot[pos] = s0 + sl;
+      if (a.reuse && rank < kNewCap) s_free[rank] = static_cast<uint16_t>(sl);
+      if constexpr (kCuckoo)
+        L.clear(b);  // no probe chain passes through a bucket: empty it
+      else
+        L.tomb(b);
+      atomicOr(&s_dirty[b >> 5], 1u << (b & 31));
+    }
+  } else if (!kLean && n_term) {
     for (uint32_t b = tid; b < H; b += kThreads) {
       if (!is_live<T>(L.raw(b))) continue;
       const uint32_t sl = lslot(b);
@@ -1030,7 +940,134 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     return ~0u;
   };
-  if (compact) {
+  if constexpr (kCuckoo) {
+    const uint32_t gs = 32u - static_cast<uint32_t>(__builtin_ctz(H / 4));
+    auto dirty = [&](uint32_t b) { atomicOr(&s_dirty[b >> 5], 1u << (b & 31)); };
+    // an empty bucket of k's two groups, claimed by CAS (~0u: both groups full)
+    auto ck_direct = [&](uint32_t k, uint32_t rel) -> uint32_t {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t g = t ? ck_g2(k, gs) : ck_g1(k, gs);
+        for (uint32_t e = 0; e < 4; ++e) {
+          const uint32_t b = g * 4 + e;
+          while (L.k[b] == T::kEmpty)
+            if (L.claim(b, T::kEmpty, k, rel)) return b;
+        }
+      }
+      return ~0u;
+    };
+    auto defer = [&](uint32_t k, uint32_t rel) {
+      const uint32_t d = atomicAdd(&s_ckn, 1u);
+      if (d < kNewCap) {
+        s_ckkey[d] = k;
+        s_ckrel[d] = static_cast<uint16_t>(rel);
+      } else {
+        atomicOr(&s_ckfail, 1u);
+      }
+    };
+    if (compact) {
+      for (uint32_t i = tid; i < n_ins; i += kThreads) {
+        const uint32_t k = static_cast<uint32_t>(s_newkey[i]), rel = s_free[i], b = ck_direct(k, rel);
+        if (b == ~0u) defer(k, rel);
+        else dirty(b);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        if (rk[j] == ~0u) continue;
+        const uint32_t k = static_cast<uint32_t>(key[j]), rel = (res[j] & KACC_SLOT_MASK) - s0;
+        const uint32_t b = ck_direct(k, rel);
+        if (b == ~0u) defer(k, rel);
+        else dirty(b);
+      }
+    }
+    jbar<V>();
+    if (s_ckn) {  // block-uniform: lane 0 alone places each key whose groups were full, by kicks
+      if (tid == 0) {
+      const uint32_t nd = min(s_ckn, kNewCap);
+      for (uint32_t d = 0; d < nd; ++d) {
+        uint32_t k = s_ckkey[d], rel = s_ckrel[d];
+        bool placed = false;
+        for (int kick = 0; kick < kCkMaxKicks && !placed; ++kick) {
+          const uint32_t ga = ck_g1(k, gs), gb = ck_g2(k, gs);
+          for (uint32_t e = 0; e < 8 && !placed; ++e) {
+            const uint32_t b = (e < 4 ? ga : gb) * 4 + (e & 3);
+            if (L.k[b] == T::kEmpty) {
+              L.k[b] = k;
+              L.s[b] = static_cast<uint16_t>(rel);
+              dirty(b);
+              placed = true;
+            }
+          }
+          if (placed) break;
+          // evict a key of one of the groups (alternating, rotating) to its other group
+          const uint32_t b = ((kick & 1) ? gb : ga) * 4 + ((kick >> 1) & 3);
+          const uint32_t vk = L.k[b], vr = L.s[b];
+          L.k[b] = k;
+          L.s[b] = static_cast<uint16_t>(rel);
+          dirty(b);
+          k = vk;
+          rel = vr;
+        }
+        if (!placed) s_ckfail = 1u;  // a homeless key: the call fails (not reached at load <= 2/3)
+      }
+      }
+      jbar<V>();
+    }
+    if (tid == 0 && s_ckfail) raise(kErrRange);
+    // an ID given twice: both entries sit in its two groups; the larger slot gives way
+    auto ck_dup = [&](uint32_t k, uint32_t rel) -> bool {
+      bool drop = false;
+      uint32_t mine_b = ~0u;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint32_t g = t ? ck_g2(k, gs) : ck_g1(k, gs);
+        const uint4 gv = *reinterpret_cast<const uint4 *>(s_ent + g * 4);
+        for (uint32_t m = ck_match(gv, k); m; m &= m - 1) {
+          const uint32_t b = g * 4 + __builtin_ctz(m), sl = L.slot(b);
+          if (sl == rel) mine_b = b;
+          else if (sl < rel) drop = true;
+        }
+      }
+      if (drop && mine_b != ~0u) L.clear(mine_b);
+      return drop || mine_b == ~0u;
+    };
+    if (compact) {  // one lane per new row (the few lanes of wave 0), then their owners
+      for (uint32_t i = tid; i < n_ins; i += kThreads)
+        if (ck_dup(static_cast<uint32_t>(s_newkey[i]), s_free[i])) s_newbad[i] = 1;
+      jbar<V>();
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j)
+        if (rk[j] != ~0u && s_newbad[rk[j]]) {
+          raise(kErrKey);
+          res[j] = kInvalid;
+        }
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j)
+        if (rk[j] != ~0u && ck_dup(static_cast<uint32_t>(key[j]), (res[j] & KACC_SLOT_MASK) - s0)) {
+          raise(kErrKey);
+          res[j] = kInvalid;
+        }
+    }
+    if (a.out_span) {  // the rows' final slots: the span rides on the barrier below
+      uint32_t lo = 0xffffffffu, hi = 0u;
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        if (res[j] != kInvalid) {
+          lo = min(lo, res[j] & KACC_SLOT_MASK);
+          hi = max(hi, res[j] & KACC_SLOT_MASK);
+        }
+      }
+      lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
+      hi = wave_reduce_dpp(hi, 0u, DppMax{});
+      if ((tid & 63) == 0 && lo <= hi) {
+        atomicMin(&s_flo, lo);
+        atomicMax(&s_fhi, hi);
+      }
+    }
+    jbar<V>();  // the dropped duplicates' buckets are empty before step 7 writes them back
+  } else if (compact) {
     for (uint32_t i = tid; i < n_ins; i += kThreads) {
       if constexpr (kInsDup) {
         const uint32_t b = insert_dup(s_newkey[i], s_free[i]);
@@ -1093,9 +1130,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   // s_occ: the buckets not empty at load (step 2) + inserts into empty buckets (step 6;
   // tombstones of step 4 keep their buckets occupied) — every write of s_occ is
   // behind step 6's barriers
-  // kJEasy: the bound the one-wave test uses (load occupancy + inserts), so a node that
-  // missed it for a crowded table leaves here rebuilt and takes the one-wave tail again
-  const bool rebuild = kEasy ? (occ_load + n_ins) * 4 > H * 3 : s_occ * 4 > H * 3;  // tombstones crowd the table
+  const bool rebuild = !kCuckoo && s_occ * 4 > H * 3;  // tombstones crowd the table (kJCuckoo has none)
   if (rebuild) {
     for (uint32_t b = tid; b < H; b += kThreads) L.clear(b);
     jbar<V>();
@@ -1144,7 +1179,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   if constexpr (kErrReg) {
     if (errs) atomicOr(a.err, errs);
   }
-  if (a.out_span) {
+  if (kCuckoo && a.out_span) {  // reduced before step 6's last barrier
+    if (tid == 0) {
+      const uint32_t flo = s_flo, fhi = s_fhi;
+      a.out_span[2 * n] = flo > fhi ? 1u : flo;
+      a.out_span[2 * n + 1] = flo > fhi ? 0u : fhi;
+    }
+  } else if (a.out_span) {
     if constexpr ((V & kJDpp) != 0) {
       lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
       hi = wave_reduce_dpp(hi, 0u, DppMax{});
@@ -1399,8 +1440,15 @@ namespace {
 constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::kJLdsBar |
                         kacc::join::kJInsDup | kacc::join::kJScan2;
 constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
-constexpr int kJoinEasy = kJoinR2 | kacc::join::kJ6B | kacc::join::kJVec | kacc::join::kJGroup | kacc::join::kJEasy;
-constexpr int kJoinDefault = kJoinEasy;
+constexpr int kJoinLean = kJoinGroup | kacc::join::kJLean;
+constexpr int kJoinCuckoo = kJoinLean | kacc::join::kJCuckoo;
+
+constexpr int kJoinDefault = kJoinCuckoo;  // production: PID tables (the u64-keyed kinds: kJoinLean)
+// the PID small-table format a variant works on (kacc_slotmap.fmt)
+int variant_fmt(int v) {
+  return (v & kacc::join::kJCuckoo) ? 3 : (v & kacc::join::kJ6B) ? 1 : 0;
+}
+const char *fmt_name(int f) { return f == 3 ? "6-B cuckoo" : f == 1 ? "6-B" : "8-B"; }
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
 int launched_variant(int v) {
@@ -1412,7 +1460,8 @@ int launched_variant(int v) {
     case kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec:
     case kJoinGroup:
     case kJoinGroup | kacc::join::kJDpp:
-    case kJoinEasy:
+    case kJoinLean:
+    case kJoinCuckoo:
       return v;
     default: return kJoinDefault;
   }
@@ -1496,7 +1545,7 @@ int kacc_slotmap_reset(kacc_slotmap *m) {
   const size_t nb = std::max<uint64_t>(m->buckets, 1);
   // the bucket format of the PID small tables follows the join variant in force now;
   // slot_join refuses a later launch in the other format (it would misread the table)
-  m->fmt6 = m->kind == KACC_KIND_PROC && (launched_variant(g_join_variant) & kacc::join::kJ6B) != 0;
+  m->fmt = m->kind == KACC_KIND_PROC ? variant_fmt(launched_variant(g_join_variant)) : 0;
   KACC_HIP(ctx, hipMemsetAsync(m->d_ent, 0xff, 8 * nb, ctx->stream));  // every bucket empty
   KACC_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return KACC_OK;
@@ -1573,12 +1622,13 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   const dim3 grid(m->n_nodes), block(kThreads);
   // the table format follows the variant: a map keeps the format of its reset
   const int var = launched_variant(g_join_variant);
-  a.fmt6 = m->kind == KACC_KIND_PROC && (var & kJ6B) ? 1u : 0u;
-  if ((a.fmt6 != 0) != m->fmt6)
+  const int fmt = m->kind == KACC_KIND_PROC ? variant_fmt(var) : 0;
+  a.fmt6 = fmt == 1 ? 1u : 0u;
+  if (fmt != m->fmt)
     return kacc_fail(ctx, KACC_EINVAL,
-                     "slot join: the join variant's table format (%s buckets) differs from the map's "
+                     "slot join: the join variant's table format (%s) differs from the map's "
                      "(%s, fixed at its last reset): reset the map first",
-                     a.fmt6 ? "6-B" : "8-B", m->fmt6 ? "6-B" : "8-B");
+                     fmt_name(fmt), fmt_name(m->fmt));
   auto small = [&](auto key) {
     using K = decltype(key);
     switch (var) {
@@ -1601,7 +1651,14 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
         break;
       case kJoinGroup | kJDpp: hipLaunchKernelGGL((join_small<K, kJoinGroup | kJDpp>), grid, block, 0, st, a); break;
       case kJoinGroup: hipLaunchKernelGGL((join_small<K, kJoinGroup>), grid, block, 0, st, a); break;
-      default: hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a); break;
+      case kJoinLean: hipLaunchKernelGGL((join_small<K, kJoinLean>), grid, block, 0, st, a); break;
+      case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
+      default:
+        if constexpr (sizeof(K) == 4)
+          hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a);
+        else  // kJCuckoo places 6-B PID tables only
+          hipLaunchKernelGGL((join_small<K, kJoinLean>), grid, block, 0, st, a);
+        break;
     }
   };
   if (m->kind == KACC_KIND_PROC) {
