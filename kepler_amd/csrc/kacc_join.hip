@@ -313,16 +313,21 @@ constexpr int kJLean = 8192;
 // 2730 live keys in 4096 buckets (load <= 2/3), far below 4-way 2-choice cuckoo's limit.
 constexpr int kJCuckoo = 16384;
 constexpr int kCkMaxKicks = 512;
-__device__ __forceinline__ uint32_t ck_g1(uint32_t k, uint32_t gs) { return (k * 0x9E3779B1u) >> gs; }
-__device__ __forceinline__ uint32_t ck_g2(uint32_t k, uint32_t gs) {
+// the key's two groups among G (>= 2): the high word of hash x G (a power-of-two G takes the
+// hash's top bits), the second moved off the first
+__device__ __forceinline__ uint32_t ck_g1(uint32_t k, uint32_t G) { return __umulhi(k * 0x9E3779B1u, G); }
+__device__ __forceinline__ uint32_t ck_g2(uint32_t k, uint32_t G) {
   uint32_t x = k ^ (k >> 15);
   x *= 0x2C1B3C6Du;
   x ^= x >> 12;
   x *= 0x297A2D39u;
   x ^= x >> 15;
-  const uint32_t g = x >> gs;
-  return g == ck_g1(k, gs) ? g ^ 1u : g;
+  const uint32_t g = __umulhi(x, G), g1 = ck_g1(k, G);
+  return g != g1 ? g : g1 + 1 == G ? 0u : g1 + 1;
 }
+// kJCkSmall: the cuckoo table fills only 4 ceil(3S / 8) of the node's H buckets (1.5 S: load
+// <= 2/3 as before, but of a table sized by the slots, not the next power of two)
+constexpr int kJCkSmall = 32768;
 // bit e: key word e of a group equals k
 __device__ __forceinline__ uint32_t ck_match(const uint4 &g, uint32_t k) {
   return (g.x == k ? 1u : 0u) | (g.y == k ? 2u : 0u) | (g.z == k ? 4u : 0u) | (g.w == k ? 8u : 0u);
@@ -429,6 +434,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
                 "kJLean builds on the lock-step lookups with counted duplicates");
   constexpr bool kBkt = kLean;  // held slots' buckets and the rows-not-found bitmap
   constexpr bool kCuckoo = k6 && kGroup && (V & kJCuckoo) != 0;  // PID tables only
+  constexpr bool kCkSmall = kCuckoo && (V & kJCkSmall) != 0;
   static_assert(!kCuckoo || kLean, "kJCuckoo empties terminated buckets through kJLean's step 4");
   using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
   using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
@@ -462,6 +468,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   if (!node_view<true>(a, n, v)) return;
   const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H, hmask = H - 1;
   const uint32_t W = (S + 31) / 32;
+  // kJCuckoo: the buckets in use (Hu <= H) and their 4-bucket groups
+  const uint32_t Hu = kCkSmall ? min(H, max(8u, 4 * ((3 * S + 7) / 8))) : H, CG = Hu / 4;
   if (R > kSmallRows) {  // more rows than the table's <= 2730 slots: ERANGE, map unchanged
     for (uint32_t r = tid; r < R; r += kThreads) a.out_slot[v.r0 + r] = kInvalid;
     if (tid == 0) {
@@ -522,7 +530,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   SlotT sv[kSplit ? kPer : 1];
   {
     if constexpr (k6) {
-      if (tid * kPer < H) {
+      if (tid * kPer < Hu) {
         __builtin_memcpy(ev, __builtin_assume_aligned(G.k + tid * kPer, 16), sizeof(ev));
         __builtin_memcpy(sv, __builtin_assume_aligned(G.s + tid * kPer, 16), sizeof(sv));
       }
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       }
     }
     if constexpr (k6) {
-      if (tid * kPer < H) {
+      if (tid * kPer < Hu) {
         __builtin_memcpy(s_ent + tid * kPer, ev, sizeof(ev));
         __builtin_memcpy(s_slot + tid * kPer, sv, sizeof(sv));
       }
@@ -581,7 +589,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     uint32_t occ = 0;
 #pragma unroll
     for (int j = 0; j < kPer; ++j) {
-      if (bucket_of(j) >= H) break;
+      if (bucket_of(j) >= Hu) break;
       const auto k = T::key_of(ev[j]);
       occ += k != T::kEmpty ? 1u : 0u;
       if (k == T::kEmpty || k == T::kTomb) continue;
@@ -619,7 +627,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     if constexpr (kCuckoo) {
       // the key's two groups; found in either or absent (three rows at a time)
-      const uint32_t gs = 32u - static_cast<uint32_t>(__builtin_ctz(H / 4));
 #pragma unroll
       for (int h2 = 0; h2 < kRpl; h2 += kRpl / 2) {
         uint4 ga[kRpl / 2], gb[kRpl / 2];
@@ -627,8 +634,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
 #pragma unroll
         for (int j = 0; j < kRpl / 2; ++j) {
           const uint32_t k = static_cast<uint32_t>(key[h2 + j]);
-          g1[j] = ck_g1(k, gs);
-          g2[j] = ck_g2(k, gs);
+          g1[j] = ck_g1(k, CG);
+          g2[j] = ck_g2(k, CG);
           ga[j] = *reinterpret_cast<const uint4 *>(s_ent + g1[j] * 4);
           gb[j] = *reinterpret_cast<const uint4 *>(s_ent + g2[j] * 4);
         }
@@ -913,6 +920,26 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     ++q;
   }
+  if constexpr (kCuckoo) {
+    // the span of the rows' slots, here with the slots just handed out (an ID given twice
+    // fails the call, whose outputs are then unspecified: a dropped row may widen it)
+    if (a.out_span) {
+      uint32_t lo = 0xffffffffu, hi = 0u;
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        if (res[j] != kInvalid) {
+          lo = min(lo, res[j] & KACC_SLOT_MASK);
+          hi = max(hi, res[j] & KACC_SLOT_MASK);
+        }
+      }
+      lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
+      hi = wave_reduce_dpp(hi, 0u, DppMax{});
+      if ((tid & 63) == 0 && lo <= hi) {
+        atomicMin(&s_flo, lo);
+        atomicMax(&s_fhi, hi);
+      }
+    }
+  }
   jbar<V>();
   if (a.stop_after == 5u) return;  // timing ablation
 
@@ -941,22 +968,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     return ~0u;
   };
   if constexpr (kCuckoo) {
-    const uint32_t gs = 32u - static_cast<uint32_t>(__builtin_ctz(H / 4));
     auto dirty = [&](uint32_t b) { atomicOr(&s_dirty[b >> 5], 1u << (b & 31)); };
-    // an empty bucket of k's two groups, claimed by CAS (~0u: both groups full)
-    auto ck_direct = [&](uint32_t k, uint32_t rel) -> uint32_t {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t g = t ? ck_g2(k, gs) : ck_g1(k, gs);
-        for (uint32_t e = 0; e < 4; ++e) {
-          const uint32_t b = g * 4 + e;
-          while (L.k[b] == T::kEmpty)
-            if (L.claim(b, T::kEmpty, k, rel)) return b;
-        }
+    const uint4 *const s_grp = reinterpret_cast<const uint4 *>(s_ent);
+    // an empty bucket of the emptier of k's two groups (both read at once), claimed by CAS;
+    // ~0u: both groups full (the serial kicks below), ~1u: k is already there — an ID given
+    // twice.  Filling the emptier group keeps the groups balanced, so a new key rarely finds
+    // both full.  Two rows of one ID inserting in ONE wave read the same groups in the same
+    // instruction, choose the same bucket and collide on it: the loser's retry finds the key
+    const auto ck_direct = [&](uint32_t k, uint32_t rel) -> uint32_t {
+      const uint32_t ga = ck_g1(k, CG), gb = ck_g2(k, CG);
+      for (int tries = 0; tries < 16; ++tries) {
+        const uint4 va = s_grp[ga], vb = s_grp[gb];
+        if (ck_match(va, k) | ck_match(vb, k)) return ~1u;
+        const uint32_t ea = ck_match(va, T::kEmpty), eb = ck_match(vb, T::kEmpty);
+        if (!(ea | eb)) return ~0u;
+        const bool use_a = __popc(ea) >= __popc(eb);
+        const uint32_t b = (use_a ? ga : gb) * 4 + __builtin_ctz(use_a ? ea : eb);
+        if (L.claim(b, T::kEmpty, k, rel)) return b;
       }
-      return ~0u;
+      return ~0u;  // lost the race 16 times: the kicks place it
     };
-    auto defer = [&](uint32_t k, uint32_t rel) {
+    const auto defer = [&](uint32_t k, uint32_t rel) {
       const uint32_t d = atomicAdd(&s_ckn, 1u);
       if (d < kNewCap) {
         s_ckkey[d] = k;
@@ -965,108 +997,99 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         atomicOr(&s_ckfail, 1u);
       }
     };
-    if (compact) {
-      for (uint32_t i = tid; i < n_ins; i += kThreads) {
-        const uint32_t k = static_cast<uint32_t>(s_newkey[i]), rel = s_free[i], b = ck_direct(k, rel);
-        if (b == ~0u) defer(k, rel);
-        else dirty(b);
-      }
-    } else {
+    // the new rows in windows of kNewCap ranks (one window unless mass churn): the window's
+    // keys and slots listed by rank (step 5 listed the first window when it is the only one),
+    // one lane per new row inserting
+    for (uint32_t w0 = 0; w0 < n_ins; w0 += kNewCap) {  // block-uniform
+      const uint32_t wn = min(kNewCap, n_ins - w0);
+      if (!compact) {
 #pragma unroll
-      for (int j = 0; j < kRpl; ++j) {
-        if (rk[j] == ~0u) continue;
-        const uint32_t k = static_cast<uint32_t>(key[j]), rel = (res[j] & KACC_SLOT_MASK) - s0;
-        const uint32_t b = ck_direct(k, rel);
-        if (b == ~0u) defer(k, rel);
+        for (int j = 0; j < kRpl; ++j) {
+          if (rk[j] == ~0u || rk[j] - w0 >= wn) continue;
+          s_newkey[rk[j] - w0] = key[j];
+          s_free[rk[j] - w0] = static_cast<uint16_t>((res[j] & KACC_SLOT_MASK) - s0);
+          s_newbad[rk[j] - w0] = 0;
+        }
+        jbar<V>();
+      }
+      for (uint32_t i = tid; i < wn; i += kThreads) {
+        const uint32_t k = static_cast<uint32_t>(s_newkey[i]), rel = s_free[i], b = ck_direct(k, rel);
+        if (b == ~1u) s_newbad[i] = 1;
+        else if (b == ~0u) defer(k, rel);
         else dirty(b);
       }
-    }
-    jbar<V>();
-    if (s_ckn) {  // block-uniform: lane 0 alone places each key whose groups were full, by kicks
-      if (tid == 0) {
-      const uint32_t nd = min(s_ckn, kNewCap);
-      for (uint32_t d = 0; d < nd; ++d) {
-        uint32_t k = s_ckkey[d], rel = s_ckrel[d];
-        bool placed = false;
-        for (int kick = 0; kick < kCkMaxKicks && !placed; ++kick) {
-          const uint32_t ga = ck_g1(k, gs), gb = ck_g2(k, gs);
-          for (uint32_t e = 0; e < 8 && !placed; ++e) {
-            const uint32_t b = (e < 4 ? ga : gb) * 4 + (e & 3);
-            if (L.k[b] == T::kEmpty) {
+      jbar<V>();
+      if (a.stop_after == 6u) return;  // timing ablation: direct inserts done
+      if (s_ckn) {  // block-uniform: lane 0 alone places each key whose groups were full, by kicks
+        if (tid == 0) {
+          const uint32_t nd = min(s_ckn, kNewCap);
+          for (uint32_t d = 0; d < nd; ++d) {
+            uint32_t k = s_ckkey[d], rel = s_ckrel[d];
+            if (ck_match(s_grp[ck_g1(k, CG)], k) | ck_match(s_grp[ck_g2(k, CG)], k)) {
+              s_ckfail |= 2u;  // an ID given twice among the deferred: the check below finds it
+              continue;
+            }
+            bool placed = false;
+            for (int kick = 0; kick < kCkMaxKicks && !placed; ++kick) {
+              const uint32_t ga = ck_g1(k, CG), gb = ck_g2(k, CG);
+              const uint32_t ea = ck_match(s_grp[ga], T::kEmpty), eb = ck_match(s_grp[gb], T::kEmpty);
+              if (ea | eb) {
+                const uint32_t b = ea ? ga * 4 + __builtin_ctz(ea) : gb * 4 + __builtin_ctz(eb);
+                L.k[b] = k;
+                L.s[b] = static_cast<uint16_t>(rel);
+                dirty(b);
+                placed = true;
+                break;
+              }
+              // evict a key of one of the groups (alternating, rotating) to its other group
+              const uint32_t b = ((kick & 1) ? gb : ga) * 4 + ((kick >> 1) & 3);
+              const uint32_t vk = L.k[b], vr = L.s[b];
               L.k[b] = k;
               L.s[b] = static_cast<uint16_t>(rel);
               dirty(b);
-              placed = true;
+              k = vk;
+              rel = vr;
+            }
+            if (!placed) s_ckfail |= 1u;  // a homeless key: the call fails (not reached at load <= 2/3)
+          }
+          s_ckn = 0u;
+        }
+        jbar<V>();
+      }
+      // inserts from more than one wave, or a deferred duplicate: an ID given twice within the
+      // window may have escaped the inline check (an earlier window's entry never does: it was
+      // in place before this window's inserts) — both entries sit in the ID's two groups, the
+      // larger slot gives way (block-uniform; rare)
+      if (wn > 64 || (s_ckfail & 2u)) {
+        for (uint32_t i = tid; i < wn; i += kThreads) {
+          if (s_newbad[i]) continue;
+          const uint32_t k = static_cast<uint32_t>(s_newkey[i]), rel = s_free[i];
+          bool drop = false;
+          uint32_t mine_b = ~0u;
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const uint32_t g = t ? ck_g2(k, CG) : ck_g1(k, CG);
+            for (uint32_t m = ck_match(s_grp[g], k); m; m &= m - 1) {
+              const uint32_t b = g * 4 + __builtin_ctz(m), sl = L.slot(b);
+              if (sl == rel) mine_b = b;
+              else if (sl < rel) drop = true;
             }
           }
-          if (placed) break;
-          // evict a key of one of the groups (alternating, rotating) to its other group
-          const uint32_t b = ((kick & 1) ? gb : ga) * 4 + ((kick >> 1) & 3);
-          const uint32_t vk = L.k[b], vr = L.s[b];
-          L.k[b] = k;
-          L.s[b] = static_cast<uint16_t>(rel);
-          dirty(b);
-          k = vk;
-          rel = vr;
+          if (drop && mine_b != ~0u) L.clear(mine_b);
+          if (drop || mine_b == ~0u) s_newbad[i] = 1;
         }
-        if (!placed) s_ckfail = 1u;  // a homeless key: the call fails (not reached at load <= 2/3)
+        jbar<V>();  // the dropped duplicates' buckets are empty before step 7 writes them back
       }
-      }
-      jbar<V>();
-    }
-    if (tid == 0 && s_ckfail) raise(kErrRange);
-    // an ID given twice: both entries sit in its two groups; the larger slot gives way
-    auto ck_dup = [&](uint32_t k, uint32_t rel) -> bool {
-      bool drop = false;
-      uint32_t mine_b = ~0u;
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const uint32_t g = t ? ck_g2(k, gs) : ck_g1(k, gs);
-        const uint4 gv = *reinterpret_cast<const uint4 *>(s_ent + g * 4);
-        for (uint32_t m = ck_match(gv, k); m; m &= m - 1) {
-          const uint32_t b = g * 4 + __builtin_ctz(m), sl = L.slot(b);
-          if (sl == rel) mine_b = b;
-          else if (sl < rel) drop = true;
-        }
-      }
-      if (drop && mine_b != ~0u) L.clear(mine_b);
-      return drop || mine_b == ~0u;
-    };
-    if (compact) {  // one lane per new row (the few lanes of wave 0), then their owners
-      for (uint32_t i = tid; i < n_ins; i += kThreads)
-        if (ck_dup(static_cast<uint32_t>(s_newkey[i]), s_free[i])) s_newbad[i] = 1;
-      jbar<V>();
 #pragma unroll
       for (int j = 0; j < kRpl; ++j)
-        if (rk[j] != ~0u && s_newbad[rk[j]]) {
+        if (rk[j] != ~0u && rk[j] - w0 < wn && s_newbad[rk[j] - w0]) {
           raise(kErrKey);
           res[j] = kInvalid;
         }
-    } else {
-#pragma unroll
-      for (int j = 0; j < kRpl; ++j)
-        if (rk[j] != ~0u && ck_dup(static_cast<uint32_t>(key[j]), (res[j] & KACC_SLOT_MASK) - s0)) {
-          raise(kErrKey);
-          res[j] = kInvalid;
-        }
+      if (w0 + kNewCap < n_ins) jbar<V>();  // the list is refilled for the next window
     }
-    if (a.out_span) {  // the rows' final slots: the span rides on the barrier below
-      uint32_t lo = 0xffffffffu, hi = 0u;
-#pragma unroll
-      for (int j = 0; j < kRpl; ++j) {
-        if (res[j] != kInvalid) {
-          lo = min(lo, res[j] & KACC_SLOT_MASK);
-          hi = max(hi, res[j] & KACC_SLOT_MASK);
-        }
-      }
-      lo = wave_reduce_dpp(lo, 0xffffffffu, DppMin{});
-      hi = wave_reduce_dpp(hi, 0u, DppMax{});
-      if ((tid & 63) == 0 && lo <= hi) {
-        atomicMin(&s_flo, lo);
-        atomicMax(&s_fhi, hi);
-      }
-    }
-    jbar<V>();  // the dropped duplicates' buckets are empty before step 7 writes them back
+    if (tid == 0 && (s_ckfail & 1u)) raise(kErrRange);
+    if (a.stop_after == 7u) return;  // timing ablation: kicks and duplicate check done
   } else if (compact) {
     for (uint32_t i = tid; i < n_ins; i += kThreads) {
       if constexpr (kInsDup) {
@@ -1147,6 +1170,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         G.e[b] = s_ent[b];
       }
     }
+  } else if constexpr (kCuckoo) {  // lane tid: its 8 buckets as two vector stores when any changed
+    if (tid * kPer < Hu && ((s_dirty[tid >> 2] >> ((tid & 3) * 8)) & 0xffu)) {
+      using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+      const u32x4 *ks = reinterpret_cast<const u32x4 *>(s_ent + tid * kPer);
+      u32x4 *kd = reinterpret_cast<u32x4 *>(G.k + tid * kPer);
+      kd[0] = ks[0];
+      kd[1] = ks[1];
+      *reinterpret_cast<u32x4 *>(G.s + tid * kPer) = *reinterpret_cast<const u32x4 *>(s_slot + tid * kPer);
+    }
   } else {
     for (uint32_t w = tid; w < H / 32; w += kThreads) {
       for (uint32_t d = s_dirty[w]; d; d &= d - 1) {
@@ -1160,6 +1192,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       }
     }
   }
+  if (a.stop_after == 8u) return;  // timing ablation: the changed buckets written back
   uint32_t *__restrict__ out = a.out_slot + v.r0;
   if (kVec && tid * kRpl + kRpl <= R) {
     __builtin_memcpy(out + tid * kRpl, res, sizeof(res));
@@ -1442,13 +1475,16 @@ constexpr int kJoinR2 = kacc::join::kJLock | kacc::join::kJErrReg | kacc::join::
 constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | kacc::join::kJVec | kacc::join::kJGroup;
 constexpr int kJoinLean = kJoinGroup | kacc::join::kJLean;
 constexpr int kJoinCuckoo = kJoinLean | kacc::join::kJCuckoo;
+constexpr int kJoinCuckooS = kJoinCuckoo | kacc::join::kJCkSmall;
 
 constexpr int kJoinDefault = kJoinCuckoo;  // production: PID tables (the u64-keyed kinds: kJoinLean)
 // the PID small-table format a variant works on (kacc_slotmap.fmt)
 int variant_fmt(int v) {
-  return (v & kacc::join::kJCuckoo) ? 3 : (v & kacc::join::kJ6B) ? 1 : 0;
+  return (v & kacc::join::kJCuckoo) ? ((v & kacc::join::kJCkSmall) ? 4 : 3) : (v & kacc::join::kJ6B) ? 1 : 0;
 }
-const char *fmt_name(int f) { return f == 3 ? "6-B cuckoo" : f == 1 ? "6-B" : "8-B"; }
+const char *fmt_name(int f) {
+  return f == 4 ? "6-B cuckoo, 1.5 S buckets" : f == 3 ? "6-B cuckoo" : f == 1 ? "6-B" : "8-B";
+}
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
 int launched_variant(int v) {
@@ -1462,6 +1498,7 @@ int launched_variant(int v) {
     case kJoinGroup | kacc::join::kJDpp:
     case kJoinLean:
     case kJoinCuckoo:
+    case kJoinCuckooS:
       return v;
     default: return kJoinDefault;
   }
@@ -1653,6 +1690,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinGroup: hipLaunchKernelGGL((join_small<K, kJoinGroup>), grid, block, 0, st, a); break;
       case kJoinLean: hipLaunchKernelGGL((join_small<K, kJoinLean>), grid, block, 0, st, a); break;
       case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
+      case kJoinCuckooS: hipLaunchKernelGGL((join_small<K, kJoinCuckooS>), grid, block, 0, st, a); break;
       default:
         if constexpr (sizeof(K) == 4)
           hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a);

@@ -117,9 +117,23 @@ def test_join_bit_exact(name, sizes, churn, kind, policy):
         assert term == want_term, f"interval {it}"
 
 
+@pytest.fixture(params=[-1, 57855], ids=["production", "cuckoo-1.5S"])
+def join_variant(request):
+    """The production join and the A/B variant of tools/bench_join_variants.py (cuckoo table
+    of 1.5 S buckets), set for the test's maps (kacc_debug_set_join_variant, read at reset)."""
+    import ctypes
+
+    lib = accel.load()
+    lib.kacc_debug_set_join_variant.argtypes = [ctypes.c_int]
+    lib.kacc_debug_set_join_variant.restype = ctypes.c_int
+    prev = lib.kacc_debug_set_join_variant(request.param)
+    yield request.param
+    lib.kacc_debug_set_join_variant(prev)
+
+
 @pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
 @pytest.mark.parametrize("churn", [0.02, 0.1, 0.3])
-def test_join_long_churn_bit_exact(churn, policy):
+def test_join_long_churn_bit_exact(churn, policy, join_variant):
     """30 intervals of churn, bit-exact every interval: at 2-10 % the small nodes take the
     one-wave tail (kJEasy) until tombstones crowd their tables, then one block-wide
     interval rebuilds them and the tail resumes; at 30 % the 2000-row nodes have more

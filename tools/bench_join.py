@@ -187,7 +187,7 @@ def main():
     lib = accel.load()
     lib.kacc_debug_join_variant.argtypes = [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 7 + [ctypes.c_uint32]
     phases = {}
-    for v in (1, 2, 3, 4, 5, 0):
+    for v in [int(x) for x in os.environ.get("STOPS", "1,2,3,4,5,0").split(",")]:
         ms = []
         for rep in range(4):
             sm.reset()
