@@ -328,6 +328,7 @@ __device__ __forceinline__ uint32_t ck_g2(uint32_t k, uint32_t G) {
 // kJCkSmall: the cuckoo table fills only 4 ceil(3S / 8) of the node's H buckets (1.5 S: load
 // <= 2/3 as before, but of a table sized by the slots, not the next power of two)
 constexpr int kJCkSmall = 32768;
+
 // bit e: key word e of a group equals k
 __device__ __forceinline__ uint32_t ck_match(const uint4 &g, uint32_t k) {
   return (g.x == k ? 1u : 0u) | (g.y == k ? 2u : 0u) | (g.z == k ? 4u : 0u) | (g.w == k ? 8u : 0u);
@@ -760,7 +761,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   }
   jbar<V>();
   if (a.stop_after == 2u) return;  // timing ablation
-
   // ---- 3: per-word free / terminated bits and their prefixes -------------------------
   uint32_t packed = 0;
   if (!kLean && tid < W) {
@@ -1477,6 +1477,7 @@ constexpr int kJoinLean = kJoinGroup | kacc::join::kJLean;
 constexpr int kJoinCuckoo = kJoinLean | kacc::join::kJCuckoo;
 constexpr int kJoinCuckooS = kJoinCuckoo | kacc::join::kJCkSmall;
 
+
 constexpr int kJoinDefault = kJoinCuckoo;  // production: PID tables (the u64-keyed kinds: kJoinLean)
 // the PID small-table format a variant works on (kacc_slotmap.fmt)
 int variant_fmt(int v) {
@@ -1691,6 +1692,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinLean: hipLaunchKernelGGL((join_small<K, kJoinLean>), grid, block, 0, st, a); break;
       case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
       case kJoinCuckooS: hipLaunchKernelGGL((join_small<K, kJoinCuckooS>), grid, block, 0, st, a); break;
+
       default:
         if constexpr (sizeof(K) == 4)
           hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a);

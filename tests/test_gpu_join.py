@@ -117,10 +117,11 @@ def test_join_bit_exact(name, sizes, churn, kind, policy):
         assert term == want_term, f"interval {it}"
 
 
-@pytest.fixture(params=[-1, 57855], ids=["production", "cuckoo-1.5S"])
+@pytest.fixture(params=[-1, 57855, 511], ids=["production", "cuckoo-1.5S", "round5-linear"])
 def join_variant(request):
-    """The production join and the A/B variant of tools/bench_join_variants.py (cuckoo table
-    of 1.5 S buckets), set for the test's maps (kacc_debug_set_join_variant, read at reset)."""
+    """The production join (the cuckoo table), its A/B variant with a table of 1.5 S buckets, and
+    round 5's linear-probing kernel (tools/bench_join_variants.py), set for the test's maps
+    (kacc_debug_set_join_variant, read at reset)."""
     import ctypes
 
     lib = accel.load()
