@@ -410,7 +410,8 @@ def pipeline_line(args, steps=10, warm=8):
     sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
     tr = accel.Tracker(acc, accel.KACC_KIND_PROC, 500, zone=0, min_energy=10 * 10**6)
     churn = fleet.ProcChurn(layout, churn=0.02)
-    keys = [torch.from_numpy(churn.next_keys().view(np.int32)).cuda() for _ in range(warm + steps)]
+    n_iv = warm + 2 * steps  # warm-up, the split pass, the sequence pass
+    keys = [torch.from_numpy(churn.next_keys().view(np.int32)).cuda() for _ in range(n_iv)]
     sim = fleet.FleetSim(layout, seed=fleet.SEED)
     statics = to_device(layout.static_arrays())
     cap = int(slot_off[-1])
@@ -421,7 +422,7 @@ def pipeline_line(args, steps=10, warm=8):
     span = torch.zeros(2 * N, dtype=torch.int32, device="cuda")
     full = [to_device({n: a for n, a in sim.next_interval().items() if n != "proc_slot"}) for _ in range(2)]
     ivs = []
-    for k in range(warm + steps):
+    for k in range(n_iv):
         t = dict(statics)
         t.update(full[k % 2])
         t.update(to_device({n: a for n, a in sim.next_node_inputs().items()
@@ -430,36 +431,54 @@ def pipeline_line(args, steps=10, warm=8):
         t["node_proc_span"] = span
         ivs.append((interval_from_tensors(t, sizes, layout.fast_flag() | accel.KACC_F_NODE_SLOT_RANGES
                                           | accel.KACC_F_STABLE_SLOT_NODES), t))
-    tj, tt, ti, tall = [], [], [], []
-    for k in range(warm + steps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        ev[0].record()
+    def interval(k):
         sm.join(P, ivs[k][1]["proc_off"].data_ptr(), keys[k].data_ptr(), 0, d_slot.data_ptr(), tk.data_ptr(),
                 ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
-        ev[1].record()
+        yield
         if k % 2:
             tr.clear(stream)
         tr.add(sm, tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), stream)
-        ev[2].record()
+        yield
         acc.run_interval(ivs[k][0], stream)
-        ev[3].record()
+        yield
+
+    tj, tt, ti, tall = [], [], [], []
+    for k in range(warm + steps):  # warm-up, then the split: events around each kernel
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        for i, _ in enumerate(interval(k)):
+            ev[i + 1].record()
         if k >= warm:
             ev[3].synchronize()
             tj.append(ev[0].elapsed_time(ev[1]))
             tt.append(ev[1].elapsed_time(ev[2]))
             ti.append(ev[2].elapsed_time(ev[3]))
             tall.append(ev[0].elapsed_time(ev[3]))
+    # the production sequence: `steps` intervals back to back, no event packet between their
+    # kernels (each costs a stream gap): one event pair around the run
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(warm + steps, n_iv):
+        for _ in interval(k):
+            pass
+    e1.record()
+    e1.synchronize()
+    seq_ms = e0.elapsed_time(e1) / steps
     acc.sync(stream)
     n_term = int(cnt.sum().item())
     tr.close()
     sm.close()
     acc.close()
-    ms = float(np.mean(tall))
-    return {"ms_per_interval": ms, "proc_attr_per_s": P / (ms * 1e-3),
+    return {"ms_per_interval": seq_ms, "proc_attr_per_s": P / (seq_ms * 1e-3),
+            "ms_per_interval_split": float(np.mean(tall)),
             "join_ms": float(np.mean(tj)), "tracker_ms": float(np.mean(tt)), "interval_ms": float(np.mean(ti)),
             "terminated_last_interval": n_term, "intervals": steps,
             "note": "kacc_slot_join (reuse policy) -> kacc_tracker_add -> kacc_run_interval on one stream, "
-                    "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device"}
+                    "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device; ms_per_interval: "
+                    "`intervals` intervals back to back with one event pair around them; join_ms / tracker_ms / "
+                    "interval_ms and ms_per_interval_split: a pass with events between the kernels (each event "
+                    "packet adds a stream gap)"}
 
 
 def host_path_line(args, steps=10):
