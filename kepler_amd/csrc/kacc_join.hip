@@ -328,6 +328,13 @@ __device__ __forceinline__ uint32_t ck_g2(uint32_t k, uint32_t G) {
 // kJCkSmall: the cuckoo table fills only 4 ceil(3S / 8) of the node's H buckets (1.5 S: load
 // <= 2/3 as before, but of a table sized by the slots, not the next power of two)
 constexpr int kJCkSmall = 32768;
+// kJCkFast: the join is VALU-issue-bound (eight waves per SIMD, 821 VALU instructions per
+// wave: 85 % of its quad-cycles), so (a) the two groups from ONE quarter-rate multiply each
+// (the top bits of k x C for the power-of-two group count of format 3, the second group
+// flipped off the first on a clash) instead of five multiplies per key, (b) a wave without
+// rows skips the lookups (R = 2000 leaves waves 6-7 idle there), (c) no occupancy count
+// (a six-step cross-lane sum per wave; only linear probing's rebuild rule reads it)
+constexpr int kJCkFast = 65536;
 
 // bit e: key word e of a group equals k
 __device__ __forceinline__ uint32_t ck_match(const uint4 &g, uint32_t k) {
@@ -436,6 +443,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   constexpr bool kBkt = kLean;  // held slots' buckets and the rows-not-found bitmap
   constexpr bool kCuckoo = k6 && kGroup && (V & kJCuckoo) != 0;  // PID tables only
   constexpr bool kCkSmall = kCuckoo && (V & kJCkSmall) != 0;
+  constexpr bool kCkFast = kCuckoo && !kCkSmall && (V & kJCkFast) != 0;
   static_assert(!kCuckoo || kLean, "kJCuckoo empties terminated buckets through kJLean's step 4");
   using T = std::conditional_t<kWide, Tab<uint64_t>, std::conditional_t<k6, TabP, Tab<uint32_t>>>;
   using EntT = std::conditional_t<k6, uint32_t, uint64_t>;   // a bucket's entry / key word
@@ -471,6 +479,20 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   const uint32_t W = (S + 31) / 32;
   // kJCuckoo: the buckets in use (Hu <= H) and their 4-bucket groups
   const uint32_t Hu = kCkSmall ? min(H, max(8u, 4 * ((3 * S + 7) / 8))) : H, CG = Hu / 4;
+  // the key's two groups (kJCkFast: CG = H / 4 is a power of two >= 16, csh = 32 - log2 CG)
+  const uint32_t csh = kCkFast ? static_cast<uint32_t>(__builtin_clz(CG)) + 1u : 0u;
+  const auto h1 = [&](uint32_t k) -> uint32_t {
+    if constexpr (kCkFast) return (k * 0x9E3779B1u) >> csh;
+    else return ck_g1(k, CG);
+  };
+  const auto h2 = [&](uint32_t k) -> uint32_t {
+    if constexpr (kCkFast) {
+      const uint32_t g1 = (k * 0x9E3779B1u) >> csh, g = ((k ^ (k >> 16)) * 0x85EBCA6Bu) >> csh;
+      return g != g1 ? g : g1 ^ 1u;
+    } else {
+      return ck_g2(k, CG);
+    }
+  };
   if (R > kSmallRows) {  // more rows than the table's <= 2730 slots: ERANGE, map unchanged
     for (uint32_t r = tid; r < R; r += kThreads) a.out_slot[v.r0 + r] = kInvalid;
     if (tid == 0) {
@@ -604,8 +626,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
         if constexpr (kBkt) s_bkt[sl] = static_cast<uint16_t>(bucket_of(j));
       }
     }
-    occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
-    if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
+    if constexpr (!kCkFast) {  // (the cuckoo table never rebuilds: kJCkFast drops the count)
+      occ = (V & kJDpp) ? wave_reduce_dpp(occ, 0u, DppAdd{}) : wave_sum(occ);
+      if ((tid & 63) == 0 && occ) atomicAdd(&s_occ, occ);  // buckets not empty at load
+    }
   }
   uint32_t mine = 0;   // new rows of this lane
   uint32_t found = 0;  // kSeenNR: rows of this lane that found their ID
@@ -618,7 +642,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     for (int j = 0; j < kRpl; ++j) {
       const uint32_t r = tid * kRpl + j;
       res[j] = kInvalid;
-      pb[j] = bucket(key[j], v.shift);
+      pb[j] = kCuckoo ? 0u : bucket(key[j], v.shift);
       if (r >= R) continue;
       if (key[j] == T::kEmpty || key[j] == T::kTomb) {
         raise(kErrKey);
@@ -628,27 +652,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     if constexpr (kCuckoo) {
       // the key's two groups; found in either or absent (three rows at a time)
+      const uint32_t wrow0 = __builtin_amdgcn_readfirstlane((tid & ~63u) * kRpl);
 #pragma unroll
-      for (int h2 = 0; h2 < kRpl; h2 += kRpl / 2) {
+      for (int hh = 0; hh < kRpl; hh += kRpl / 2) {
+        if (kCkFast && wrow0 >= R) break;  // wave-uniform: no row of this wave
         uint4 ga[kRpl / 2], gb[kRpl / 2];
         uint32_t g1[kRpl / 2], g2[kRpl / 2];
 #pragma unroll
         for (int j = 0; j < kRpl / 2; ++j) {
-          const uint32_t k = static_cast<uint32_t>(key[h2 + j]);
-          g1[j] = ck_g1(k, CG);
-          g2[j] = ck_g2(k, CG);
+          const uint32_t k = static_cast<uint32_t>(key[hh + j]);
+          g1[j] = h1(k);
+          g2[j] = h2(k);
           ga[j] = *reinterpret_cast<const uint4 *>(s_ent + g1[j] * 4);
           gb[j] = *reinterpret_cast<const uint4 *>(s_ent + g2[j] * 4);
         }
 #pragma unroll
         for (int j = 0; j < kRpl / 2; ++j) {
-          const uint32_t k = static_cast<uint32_t>(key[h2 + j]);
+          const uint32_t k = static_cast<uint32_t>(key[hh + j]);
           const uint32_t m1 = ck_match(ga[j], k), m2 = ck_match(gb[j], k);
           const uint32_t b = m1 ? g1[j] * 4 + __builtin_ctz(m1) : g2[j] * 4 + __builtin_ctz(m2 | 16u);
-          const bool act = ((state >> (2 * (h2 + j))) & 3u) == 1u;
           const uint32_t nv = (m1 | m2) ? 2u : 3u;
-          state = act ? (state & ~(3u << (2 * (h2 + j)))) | (nv << (2 * (h2 + j))) : state;
-          pb[h2 + j] = b;
+          const bool act = ((state >> (2 * (hh + j))) & 3u) == 1u;
+          state = act ? (state & ~(3u << (2 * (hh + j)))) | (nv << (2 * (hh + j))) : state;
+          pb[hh + j] = b;
         }
       }
     } else if constexpr (kGroup) {
@@ -976,7 +1002,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     // both full.  Two rows of one ID inserting in ONE wave read the same groups in the same
     // instruction, choose the same bucket and collide on it: the loser's retry finds the key
     const auto ck_direct = [&](uint32_t k, uint32_t rel) -> uint32_t {
-      const uint32_t ga = ck_g1(k, CG), gb = ck_g2(k, CG);
+      const uint32_t ga = h1(k), gb = h2(k);
       for (int tries = 0; tries < 16; ++tries) {
         const uint4 va = s_grp[ga], vb = s_grp[gb];
         if (ck_match(va, k) | ck_match(vb, k)) return ~1u;
@@ -1025,13 +1051,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
           const uint32_t nd = min(s_ckn, kNewCap);
           for (uint32_t d = 0; d < nd; ++d) {
             uint32_t k = s_ckkey[d], rel = s_ckrel[d];
-            if (ck_match(s_grp[ck_g1(k, CG)], k) | ck_match(s_grp[ck_g2(k, CG)], k)) {
+            if (ck_match(s_grp[h1(k)], k) | ck_match(s_grp[h2(k)], k)) {
               s_ckfail |= 2u;  // an ID given twice among the deferred: the check below finds it
               continue;
             }
             bool placed = false;
             for (int kick = 0; kick < kCkMaxKicks && !placed; ++kick) {
-              const uint32_t ga = ck_g1(k, CG), gb = ck_g2(k, CG);
+              const uint32_t ga = h1(k), gb = h2(k);
               const uint32_t ea = ck_match(s_grp[ga], T::kEmpty), eb = ck_match(s_grp[gb], T::kEmpty);
               if (ea | eb) {
                 const uint32_t b = ea ? ga * 4 + __builtin_ctz(ea) : gb * 4 + __builtin_ctz(eb);
@@ -1068,7 +1094,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
           uint32_t mine_b = ~0u;
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            const uint32_t g = t ? ck_g2(k, CG) : ck_g1(k, CG);
+            const uint32_t g = t ? h2(k) : h1(k);
             for (uint32_t m = ck_match(s_grp[g], k); m; m &= m - 1) {
               const uint32_t b = g * 4 + __builtin_ctz(m), sl = L.slot(b);
               if (sl == rel) mine_b = b;
@@ -1476,15 +1502,17 @@ constexpr int kJoinGroup = kJoinR2 | kacc::join::kJ6B | kacc::join::kJSeenNR | k
 constexpr int kJoinLean = kJoinGroup | kacc::join::kJLean;
 constexpr int kJoinCuckoo = kJoinLean | kacc::join::kJCuckoo;
 constexpr int kJoinCuckooS = kJoinCuckoo | kacc::join::kJCkSmall;
+constexpr int kJoinCuckooF = kJoinCuckoo | kacc::join::kJCkFast;
 
 
 constexpr int kJoinDefault = kJoinCuckoo;  // production: PID tables (the u64-keyed kinds: kJoinLean)
 // the PID small-table format a variant works on (kacc_slotmap.fmt)
 int variant_fmt(int v) {
-  return (v & kacc::join::kJCuckoo) ? ((v & kacc::join::kJCkSmall) ? 4 : 3) : (v & kacc::join::kJ6B) ? 1 : 0;
+  return (v & kacc::join::kJCuckoo) ? ((v & kacc::join::kJCkSmall) ? 4 : (v & kacc::join::kJCkFast) ? 5 : 3)
+                                    : (v & kacc::join::kJ6B) ? 1 : 0;
 }
 const char *fmt_name(int f) {
-  return f == 4 ? "6-B cuckoo, 1.5 S buckets" : f == 3 ? "6-B cuckoo" : f == 1 ? "6-B" : "8-B";
+  return f == 5 ? "6-B cuckoo, shift hashes" : f == 4 ? "6-B cuckoo, 1.5 S buckets" : f == 3 ? "6-B cuckoo" : f == 1 ? "6-B" : "8-B";
 }
 int g_join_variant = -1;  // kacc_debug_set_join_variant: -1 = production (kJoinDefault)
 // the variant join_small is launched with (the instantiated ones; else production)
@@ -1500,6 +1528,7 @@ int launched_variant(int v) {
     case kJoinLean:
     case kJoinCuckoo:
     case kJoinCuckooS:
+    case kJoinCuckooF:
       return v;
     default: return kJoinDefault;
   }
@@ -1692,6 +1721,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinLean: hipLaunchKernelGGL((join_small<K, kJoinLean>), grid, block, 0, st, a); break;
       case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
       case kJoinCuckooS: hipLaunchKernelGGL((join_small<K, kJoinCuckooS>), grid, block, 0, st, a); break;
+      case kJoinCuckooF: hipLaunchKernelGGL((join_small<K, kJoinCuckooF>), grid, block, 0, st, a); break;
 
       default:
         if constexpr (sizeof(K) == 4)
