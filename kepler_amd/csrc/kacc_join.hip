@@ -1505,7 +1505,7 @@ constexpr int kJoinCuckooS = kJoinCuckoo | kacc::join::kJCkSmall;
 constexpr int kJoinCuckooF = kJoinCuckoo | kacc::join::kJCkFast;
 
 
-constexpr int kJoinDefault = kJoinCuckoo;  // production: PID tables (the u64-keyed kinds: kJoinLean)
+constexpr int kJoinDefault = kJoinCuckooF;  // production: PID tables (the u64-keyed kinds: kJoinLean)
 // the PID small-table format a variant works on (kacc_slotmap.fmt)
 int variant_fmt(int v) {
   return (v & kacc::join::kJCuckoo) ? ((v & kacc::join::kJCkSmall) ? 4 : (v & kacc::join::kJCkFast) ? 5 : 3)

@@ -117,7 +117,7 @@ def test_join_bit_exact(name, sizes, churn, kind, policy):
         assert term == want_term, f"interval {it}"
 
 
-@pytest.fixture(params=[-1, 90623, 57855, 511], ids=["production", "cuckoo-shift", "cuckoo-1.5S", "round5-linear"])
+@pytest.fixture(params=[-1, 25087, 57855, 511], ids=["production", "cuckoo-umulhi", "cuckoo-1.5S", "round5-linear"])
 def join_variant(request):
     """The production join (the cuckoo table), its A/B variant with a table of 1.5 S buckets, and
     round 5's linear-probing kernel (tools/bench_join_variants.py), set for the test's maps
