@@ -52,13 +52,15 @@ run c5 400 --config 5 --intervals 60 --no-cpu-baseline
 run s8 300 --shard-of 8 --steps 50 --warmup 10 $B
 run s8_handoff 300 --shard-of 8 --steps 48 --warmup 8 --comm-wait always --allreduce-every 8 $B
 # the slot join: per-phase times (stops 1..8), the round-5 kernel (511) beside production (-1)
-# and the 1.5 S-bucket table (57855), then the per-wave SQ counters of the same three
+# and the first cuckoo build (25087), the per-wave SQ counters of the same three, then the
+# production kernel's SQ counters per phase stop
 if [ "${JOIN:-1}" = 1 ]; then
   echo "== join"
   timeout -k 10 400 env STOPS=1,2,3,4,5,6,7,8,0 python -u tools/bench_join.py > gpurun_out/$O/join.json 2>gpurun_out/$O/join.err || exit $?
   python -c "import json;d=json.load(open('gpurun_out/$O/join.json'));print(d['join_ms'], d['phase_ms'])"
-  timeout -k 10 300 env VARIANTS=511,-1,57855 ROUNDS=5 python -u tools/bench_join_variants.py > gpurun_out/$O/variants.json 2>gpurun_out/$O/variants.err || exit $?
+  timeout -k 10 300 env VARIANTS=511,-1,25087 ROUNDS=5 python -u tools/bench_join_variants.py > gpurun_out/$O/variants.json 2>gpurun_out/$O/variants.err || exit $?
   python -c "import json;d=json.load(open('gpurun_out/$O/variants.json'));print(d['join_ms'], d['identical_to_first'])"
-  OUT=$O/join_pmc VARIANTS=511,-1,57855 bash tools/join_pmc.sh > /dev/null || exit $?
+  OUT=$O/join_pmc VARIANTS=511,-1,25087 bash tools/join_pmc.sh > /dev/null || exit $?
+  OUT=$O/join_phase_pmc STOPS=1,2,3,4,5,6,7,8,0 REPS=4 bash tools/join_pmc.sh > /dev/null || exit $?
 fi
 fi

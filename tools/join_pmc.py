@@ -2,7 +2,8 @@
 """Slot-join dispatches for rocprofv3 --pmc passes (tools/join_pmc.sh): config 3's small-node
 PID join in its steady state (2 % churn, fleet.KeyedChurn), REPS joins per variant in
 VARIANTS order (kacc_debug_set_join_variant; -1 = production), each variant from a reset
-map and two warm-up joins.  tools/join_pmc_summary.py averages the counters per kernel
+map and two warm-up joins; or, with STOPS=1,2,...,0, the production kernel stopped after each
+phase (kacc_debug_join_variant), REPS times a reset + two full joins + the stopped join.  tools/join_pmc_summary.py averages the counters per kernel
 instance (the variants are distinct template instances, so distinct kernel names)."""
 import ctypes
 import os
@@ -44,6 +45,21 @@ def main():
     ts = torch.zeros(cap, dtype=torch.int32, device="cuda")
     cnt = torch.zeros(layout.n_nodes, dtype=torch.int32, device="cuda")
     span = torch.zeros(2 * layout.n_nodes, dtype=torch.int32, device="cuda")
+    stops = [int(x) for x in os.environ.get("STOPS", "").split(",") if x]
+    if stops:  # per-phase counters of the production kernel: reset, two full joins, one stopped join
+        lib.kacc_debug_join_variant.argtypes = [ctypes.c_void_p, ctypes.c_uint32] + [ctypes.c_void_p] * 7 + [ctypes.c_uint32]
+        lib.kacc_debug_set_join_variant(-1)
+        for s_ in stops:
+            for _ in range(reps):
+                sm.reset()
+                for k in range(2):
+                    sm.join(P, off.data_ptr(), keys[k].data_ptr(), 0, out.data_ptr(), tk.data_ptr(), ts.data_ptr(),
+                            cnt.data_ptr(), stream, span.data_ptr())
+                rc = lib.kacc_debug_join_variant(sm.handle, P, off.data_ptr(), keys[2].data_ptr(), out.data_ptr(),
+                                                 tk.data_ptr(), ts.data_ptr(), cnt.data_ptr(), stream, s_)
+                assert rc == 0, rc
+        acc.sync(stream)
+        variants = []
     for v in variants:
         lib.kacc_debug_set_join_variant(v)
         sm.reset()
