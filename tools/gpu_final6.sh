@@ -13,13 +13,13 @@ O=${OUT:-final6}
 mkdir -p gpurun_out/$O
 sha=$(sha256sum kepler_amd/lib/libkepler_accel.so | cut -c1-16)
 echo "lib sha256 $sha" | tee gpurun_out/$O/lib_sha256.txt
+B="--no-cpu-baseline --frag-line 0 --no-pipeline-line --no-host-line"
 if [ "${PART:-a}" = a ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/$O/pytest_gpu.log 2>&1 || { echo "pytest failed rc=$?"; tail -30 gpurun_out/$O/pytest_gpu.log; exit 1; }
 tail -n 1 gpurun_out/$O/pytest_gpu.log
 timeout -k 10 200 python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/$O/smoke.log 2>&1 || exit $?
 tail -n 1 gpurun_out/$O/smoke.log
-B="--no-cpu-baseline --frag-line 0 --no-pipeline-line --no-host-line"
 prof() {  # NAME SECONDS bench-args...
   local n=$1 s=$2; shift 2
   echo "== prof $n"
