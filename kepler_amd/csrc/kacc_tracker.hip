@@ -39,7 +39,10 @@ namespace kacc {
 namespace trk {
 
 constexpr int kThreads = 256;
-constexpr uint32_t kChunk = 512;  // batch items filtered / sorted per step; tracked set staged in LDS up to this
+constexpr uint32_t kChunk = 256;   // batch items filtered / sorted per step (one per lane)
+constexpr uint32_t kSetLds = 512;  // tracked target-zone energies staged in LDS up to this set size
+// (15.5 KB of LDS: eight workgroups per CU, as many as the 32 waves allow; kChunk 512 held
+// 27.6 KB, five)
 constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node capacity
 
 struct Args {
@@ -125,7 +128,10 @@ __device__ void bitonic_wave(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
+// kZ: the zones a moved item carries in registers (Z <= 4: 16 fewer VGPRs, eight waves per SIMD)
+template <uint32_t kZ>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kZ <= 4 ? 8 : 4))) void node_add_kernel(
+    const Args a) {
   __shared__ uint64_t s_key[kChunk];    // survivors (filter order), then sort keys ~energy
   __shared__ uint64_t s_e[kChunk];
   __shared__ uint32_t s_slot[kChunk];
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
   __shared__ uint16_t s_ix[kChunk];
   __shared__ uint32_t s_rank[kChunk];
   __shared__ uint64_t s_tk[kChunk];     // a block of tracked keys (duplicate check)
-  __shared__ uint64_t s_te[kChunk];     // tracked target-zone energies (size <= kChunk: the rank search)
+  __shared__ uint64_t s_te[kSetLds];    // tracked target-zone energies (size <= kSetLds: the rank search)
   __shared__ uint32_t s_cnt;
   const uint32_t n = blockIdx.x, tid = threadIdx.x;
   const uint32_t Z = a.Z, z0 = a.z0, cap = a.cap;
@@ -164,14 +170,19 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
         pass[u] = e[u] >= a.min_e && !(full && e[u] <= min_full);  // :102, :124
       }
     }
-    const bool lds_set = size <= kChunk;  // block-uniform
+    bool any_pass = false;
+#pragma unroll
+    for (uint32_t u = 0; u < kChunk / kThreads; ++u) any_pass |= pass[u];
+    // no candidate of the chunk passes (a full set's minimum beats them all: the steady
+    // state): the tracked set is neither read nor changed
+    if (!__syncthreads_or(any_pass)) continue;
+    const bool lds_set = size <= kSetLds;  // block-uniform
+    if (lds_set)  // (read after the duplicate check's barriers)
+      for (uint32_t t = tid; t < size; t += kThreads) s_te[t] = a.set_e[(base + t) * Z + z0];
     for (uint32_t t0 = 0; t0 < size; t0 += kChunk) {  // :90 already tracked
       const uint32_t tn = min(kChunk, size - t0);
       __syncthreads();
-      for (uint32_t t = tid; t < tn; t += kThreads) {
-        s_tk[t] = a.set_key[base + t0 + t];
-        if (lds_set) s_te[t] = a.set_e[(base + t) * Z + z0];
-      }
+      for (uint32_t t = tid; t < tn; t += kThreads) s_tk[t] = a.set_key[base + t0 + t];
       __syncthreads();
 #pragma unroll
       for (uint32_t u = 0; u < kChunk / kThreads; ++u)
@@ -233,8 +244,8 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
       const bool have = i < size;
       uint32_t r = 0;
       uint64_t k = 0;
-      uint64_t E[KACC_MAX_ZONES];
-      double P[KACC_MAX_ZONES];
+      uint64_t E[kZ];
+      double P[kZ];
       if (have) {  // i + #survivors with a strictly higher energy (ties: tracked first)
         const uint64_t ei = lds_set ? s_te[i] : a.set_e[(base + i) * Z + z0];
         uint32_t lo = 0, hi = m;
@@ -246,16 +257,18 @@ __global__ __launch_bounds__(kThreads) void node_add_kernel(const Args a) {
             hi = mid;
         }
         r = i + lo;
-        k = a.set_key[base + i];
-        for (uint32_t z = 0; z < Z; ++z) {
-          E[z] = a.set_e[(base + i) * Z + z];
-          P[z] = a.set_p[(base + i) * Z + z];
+        if (r != i && r < new_size) {  // only the items that move are read
+          k = a.set_key[base + i];
+          for (uint32_t z = 0; z < kZ && z < Z; ++z) {
+            E[z] = a.set_e[(base + i) * Z + z];
+            P[z] = a.set_p[(base + i) * Z + z];
+          }
         }
       }
       __syncthreads();
       if (have && r != i && r < new_size) {
         a.set_key[base + r] = k;
-        for (uint32_t z = 0; z < Z; ++z) {
+        for (uint32_t z = 0; z < kZ && z < Z; ++z) {
           a.set_e[(base + r) * Z + z] = E[z];
           a.set_p[(base + r) * Z + z] = P[z];
         }
@@ -460,7 +473,11 @@ int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *ter
   a.term_slot = term_slot;
   a.term_count = term_count;
   (void)hipGetLastError();  // clear a stale error of an earlier call
-  hipLaunchKernelGGL(kacc::trk::node_add_kernel, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0, st, a);
+  if (a.Z <= 4)
+    hipLaunchKernelGGL(kacc::trk::node_add_kernel<4>, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(kacc::trk::node_add_kernel<KACC_MAX_ZONES>, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0,
+                       st, a);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }
