@@ -17,15 +17,15 @@
 // heap keeps the max_size best of (tracked ∪ batch), ties at the boundary
 // going to tracked items first (eviction needs a strictly higher energy) and
 // then to the batch order.  Each node's set is kept sorted (energy desc, then
-// insertion order), so one add is, per node (one workgroup each):
-//   filter  threshold, "beats the current minimum" when full, not tracked;
-//           survivors compacted in LDS (chunks of kChunk in slot order —
-//           equivalent, since the batch order breaks ties by slot)
-//   sort    survivors by (energy desc, slot) — bitonic in LDS
+// insertion order), so one add is, per node (one wavefront each):
+//   filter  threshold, "beats the current minimum" when full, not tracked —
+//           in chunks of 64 candidates in slot order (equivalent, since the
+//           batch order breaks ties by slot)
+//   sort    survivors by (energy desc, slot) — bitonic across the lanes
 //   merge   ranks by binary search (tracked i -> i + #survivors strictly
 //           above; survivor j -> j + #tracked at or above), then in place:
 //           tracked items only move to later positions, so they are moved
-//           in blocks from the end (read block, barrier, write block)
+//           in blocks of 64 from the end (a block's loads before its stores)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -39,10 +39,7 @@ namespace kacc {
 namespace trk {
 
 constexpr int kThreads = 256;
-constexpr uint32_t kChunk = 256;   // batch items filtered / sorted per step (one per lane)
 constexpr uint32_t kSetLds = 512;  // tracked target-zone energies staged in LDS up to this set size
-// (15.5 KB of LDS: eight workgroups per CU, as many as the 32 waves allow; kChunk 512 held
-// 27.6 KB, five)
 constexpr uint32_t kErrCap = 1u << 10;  // unlimited tracker past its per-node capacity
 
 struct Args {
@@ -64,233 +61,149 @@ struct Args {
   uint32_t *err;
 };
 
-// Bitonic sort of n (<= kChunk) (k1, k2, idx) triples in LDS, ascending.
-__device__ void bitonic(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t n) {
-  uint32_t m = 1;
-  while (m < n) m <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < m; i += kThreads) {
-    k1[i] = ~0ull;
-    k2[i] = ~0u;
-    ix[i] = 0xffffu;
-  }
-  __syncthreads();
-  for (uint32_t size = 2; size <= m; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < m; i += kThreads) {
-        const uint32_t j = i ^ stride;
-        if (j <= i) continue;
-        const bool up = (i & size) == 0;
-        const bool gt = k1[i] > k1[j] || (k1[i] == k1[j] && k2[i] > k2[j]);
-        if (gt == up) {
-          const uint64_t t1 = k1[i];
-          const uint32_t t2 = k2[i];
-          const uint16_t t3 = ix[i];
-          k1[i] = k1[j];
-          k2[i] = k2[j];
-          ix[i] = ix[j];
-          k1[j] = t1;
-          k2[j] = t2;
-          ix[j] = t3;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// The same network for n <= 64 in one wave's registers (lane j holds triple j, lanes
-// >= n the +inf padding): compare-exchange with the lane at distance `stride` by
-// shuffles, no workgroup barriers; the first n triples written back.  Caller: the
-// lanes of wave 0 only.
-__device__ void bitonic_wave(uint64_t *k1, uint32_t *k2, uint16_t *ix, uint32_t n) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint64_t a1 = lane < n ? k1[lane] : ~0ull;
-  uint32_t a2 = lane < n ? k2[lane] : ~0u;
-  uint32_t a3 = lane < n ? ix[lane] : 0xffffu;
-  for (uint32_t size = 2; size <= 64; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      const uint64_t b1 = __shfl_xor(a1, static_cast<int>(stride), 64);
-      const uint32_t b2 = __shfl_xor(a2, static_cast<int>(stride), 64);
-      const uint32_t b3 = __shfl_xor(a3, static_cast<int>(stride), 64);
-      const bool up = (lane & size) == 0, lower = (lane & stride) == 0;
-      const bool a_gt = a1 > b1 || (a1 == b1 && a2 > b2), b_gt = b1 > a1 || (b1 == a1 && b2 > a2);
-      // the pair's lower lane keeps the min when ascending (up), the max otherwise
-      const bool take = lower == up ? a_gt : b_gt;
-      a1 = take ? b1 : a1;
-      a2 = take ? b2 : a2;
-      a3 = take ? b3 : a3;
-    }
-  }
-  if (lane < n) {
-    k1[lane] = a1;
-    k2[lane] = a2;
-    ix[lane] = static_cast<uint16_t>(a3);
-  }
-}
-
-// kZ: the zones a moved item carries in registers (Z <= 4: 16 fewer VGPRs, eight waves per SIMD)
+// One WAVE per node (four nodes per workgroup, no workgroup barriers), 64 candidates per
+// chunk (one per lane).  A node's add is one dependent chain — term words -> energies ->
+// tracked set -> ranks -> moves -> copies — so it pays in nodes in flight: 32 per CU
+// (round 6; the workgroup-per-node kernel it replaces held 5, then 8).  Per wave in LDS:
+// the tracked target-zone energies (<= kSetLds, the rank search) and the sorted survivors'
+// energies.
+constexpr int kWaveNodes = kThreads / 64;
 template <uint32_t kZ>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kZ <= 4 ? 8 : 4))) void node_add_kernel(
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kZ <= 4 ? 8 : 4))) void node_add_wave_kernel(
     const Args a) {
-  __shared__ uint64_t s_key[kChunk];    // survivors (filter order), then sort keys ~energy
-  __shared__ uint64_t s_e[kChunk];
-  __shared__ uint32_t s_slot[kChunk];
-  __shared__ uint64_t s_k1[kChunk];
-  __shared__ uint32_t s_k2[kChunk];
-  __shared__ uint16_t s_ix[kChunk];
-  __shared__ uint32_t s_rank[kChunk];
-  __shared__ uint64_t s_tk[kChunk];     // a block of tracked keys (duplicate check)
-  __shared__ uint64_t s_te[kSetLds];    // tracked target-zone energies (size <= kSetLds: the rank search)
-  __shared__ uint32_t s_cnt;
-  const uint32_t n = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint64_t s_te_all[kWaveNodes][kSetLds];
+  __shared__ uint64_t s_se_all[kWaveNodes][64];
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
+  const uint32_t n = blockIdx.x * kWaveNodes + wv;
+  if (n >= a.n_nodes) return;  // wave-uniform
+  uint64_t *const s_te = s_te_all[wv];
+  uint64_t *const s_se = s_se_all[wv];
   const uint32_t Z = a.Z, z0 = a.z0, cap = a.cap;
   const uint64_t base = static_cast<uint64_t>(n) * cap;
   const uint32_t b0 = a.slot_off[n];
   const uint32_t c = min(a.term_count[n], a.slot_off[n + 1] - b0);
   const uint32_t K = a.max_size > 0 ? static_cast<uint32_t>(a.max_size) : cap;
   uint32_t size = min(a.size[n], cap);
-  for (uint32_t c0 = 0; c0 < c; c0 += kChunk) {
-    const uint32_t m0 = min(kChunk, c - c0);
+  for (uint32_t c0 = 0; c0 < c; c0 += 64) {
+    const uint32_t m0 = min(64u, c - c0);
     const bool full = a.max_size > 0 && size >= K;
     const uint64_t min_full = full ? a.set_e[(base + size - 1) * Z + z0] : 0ull;
     // ---- filter (terminated_resource_tracker.go:90-124) ----------------------------
-    uint64_t key[kChunk / kThreads], e[kChunk / kThreads];
-    uint32_t slot[kChunk / kThreads];
-    bool pass[kChunk / kThreads];
-#pragma unroll
-    for (uint32_t u = 0; u < kChunk / kThreads; ++u) {
-      const uint32_t i = tid + u * kThreads;
-      pass[u] = false;
-      key[u] = e[u] = 0;
-      slot[u] = 0;
-      if (i < m0) {
-        slot[u] = a.term_slot[b0 + c0 + i];
-        key[u] = a.term_key[b0 + c0 + i];
-        e[u] = a.tab_e[static_cast<uint64_t>(slot[u]) * a.tab_stride + z0];
-        pass[u] = e[u] >= a.min_e && !(full && e[u] <= min_full);  // :102, :124
+    uint64_t key = 0, e = 0;
+    uint32_t slot = 0;
+    bool pass = false;
+    if (lane < m0) {
+      slot = a.term_slot[b0 + c0 + lane];
+      key = a.term_key[b0 + c0 + lane];
+      e = a.tab_e[static_cast<uint64_t>(slot) * a.tab_stride + z0];
+      pass = e >= a.min_e && !(full && e <= min_full);  // :102, :124
+    }
+    if (__ballot(pass) == 0) continue;  // the tracked set is neither read nor changed
+    const bool lds_set = size <= kSetLds;  // wave-uniform
+    for (uint32_t t0 = 0; t0 < size; t0 += 64) {  // :90 already tracked; the energies staged
+      const uint32_t t = t0 + lane;
+      const uint64_t tk = t < size ? a.set_key[base + t] : 0ull;
+      if (lds_set && t < size) s_te[t] = a.set_e[(base + t) * Z + z0];
+      const uint32_t tn = min(64u, size - t0);
+      const uint32_t tk_lo = static_cast<uint32_t>(tk), tk_hi = static_cast<uint32_t>(tk >> 32);
+      for (uint32_t j = 0; j < tn; ++j) {
+        const uint64_t kj = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(tk_hi), j))) << 32) |
+                            static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(tk_lo), j));
+        pass = pass && key != kj;
       }
     }
-    bool any_pass = false;
-#pragma unroll
-    for (uint32_t u = 0; u < kChunk / kThreads; ++u) any_pass |= pass[u];
-    // no candidate of the chunk passes (a full set's minimum beats them all: the steady
-    // state): the tracked set is neither read nor changed
-    if (!__syncthreads_or(any_pass)) continue;
-    const bool lds_set = size <= kSetLds;  // block-uniform
-    if (lds_set)  // (read after the duplicate check's barriers)
-      for (uint32_t t = tid; t < size; t += kThreads) s_te[t] = a.set_e[(base + t) * Z + z0];
-    for (uint32_t t0 = 0; t0 < size; t0 += kChunk) {  // :90 already tracked
-      const uint32_t tn = min(kChunk, size - t0);
-      __syncthreads();
-      for (uint32_t t = tid; t < tn; t += kThreads) s_tk[t] = a.set_key[base + t0 + t];
-      __syncthreads();
-#pragma unroll
-      for (uint32_t u = 0; u < kChunk / kThreads; ++u)
-        if (pass[u])
-          for (uint32_t t = 0; t < tn; ++t)
-            if (s_tk[t] == key[u]) pass[u] = false;
+    const uint64_t pmask = __ballot(pass);
+    const uint32_t m = static_cast<uint32_t>(__popcll(pmask));
+    if (m == 0) continue;
+    // ---- sort: survivors by (energy desc, slot) = ascending (~e, slot); the others +inf ----
+    uint64_t k1 = pass ? ~e : ~0ull;
+    uint32_t k2 = pass ? slot : ~0u, ix = lane;
+    for (uint32_t sz = 2; sz <= 64; sz <<= 1) {
+      for (uint32_t stride = sz >> 1; stride > 0; stride >>= 1) {
+        const uint64_t b1 = __shfl_xor(k1, static_cast<int>(stride), 64);
+        const uint32_t b2 = __shfl_xor(k2, static_cast<int>(stride), 64);
+        const uint32_t b3 = __shfl_xor(ix, static_cast<int>(stride), 64);
+        const bool up = (lane & sz) == 0, lower = (lane & stride) == 0;
+        const bool a_gt = k1 > b1 || (k1 == b1 && k2 > b2), b_gt = b1 > k1 || (b1 == k1 && b2 > k2);
+        const bool take = lower == up ? a_gt : b_gt;
+        k1 = take ? b1 : k1;
+        k2 = take ? b2 : k2;
+        ix = take ? b3 : ix;
+      }
     }
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-#pragma unroll
-    for (uint32_t u = 0; u < kChunk / kThreads; ++u) {  // compaction order is irrelevant: sorted next
-      if (!pass[u]) continue;
-      const uint32_t j = atomicAdd(&s_cnt, 1u);
-      s_key[j] = key[u];
-      s_e[j] = e[u];
-      s_slot[j] = slot[u];
-    }
-    __syncthreads();
-    const uint32_t m = s_cnt;
-    if (m == 0) continue;  // block-uniform
-    // ---- sort survivors: energy desc, then slot (the batch order) -------------------
-    for (uint32_t j = tid; j < m; j += kThreads) {
-      s_k1[j] = ~s_e[j];
-      s_k2[j] = s_slot[j];
-      s_ix[j] = static_cast<uint16_t>(j);
-    }
-    __syncthreads();
-    if (m <= 64) {  // block-uniform: one wave, no barriers inside
-      if (tid < 64) bitonic_wave(s_k1, s_k2, s_ix, m);
-      __syncthreads();
-    } else {
-      bitonic(s_k1, s_k2, s_ix, m);
-    }
-    // ---- ranks (before anything moves) ----------------------------------------------
+    // lane j < m: the j-th survivor (its key and slot from lane ix)
+    const uint64_t skey = __shfl(key, static_cast<int>(ix), 64);
+    const uint32_t sslot = static_cast<uint32_t>(__shfl(static_cast<int>(slot), static_cast<int>(ix), 64));
+    const uint64_t se = ~k1;
+    s_se[lane] = se;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t new_size = size + m;
     if (a.max_size > 0) {
       new_size = min(new_size, K);
     } else if (new_size > cap) {  // unlimited: per-node capacity exceeded
-      if (tid == 0) atomicOr(a.err, kErrCap);
+      if (lane == 0) atomicOr(a.err, kErrCap);
       new_size = cap;
     }
-    for (uint32_t j = tid; j < m; j += kThreads) {  // survivor j: + #tracked with e >= its e
-      const uint64_t ej = ~s_k1[j];
+    // ---- ranks (before anything moves): survivor j -> j + #tracked with e >= its e -------
+    uint32_t rank = ~0u;
+    if (lane < m) {
       uint32_t lo = 0, hi = size;
-      while (lo < hi) {  // the staged energies when the set fits LDS (no dependent global loads)
+      while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
-        if ((lds_set ? s_te[mid] : a.set_e[(base + mid) * Z + z0]) >= ej)
+        if ((lds_set ? s_te[mid] : a.set_e[(base + mid) * Z + z0]) >= se)
           lo = mid + 1;
         else
           hi = mid;
       }
-      s_rank[j] = j + lo;
+      rank = lane + lo;
     }
-    __syncthreads();
-    // ---- tracked items move to later ranks: blocks from the end ----------------------
-    for (int64_t blk = static_cast<int64_t>(size) - 1 - ((static_cast<int64_t>(size) - 1) % kThreads); blk >= 0;
-         blk -= kThreads) {
-      const uint32_t i = static_cast<uint32_t>(blk) + tid;
-      const bool have = i < size;
-      uint32_t r = 0;
-      uint64_t k = 0;
-      uint64_t E[kZ];
-      double P[kZ];
-      if (have) {  // i + #survivors with a strictly higher energy (ties: tracked first)
+    // ---- tracked items move to later ranks, blocks of 64 from the end (a block's loads
+    //      complete before its stores: the stores consume them) ------------------------
+    if (size > 0) {
+      for (int64_t blk = static_cast<int64_t>((size - 1) & ~63u); blk >= 0; blk -= 64) {
+        const uint32_t i = static_cast<uint32_t>(blk) + lane;
+        if (i >= size) continue;
         const uint64_t ei = lds_set ? s_te[i] : a.set_e[(base + i) * Z + z0];
-        uint32_t lo = 0, hi = m;
+        uint32_t lo = 0, hi = m;  // i + #survivors with a strictly higher energy (ties: tracked first)
         while (lo < hi) {
           const uint32_t mid = (lo + hi) >> 1;
-          if (~s_k1[mid] > ei)
+          if (s_se[mid] > ei)
             lo = mid + 1;
           else
             hi = mid;
         }
-        r = i + lo;
-        if (r != i && r < new_size) {  // only the items that move are read
-          k = a.set_key[base + i];
-          for (uint32_t z = 0; z < kZ && z < Z; ++z) {
-            E[z] = a.set_e[(base + i) * Z + z];
-            P[z] = a.set_p[(base + i) * Z + z];
-          }
+        const uint32_t r = i + lo;
+        if (r == i || r >= new_size) continue;
+        const uint64_t k = a.set_key[base + i];
+        uint64_t E[kZ];
+        double P[kZ];
+        for (uint32_t z = 0; z < kZ && z < Z; ++z) {
+          E[z] = a.set_e[(base + i) * Z + z];
+          P[z] = a.set_p[(base + i) * Z + z];
         }
-      }
-      __syncthreads();
-      if (have && r != i && r < new_size) {
         a.set_key[base + r] = k;
         for (uint32_t z = 0; z < kZ && z < Z; ++z) {
           a.set_e[(base + r) * Z + z] = E[z];
           a.set_p[(base + r) * Z + z] = P[z];
         }
       }
-      __syncthreads();
     }
     // ---- survivors take their ranks (frozen copies: Add(prev.Clone())) -------------
-    for (uint32_t j = tid; j < m; j += kThreads) {
-      const uint32_t r = s_rank[j];
-      if (r >= new_size) continue;
-      const uint32_t src = s_ix[j];
-      const uint64_t sl = s_slot[src];
-      a.set_key[base + r] = s_key[src];
+    if (lane < m && rank < new_size) {
+      a.set_key[base + rank] = skey;
       for (uint32_t z = 0; z < Z; ++z) {
-        a.set_e[(base + r) * Z + z] = a.tab_e[sl * a.tab_stride + z];
-        a.set_p[(base + r) * Z + z] = a.tab_p ? a.tab_p[sl * a.tab_stride + z] : proc_power(a.pd, sl, z);
+        a.set_e[(base + rank) * Z + z] = a.tab_e[static_cast<uint64_t>(sslot) * a.tab_stride + z];
+        a.set_p[(base + rank) * Z + z] =
+            a.tab_p ? a.tab_p[static_cast<uint64_t>(sslot) * a.tab_stride + z] : proc_power(a.pd, sslot, z);
       }
     }
     size = new_size;
-    __syncthreads();
+    // the next chunk reads the set this one wrote (minimum, keys, energies): stores complete first
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
   }
-  if (tid == 0) a.size[n] = size;
+  if (lane == 0) a.size[n] = size;
 }
 
 // Items(): the nodes' sets packed node by node (offsets from the host).
@@ -473,11 +386,11 @@ int kacc_tracker_add(kacc_tracker *t, const kacc_slotmap *m, const uint64_t *ter
   a.term_slot = term_slot;
   a.term_count = term_count;
   (void)hipGetLastError();  // clear a stale error of an earlier call
+  const dim3 wgrid((m->n_nodes + kacc::trk::kWaveNodes - 1) / kacc::trk::kWaveNodes);
   if (a.Z <= 4)
-    hipLaunchKernelGGL(kacc::trk::node_add_kernel<4>, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0, st, a);
+    hipLaunchKernelGGL(kacc::trk::node_add_wave_kernel<4>, wgrid, dim3(kacc::trk::kThreads), 0, st, a);
   else
-    hipLaunchKernelGGL(kacc::trk::node_add_kernel<KACC_MAX_ZONES>, dim3(m->n_nodes), dim3(kacc::trk::kThreads), 0,
-                       st, a);
+    hipLaunchKernelGGL(kacc::trk::node_add_wave_kernel<KACC_MAX_ZONES>, wgrid, dim3(kacc::trk::kThreads), 0, st, a);
   KACC_HIP(ctx, hipGetLastError());
   return KACC_OK;
 }

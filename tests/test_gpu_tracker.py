@@ -67,6 +67,7 @@ FLEETS = [
     ("config3-like", [2000] * 16, 4, 0.02, 500),
     ("unlimited", [500, 200, 1500], 2, 0.05, -1),
     ("big-node", [12000, 300, 2500], 4, 0.03, 200),
+    ("five-zones", [700, 300, 1300], 5, 0.05, 100),  # the kernel instance that carries 8 zones
     ("config3-shape-1k-nodes", [2000] * 1000, 4, 0.02, 500),  # 2M rows: the production pipeline's scale per node
 ]
 
