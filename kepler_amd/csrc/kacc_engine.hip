@@ -3124,38 +3124,44 @@ __global__ __launch_bounds__(kBlock) void cluster_partials_kernel(uint32_t ns_bl
 
 
 // Derived powers of elements [first, first + count) ([slot*Z + z]) into out: one lane per
-// element, kPowPerLane elements per lane a block-width apart (every wave store 512
-// contiguous bytes), slot = e / Z by a compile-time Z (a multiply, not a 64-bit
-// division).  Each element's slot ratio and node load together, all of the lane's at
-// once, then the node's guard values (cache hits): two round trips per lane, four
-// elements' bytes in flight behind each.  Per slot: ratio 8 + node 4 in, 8Z out
-// (bench.py scrape_powers).
-constexpr int kPowPerLane = 4;
+// SLOT (round 6), a wave per 64 consecutive slots — the slots' ratio and node words load
+// coalesced (768 B per wave, once per slot instead of once per element), the node's guard
+// values from cache, the lane's Z powers through the wave's LDS so that every store is 64
+// consecutive elements (512 B, non-temporal).  The arithmetic is process.go:124, 142's,
+// one multiply per power.  Per slot: ratio 8 + node 4 in, 8Z out (bench.py scrape_powers).
+constexpr int kPowWaves = kBlock / 64;
 template <int Z>
 __global__ __launch_bounds__(kBlock) void proc_power_kernel(const ProcDerive d, uint64_t first, uint64_t count,
                                                             double *out) {
-  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kBlock * kPowPerLane + threadIdx.x;
-  uint32_t n[kPowPerLane];
-  double r[kPowPerLane];
+  __shared__ double s_p[kPowWaves][64 * Z];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint64_t s_first = first / Z, s_last = (first + count - 1) / Z;  // count > 0
+  const uint64_t S0 = s_first + (static_cast<uint64_t>(blockIdx.x) * kPowWaves + wv) * 64u;
+  if (S0 > s_last) return;  // wave-uniform
+  const uint64_t s = min(S0 + lane, s_last);  // (clamped: the loads stay unconditional)
+  const uint32_t n = d.node[s];
+  const double r = d.ratio[s];
+  double *const sp = s_p[wv];
+  if (n < d.nodes) {
+    const bool busy = d.cpu_delta[n] != 0;
 #pragma unroll
-  for (int u = 0; u < kPowPerLane; ++u) {  // unconditional from a clamped element
-    const uint64_t s = (first + min(i0 + static_cast<uint64_t>(u) * kBlock, count - 1)) / Z;
-    n[u] = d.node[s];
-    r[u] = d.ratio[s];
-  }
-#pragma unroll
-  for (int u = 0; u < kPowPerLane; ++u) {
-    const uint64_t i = i0 + static_cast<uint64_t>(u) * kBlock;
-    if (i >= count) break;
-    const uint64_t e = first + i, s = e / Z;
-    const uint32_t z = static_cast<uint32_t>(e - s * Z);
-    double p = 0.0;
-    if (n[u] < d.nodes) {
-      const uint64_t k = static_cast<uint64_t>(n[u]) * Z + z;
+    for (int z = 0; z < Z; ++z) {
+      const uint64_t k = static_cast<uint64_t>(n) * Z + z;
       const double aP = d.active_power[k];
-      if (d.active_energy[k] != 0 && d.cpu_delta[n[u]] != 0 && aP != 0) p = r[u] * aP;  // process.go:124, 142
+      sp[lane * Z + z] = (d.active_energy[k] != 0 && busy && aP != 0) ? r * aP : 0.0;
     }
-    __builtin_nontemporal_store(p, out + i);
+  } else {
+#pragma unroll
+    for (int z = 0; z < Z; ++z) sp[lane * Z + z] = 0.0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t e0 = S0 * Z, end = first + count;
+#pragma unroll
+  for (int z = 0; z < Z; ++z) {
+    const uint64_t e = e0 + static_cast<uint64_t>(z) * 64u + lane;
+    if (e >= first && e < end) __builtin_nontemporal_store(sp[z * 64 + lane], out + (e - first));
   }
 }
 
@@ -4485,10 +4491,10 @@ int kacc_internal_derived_power(kacc_ctx *ctx, int t, uint64_t first, uint64_t c
   KACC_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const uint32_t Z = ctx->cfg.zones;
-  // kPowPerLane elements per lane, no grid-stride loop (a loop would serialise the lanes'
-  // round trips); count <= 2^31 * 1024 elements for any table the context can hold
-  const uint64_t per_block = static_cast<uint64_t>(kacc::kBlock) * kacc::kPowPerLane;
-  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((count + per_block - 1) / per_block, 0x7fffffffull)));
+  // one lane per slot, kPowWaves x 64 slots per workgroup, no grid-stride loop (a loop would
+  // serialise the lanes' round trips)
+  const uint64_t slots = (first + count - 1) / Z - first / Z + 1, per_block = 64ull * kacc::kPowWaves;
+  const dim3 grid(static_cast<uint32_t>(std::min<uint64_t>((slots + per_block - 1) / per_block, 0x7fffffffull)));
   const kacc::ProcDerive d = kacc_derive(ctx, static_cast<kacc_kind>(kind));
   (void)hipGetLastError();
   switch (Z) {

@@ -28,5 +28,5 @@ for r in $(seq 1 ${REPS:-2}); do
 done
 tools/gpu_steps.sh "${args[@]}" || exit $?
 for f in gpurun_out/$O/*_r*.json; do
-  python -c "import json;d=json.load(open('$f'));r=d['roofline'];K=d['config']['intervals_per_step'];print('$f', 'value %.2fG step/interval %.2f us kern %.2f us totals %s frac %.3f' % (d['value']/1e9, d['ms_per_step']*1e3/K, d['kernel_ms']*1e3, d.get('totals_compute_ms'), r['frac']))"
+  python -c "import json;d=json.load(open('$f'));r=d['roofline'];K=d['config']['intervals_per_step'];print('$f', 'value %.2fG step/interval %.2f us kern %.2f us totals %s frac %.3f scrape %s' % (d['value']/1e9, d['ms_per_step']*1e3/K, d['kernel_ms']*1e3, d.get('totals_compute_ms'), r['frac'], (d.get('scrape_powers') or {}).get('ms')))"
 done
