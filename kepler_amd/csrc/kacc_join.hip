@@ -471,10 +471,58 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   __shared__ uint32_t s_ckn, s_ckfail;
   __shared__ uint32_t s_tot[1], s_flo, s_fhi;
 
-  const uint32_t n = blockIdx.x, tid = threadIdx.x;
-  if (n >= a.n_nodes) return;
-  NodeView v;
-  if (!node_view<true>(a, n, v)) return;
+  const uint32_t tid = threadIdx.x;
+  constexpr int kPer = kLdsBuckets / kThreads;
+  // node n's words, keys and table, loaded into registers (the loads issued, not waited for)
+  struct Pf {
+    bool ok;
+    NodeView v;
+    K key[kRpl];
+    EntT ev[kPer];
+    SlotT sv[kSplit ? kPer : 1];
+  };
+  const auto prefetch = [&](uint32_t n, Pf &p) {
+    p.ok = n < a.n_nodes && node_view<true>(a, n, p.v);
+    if (!p.ok) return;
+    const NodeView &v = p.v;
+    const uint32_t R = v.r1 - v.r0, H = v.H, S = v.S;
+    const uint32_t Hu = kCkSmall ? min(H, max(8u, 4 * ((3 * S + 7) / 8))) : H;
+    const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
+    if (kVec && tid * kRpl + kRpl <= R) {  // the lane's rows as one vector (4-B aligned)
+      __builtin_memcpy(p.key, keys + tid * kRpl, sizeof(p.key));
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRpl; ++j) {
+        const uint32_t r = tid * kRpl + j;
+        p.key[j] = r < R ? keys[r] : T::kEmpty;
+      }
+    }
+    if constexpr (k6) {
+      const uint32_t *gk = reinterpret_cast<const uint32_t *>(a.ent + v.hb);
+      const uint16_t *gs = reinterpret_cast<const uint16_t *>(gk + H);
+      if (tid * kPer < Hu) {
+        __builtin_memcpy(p.ev, __builtin_assume_aligned(gk + tid * kPer, 16), sizeof(p.ev));
+        __builtin_memcpy(p.sv, __builtin_assume_aligned(gs + tid * kPer, 16), sizeof(p.sv));
+      }
+    } else if (H) {  // node-uniform; clamped addresses keep the loads unconditional
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const uint32_t b = tid + j * kThreads, bb = b < H ? b : 0u;
+        if constexpr (kWide) {
+          p.ev[j] = a.ent[v.hb + bb];
+          p.sv[j] = a.slots[v.hb + bb];
+        } else {
+          p.ev[j] = static_cast<EntT>(a.ent[v.hb + bb]);
+        }
+      }
+    }
+  };
+  // the join of node n from the registers prefetch() loaded (round 6: the loads behind one
+  // function and the join behind another — the same work, 3-4 % faster than the inline form,
+  // 50 VGPRs instead of 53: profiles/r06/join/r06v_*.json)
+  const auto join_one = [&](uint32_t n, const Pf &cur) {
+  if (!cur.ok) return;
+  const NodeView v = cur.v;
   const uint32_t R = v.r1 - v.r0, S = v.S, s0 = v.s0, H = v.H, hmask = H - 1;
   const uint32_t W = (S + 31) / 32;
   // kJCuckoo: the buckets in use (Hu <= H) and their 4-bucket groups
@@ -505,7 +553,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     }
     return;
   }
-  const K *__restrict__ keys = static_cast<const K *>(a.keys) + v.r0;
   T G, L;
   if constexpr (kWide) {
     G.k = a.ent + v.hb;
@@ -532,43 +579,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
   };
 
   // ---- 1: table -> LDS, keys -> registers, marks cleared ---------------------------
-  // All loads of the phase are issued before the first LDS store (register
-  // staging): the node pays one memory round trip, not one per bucket.
+  // All loads of the phase were issued before the first LDS store (register staging, in
+  // prefetch): the node pays one memory round trip, not one per bucket.
   // kJ6B: lane tid owns buckets [kPer tid, kPer tid + kPer) — 32 B of keys and
   // 16 B of slots, 16-B aligned (H >= 64 and every node's hb a multiple of 64)
-  constexpr int kPer = kLdsBuckets / kThreads;
   auto bucket_of = [&](int j) -> uint32_t { return k6 ? tid * kPer + j : tid + j * kThreads; };
   K key[kRpl];
   uint32_t res[kRpl];
-  if (kVec && tid * kRpl + kRpl <= R) {  // the lane's rows as one vector (4-B aligned)
-    __builtin_memcpy(key, keys + tid * kRpl, sizeof(key));
-  } else {
 #pragma unroll
-    for (int j = 0; j < kRpl; ++j) {
-      const uint32_t r = tid * kRpl + j;
-      key[j] = r < R ? keys[r] : T::kEmpty;
-    }
-  }
-  EntT ev[kPer];
-  SlotT sv[kSplit ? kPer : 1];
+  for (int j = 0; j < kRpl; ++j) key[j] = cur.key[j];
+  const EntT (&ev)[kPer] = cur.ev;
+  const SlotT (&sv)[kSplit ? kPer : 1] = cur.sv;
   {
-    if constexpr (k6) {
-      if (tid * kPer < Hu) {
-        __builtin_memcpy(ev, __builtin_assume_aligned(G.k + tid * kPer, 16), sizeof(ev));
-        __builtin_memcpy(sv, __builtin_assume_aligned(G.s + tid * kPer, 16), sizeof(sv));
-      }
-    } else if (H) {  // node-uniform; clamped addresses keep the loads unconditional
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        const uint32_t b = tid + j * kThreads, bb = b < H ? b : 0u;
-        if constexpr (kWide) {
-          ev[j] = G.k[bb];
-          sv[j] = G.s[bb];
-        } else {
-          ev[j] = G.e[bb];
-        }
-      }
-    }
     for (uint32_t i = tid; i < W; i += kThreads) {
       s_used[i] = 0u;
       s_seen[i] = 0u;
@@ -1271,6 +1293,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
       a.out_span[2 * n + 1] = none ? 0u : hi;
     }
   }
+  };
+  {
+    if (blockIdx.x >= a.n_nodes) return;
+    Pf cur;
+    prefetch(blockIdx.x, cur);
+    join_one(blockIdx.x, cur);
+  }
 }
 
 // ============================ big nodes (global table) =============================
@@ -1722,7 +1751,6 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
       case kJoinCuckooS: hipLaunchKernelGGL((join_small<K, kJoinCuckooS>), grid, block, 0, st, a); break;
       case kJoinCuckooF: hipLaunchKernelGGL((join_small<K, kJoinCuckooF>), grid, block, 0, st, a); break;
-
       default:
         if constexpr (sizeof(K) == 4)
           hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a);
