@@ -410,7 +410,7 @@ def pipeline_line(args, steps=10, warm=8):
     sm.set_policy(accel.KACC_JOIN_REUSE_TERMINATED)
     tr = accel.Tracker(acc, accel.KACC_KIND_PROC, 500, zone=0, min_energy=10 * 10**6)
     churn = fleet.ProcChurn(layout, churn=0.02)
-    n_iv = warm + 2 * steps  # warm-up, the split pass, the sequence pass
+    n_iv = warm + 3 * steps  # warm-up, the split pass, the sequence pass, the join-only pass
     keys = [torch.from_numpy(churn.next_keys().view(np.int32)).cuda() for _ in range(n_iv)]
     sim = fleet.FleetSim(layout, seed=fleet.SEED)
     statics = to_device(layout.static_arrays())
@@ -465,6 +465,15 @@ def pipeline_line(args, steps=10, warm=8):
     e1.record()
     e1.synchronize()
     seq_ms = e0.elapsed_time(e1) / steps
+    # the join alone, `steps` joins of the continuing churn back to back (one event pair)
+    j0, j1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    j0.record()
+    for k in range(warm + 2 * steps, n_iv):
+        sm.join(P, ivs[k][1]["proc_off"].data_ptr(), keys[k].data_ptr(), 0, d_slot.data_ptr(), tk.data_ptr(),
+                ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
+    j1.record()
+    j1.synchronize()
+    join_seq_ms = j0.elapsed_time(j1) / steps
     acc.sync(stream)
     n_term = int(cnt.sum().item())
     tr.close()
@@ -473,12 +482,14 @@ def pipeline_line(args, steps=10, warm=8):
     return {"ms_per_interval": seq_ms, "proc_attr_per_s": P / (seq_ms * 1e-3),
             "ms_per_interval_split": float(np.mean(tall)),
             "join_ms": float(np.mean(tj)), "tracker_ms": float(np.mean(tt)), "interval_ms": float(np.mean(ti)),
+            "join_ms_back_to_back": join_seq_ms,
             "terminated_last_interval": n_term, "intervals": steps,
             "note": "kacc_slot_join (reuse policy) -> kacc_tracker_add -> kacc_run_interval on one stream, "
                     "keys of fleet.ProcChurn (2 % /proc-shaped churn) resident on the device; ms_per_interval: "
                     "`intervals` intervals back to back with one event pair around them; join_ms / tracker_ms / "
                     "interval_ms and ms_per_interval_split: a pass with events between the kernels (each event "
-                    "packet adds a stream gap)"}
+                    "packet adds a stream gap); join_ms_back_to_back: `intervals` more joins of the same churn "
+                    "back to back, one event pair around them"}
 
 
 def host_path_line(args, steps=10):
