@@ -459,7 +459,7 @@ def pipeline_line(args, steps=10, warm=8):
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for k in range(warm + steps, n_iv):
+    for k in range(warm + steps, warm + 2 * steps):
         for _ in interval(k):
             pass
     e1.record()
