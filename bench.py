@@ -468,7 +468,7 @@ def pipeline_line(args, steps=10, warm=8):
     # the join alone, `steps` joins of the continuing churn back to back (one event pair)
     j0, j1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     j0.record()
-    for k in range(warm + 2 * steps, n_iv):
+    for k in range(warm + 2 * steps, warm + 3 * steps):
         sm.join(P, ivs[k][1]["proc_off"].data_ptr(), keys[k].data_ptr(), 0, d_slot.data_ptr(), tk.data_ptr(),
                 ts.data_ptr(), cnt.data_ptr(), stream, span.data_ptr())
     j1.record()
