@@ -123,6 +123,7 @@ struct kacc_slotmap {
   uint32_t *d_slot_off = nullptr;
   uint64_t *d_hoff = nullptr;
   bool has_big = false;         // some node's table exceeds the LDS size
+  bool uniform = false;         // every node's table has kLdsBuckets buckets: hoff[n] = n kLdsBuckets
   uint32_t policy = 0;          // KACC_JOIN_* bits (kacc_slotmap_set_policy)
   int fmt = 0;                  // PID small-table format, fixed at reset (the join variant
                                 // launched then): 0 8-B buckets, 1 6-B buckets, 2 slot-keyed

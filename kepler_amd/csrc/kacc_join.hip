@@ -60,6 +60,7 @@ struct Args {
   uint32_t stop_after;  // timing ablation (kacc_debug_join_variant): 0 = full join
   uint32_t reuse;       // KACC_JOIN_REUSE_TERMINATED
   uint32_t fmt6;        // PID tables of small nodes are 6-B buckets (join_small's kJ6B)
+  uint32_t uniform;     // every node's table has kLdsBuckets buckets (hoff[n] = n kLdsBuckets)
   const uint32_t *row_off;
   const void *keys;
   const uint32_t *node_status;
@@ -335,6 +336,10 @@ constexpr int kJCkSmall = 32768;
 // rows skips the lookups (R = 2000 leaves waves 6-7 idle there), (c) no occupancy count
 // (a six-step cross-lane sum per wave; only linear probing's rebuild rule reads it)
 constexpr int kJCkFast = 65536;
+// kJUni: on a map whose every node has a kLdsBuckets table (hoff[n] = n kLdsBuckets) the
+// node's table address needs no node word, so its loads issue at the kernel's first
+// instruction, beside the node words' round trip instead of after it
+constexpr int kJUni = 131072;
 
 // bit e: key word e of a group equals k
 __device__ __forceinline__ uint32_t ck_match(const uint4 &g, uint32_t k) {
@@ -482,6 +487,16 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     SlotT sv[kSplit ? kPer : 1];
   };
   const auto prefetch = [&](uint32_t n, Pf &p) {
+    bool early = false;
+    if constexpr (k6 && (V & kJUni) != 0) {
+      if (a.uniform && n < a.n_nodes) {  // the table before the node words (map-uniform)
+        const uint32_t *gk = reinterpret_cast<const uint32_t *>(a.ent + static_cast<uint64_t>(n) * kLdsBuckets);
+        const uint16_t *gs = reinterpret_cast<const uint16_t *>(gk + kLdsBuckets);
+        __builtin_memcpy(p.ev, __builtin_assume_aligned(gk + tid * kPer, 16), sizeof(p.ev));
+        __builtin_memcpy(p.sv, __builtin_assume_aligned(gs + tid * kPer, 16), sizeof(p.sv));
+        early = true;
+      }
+    }
     p.ok = n < a.n_nodes && node_view<true>(a, n, p.v);
     if (!p.ok) return;
     const NodeView &v = p.v;
@@ -500,7 +515,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(sizeof
     if constexpr (k6) {
       const uint32_t *gk = reinterpret_cast<const uint32_t *>(a.ent + v.hb);
       const uint16_t *gs = reinterpret_cast<const uint16_t *>(gk + H);
-      if (tid * kPer < Hu) {
+      if (!early && tid * kPer < Hu) {
         __builtin_memcpy(p.ev, __builtin_assume_aligned(gk + tid * kPer, 16), sizeof(p.ev));
         __builtin_memcpy(p.sv, __builtin_assume_aligned(gs + tid * kPer, 16), sizeof(p.sv));
       }
@@ -1532,9 +1547,10 @@ constexpr int kJoinLean = kJoinGroup | kacc::join::kJLean;
 constexpr int kJoinCuckoo = kJoinLean | kacc::join::kJCuckoo;
 constexpr int kJoinCuckooS = kJoinCuckoo | kacc::join::kJCkSmall;
 constexpr int kJoinCuckooF = kJoinCuckoo | kacc::join::kJCkFast;
+constexpr int kJoinUni = kJoinCuckooF | kacc::join::kJUni;
 
 
-constexpr int kJoinDefault = kJoinCuckooF;  // production: PID tables (the u64-keyed kinds: kJoinLean)
+constexpr int kJoinDefault = kJoinUni;  // production: PID tables (the u64-keyed kinds: kJoinLean)
 // the PID small-table format a variant works on (kacc_slotmap.fmt)
 int variant_fmt(int v) {
   return (v & kacc::join::kJCuckoo) ? ((v & kacc::join::kJCkSmall) ? 4 : (v & kacc::join::kJCkFast) ? 5 : 3)
@@ -1558,6 +1574,7 @@ int launched_variant(int v) {
     case kJoinCuckoo:
     case kJoinCuckooS:
     case kJoinCuckooF:
+    case kJoinUni:
       return v;
     default: return kJoinDefault;
   }
@@ -1584,7 +1601,12 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
     hoff[n + 1] = hoff[n] + node_buckets(S);
   }
   bool has_big = false;
-  for (uint32_t n = 0; n < n_nodes; ++n) has_big |= hoff[n + 1] - hoff[n] > kacc::join::kLdsBuckets;
+  bool uniform = n_nodes > 0;
+  for (uint32_t n = 0; n < n_nodes; ++n) {
+    has_big |= hoff[n + 1] - hoff[n] > kacc::join::kLdsBuckets;
+    uniform &= hoff[n] == static_cast<uint64_t>(n) * kacc::join::kLdsBuckets &&
+               hoff[n + 1] - hoff[n] == kacc::join::kLdsBuckets;
+  }
   if (n_nodes && slot_off[n_nodes] > cap)
     return kacc_fail(ctx, KACC_EINVAL, "slot_off[n] = %u exceeds the kind's slot capacity %llu",
                      slot_off[n_nodes], (unsigned long long)cap);
@@ -1597,6 +1619,7 @@ int kacc_slotmap_create(kacc_ctx *ctx, kacc_kind kind, uint32_t n_nodes, const u
   m->total_slots = n_nodes ? slot_off[n_nodes] : 0;
   m->buckets = hoff[n_nodes];
   m->has_big = has_big;
+  m->uniform = uniform;
   auto bail = [&](hipError_t e) {
     kacc_slotmap_destroy(m);
     return kacc_fail(ctx, e == hipErrorOutOfMemory ? KACC_ENOMEM : KACC_EHIP, "slot map allocation: %s",
@@ -1720,6 +1743,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
   const int var = launched_variant(g_join_variant);
   const int fmt = m->kind == KACC_KIND_PROC ? variant_fmt(var) : 0;
   a.fmt6 = fmt == 1 ? 1u : 0u;
+  a.uniform = m->uniform ? 1u : 0u;
   if (fmt != m->fmt)
     return kacc_fail(ctx, KACC_EINVAL,
                      "slot join: the join variant's table format (%s) differs from the map's "
@@ -1751,6 +1775,7 @@ static int slot_join(kacc_slotmap *m, uint32_t n_rows, const uint32_t *row_off, 
       case kJoinCuckoo: hipLaunchKernelGGL((join_small<K, kJoinCuckoo>), grid, block, 0, st, a); break;
       case kJoinCuckooS: hipLaunchKernelGGL((join_small<K, kJoinCuckooS>), grid, block, 0, st, a); break;
       case kJoinCuckooF: hipLaunchKernelGGL((join_small<K, kJoinCuckooF>), grid, block, 0, st, a); break;
+      case kJoinUni: hipLaunchKernelGGL((join_small<K, kJoinUni>), grid, block, 0, st, a); break;
       default:
         if constexpr (sizeof(K) == 4)
           hipLaunchKernelGGL((join_small<K, kJoinDefault>), grid, block, 0, st, a);

@@ -117,7 +117,7 @@ def test_join_bit_exact(name, sizes, churn, kind, policy):
         assert term == want_term, f"interval {it}"
 
 
-@pytest.fixture(params=[-1, 25087, 57855, 511], ids=["production", "cuckoo-umulhi", "cuckoo-1.5S", "round5-linear"])
+@pytest.fixture(params=[-1, 90623, 57855, 511], ids=["production", "cuckoo-shift", "cuckoo-1.5S", "round5-linear"])
 def join_variant(request):
     """The production join (the cuckoo table), its A/B variant with a table of 1.5 S buckets, and
     round 5's linear-probing kernel (tools/bench_join_variants.py), set for the test's maps
@@ -155,6 +155,36 @@ def test_join_long_churn_bit_exact(churn, policy, join_variant):
         status = None
         if it % 4 == 3 and churn <= 0.1:
             status = np.where(rng.random(len(sizes)) < 0.3, accel.KACC_NODE_READ_ERROR, 0).astype(np.uint32)
+        rc, want, tk, ts, cnt = ora.join(row_off, keys, status)
+        assert rc == 0
+        want_term = ora.terminated(tk, ts, cnt)
+        got, term = gpu.join(row_off, keys, status)
+        if status is not None:
+            keep = np.repeat(status == 0, np.diff(row_off.astype(np.int64)))
+            got, want = got[keep], want[keep]
+        np.testing.assert_array_equal(got, want, err_msg=f"interval {it}")
+        assert term == want_term, f"interval {it}"
+
+
+@pytest.mark.parametrize("policy", [0, accel.KACC_JOIN_REUSE_TERMINATED], ids=["held", "reuse"])
+@pytest.mark.parametrize("churn", [0.02, 0.1])
+def test_join_uniform_map_bit_exact(churn, policy, join_variant):
+    """A map whose every node has a 4096-bucket table (1,100-2,000 rows, 1.3 x rows + 8
+    slots: room for the held policy's terminated slots; the config-3 shape), where the production join loads each node's table before its
+    node words (kJUni); 20 intervals of churn with read errors, bit-exact every interval."""
+    rng = np.random.default_rng(17)
+    sizes = rng.integers(1100, 2001, size=24).tolist()
+    row_off = np.r_[0, np.cumsum(sizes)].astype(np.uint32)
+    slot_off = np.r_[0, np.cumsum([s * 13 // 10 + 8 for s in sizes])].astype(np.uint32)
+    acc = accel.Accel(1, **caps_for(slot_off))
+    gpu = GpuJoin(acc, accel.KACC_KIND_PROC, slot_off, policy)
+    ora = OracleSlotMap(slot_off, policy)
+    sim = fleet.KeyedChurn(row_off, seed=23, churn=churn, kind="proc")
+    for it in range(20):
+        keys = sim.next_keys()
+        status = None
+        if it % 5 == 4:
+            status = np.where(rng.random(len(sizes)) < 0.25, accel.KACC_NODE_READ_ERROR, 0).astype(np.uint32)
         rc, want, tk, ts, cnt = ora.join(row_off, keys, status)
         assert rc == 0
         want_term = ora.terminated(tk, ts, cnt)
