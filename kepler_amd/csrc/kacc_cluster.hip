@@ -166,6 +166,8 @@ struct kacc_cluster {
   std::vector<ncclComm_t> comms;     // per local GPU
   std::vector<hipEvent_t> events;    // per shard
   std::vector<uint64_t *> d_count;   // per local GPU: [1 + nranks] u64 (pod-gather count exchange)
+  std::vector<double *> d_gather;    // per local GPU: the f64 rows of every rank (ordered sums)
+  uint64_t gather_n = 0;             // doubles each d_gather holds
 };
 
 namespace {
@@ -274,9 +276,23 @@ int local_broadcast(kacc_cluster *c, void *const *streams, uint64_t *const *e, u
   return KACC_OK;
 }
 
+// f64 sums in RANK order, ((x_0 + x_1) + x_2) + ...: every rank's row gathered, then
+// added here, so the result does not depend on RCCL's ring / tree order (round 6: the
+// loopback tests' order is the one every run has)
+__global__ void ordered_sum_kernel(const double *__restrict__ rows, uint64_t n, int nranks, double *out) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    double s = rows[i];
+    for (int r = 1; r < nranks; ++r) s = s + rows[static_cast<uint64_t>(r) * n + i];
+    out[i] = s;
+  }
+}
+
 // In-place all-reduces (sum) of the vectors of `reqs` (u64 e [n_e], f64 p
 // [n_p] of each local GPU's first shard) as ONE RCCL group: one launch of
-// RCCL's kernels per step however many vectors cross the GPUs.
+// RCCL's kernels per step however many vectors cross the GPUs.  The u64 sums
+// are exact in any order (all-reduce); the f64 rows are all-gathered and summed
+// in rank order (ordered_sum_kernel) so every run gives the same bits.
 struct ReduceReq {
   uint64_t *const *e;
   uint64_t n_e;
@@ -285,7 +301,21 @@ struct ReduceReq {
 };
 int allreduce(kacc_cluster *c, void *const *streams, const ReduceReq *reqs, int n_reqs) {
   kacc_ctx *c0 = c->shards[0];
+  uint64_t need = 0;  // every request's f64 rows of every rank
+  for (int q = 0; q < n_reqs; ++q) need += reqs[q].n_p * static_cast<uint64_t>(c->nranks);
+  if (need > c->gather_n) {
+    c->d_gather.resize(c->dev_first.size(), nullptr);
+    for (size_t d = 0; d < c->dev_first.size(); ++d) {
+      KACC_HIP(c0, hipSetDevice(c->shards[c->dev_first[d]]->device));
+      KACC_HIP(c0, hipDeviceSynchronize());
+      (void)hipFree(c->d_gather[d]);
+      c->d_gather[d] = nullptr;
+      KACC_HIP(c0, hipMalloc(&c->d_gather[d], 8 * need));
+    }
+    c->gather_n = need;
+  }
   KACC_NCCL(c0, rccl().GroupStart());
+  uint64_t off = 0;
   for (int q = 0; q < n_reqs; ++q) {
     const ReduceReq &rq = reqs[q];
     for (size_t d = 0; d < c->dev_first.size(); ++d) {
@@ -299,15 +329,31 @@ int allreduce(kacc_cluster *c, void *const *streams, const ReduceReq *reqs, int 
         }
       }
       if (rq.n_p) {
-        const ncclResult_t r = rccl().AllReduce(rq.p[f], rq.p[f], rq.n_p, ncclFloat64, ncclSum, c->comms[d], sf);
+        const ncclResult_t r = rccl().AllGather(rq.p[f], c->d_gather[d] + off, rq.n_p, ncclFloat64, c->comms[d], sf);
         if (r != ncclSuccess) {
           (void)rccl().GroupEnd();
-          return nccl_fail(c0, r, "ncclAllReduce(f64)");
+          return nccl_fail(c0, r, "ncclAllGather(f64)");
         }
       }
     }
+    off += rq.n_p * static_cast<uint64_t>(c->nranks);
   }
   KACC_NCCL(c0, rccl().GroupEnd());
+  off = 0;
+  for (int q = 0; q < n_reqs; ++q) {
+    const ReduceReq &rq = reqs[q];
+    if (rq.n_p) {
+      for (size_t d = 0; d < c->dev_first.size(); ++d) {
+        const int f = c->dev_first[d];
+        KACC_HIP(c0, hipSetDevice(c->shards[f]->device));
+        const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((rq.n_p + 255) / 256, 1024));
+        hipLaunchKernelGGL(ordered_sum_kernel, dim3(grid), dim3(256), 0, shard_stream(c, streams, f),
+                           c->d_gather[d] + off, rq.n_p, c->nranks, rq.p[f]);
+        KACC_HIP(c0, hipGetLastError());
+      }
+    }
+    off += rq.n_p * static_cast<uint64_t>(c->nranks);
+  }
   return KACC_OK;
 }
 
@@ -429,6 +475,11 @@ void kacc_cluster_destroy(kacc_cluster *c) {
     if (c->d_count[d]) {
       (void)hipSetDevice(c->shards[c->dev_first[d]]->device);
       (void)hipFree(c->d_count[d]);
+    }
+  for (size_t d = 0; d < c->d_gather.size(); ++d)
+    if (c->d_gather[d]) {
+      (void)hipSetDevice(c->shards[c->dev_first[d]]->device);
+      (void)hipFree(c->d_gather[d]);
     }
   for (size_t s = 0; s < c->events.size(); ++s)
     if (c->events[s]) {
